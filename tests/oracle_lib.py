@@ -1,0 +1,123 @@
+"""ctypes binding of the CPU parity oracle (oracle/liboracle.so).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and the
+cpu_baseline leg of bench.py -- never by the product package.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE_DIR = os.path.join(ROOT, "oracle")
+LIB_PATH = os.path.join(ORACLE_DIR, "build", "liboracle.so")
+
+INFO_FIELDS = [
+    "x", "y", "vx", "vy", "angle", "omega", "rpm", "lateral_force", "slip_deg", "banking",
+    "load_fl", "load_fr", "load_rl", "load_rr", "temp_fl", "temp_fr", "temp_rl", "temp_rr",
+    "wear_fl", "wear_fr", "wear_rl", "wear_rr", "lap_count", "last_lap", "best_lap", "is_timing",
+    "current_lap_time", "lap_distance", "disabled", "cum_impact", "cum_reward", "stuck_duration",
+    "backward", "progress", "sim_time", "impulse", "sleep_time", "awake", "n_contacts", "overflow",
+    "on_track", "n_active_collisions", "info_cum_reward", "speed",
+]
+_lib = None
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", ORACLE_DIR], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = ctypes.CDLL(LIB_PATH)
+        vp, f32p, f64p = ctypes.c_void_p, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_double)
+        L.or_create.restype = vp
+        L.or_create.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.c_int]
+        L.or_destroy.argtypes = [vp]
+        L.or_num_walls.argtypes = [vp]
+        L.or_num_segments.argtypes = [vp]
+        L.or_total_length.argtypes = [vp]
+        L.or_total_length.restype = ctypes.c_double
+        L.or_walls.argtypes = [vp, f64p, f32p]
+        L.or_segments.argtypes = [vp, f64p]
+        L.or_reset.argtypes = [vp, ctypes.c_int]
+        L.or_step.argtypes = [vp, f32p]
+        L.or_outputs.argtypes = [vp, f32p, f32p, ctypes.POINTER(ctypes.c_uint8), ctypes.POINTER(ctypes.c_int32)]
+        L.or_car_info.argtypes = [vp, ctypes.c_int, f64p]
+        L.or_sinf.restype = ctypes.c_float
+        L.or_sinf.argtypes = [ctypes.c_float]
+        L.or_cosf.restype = ctypes.c_float
+        L.or_cosf.argtypes = [ctypes.c_float]
+        L.or_raycast.restype = ctypes.c_float
+        L.or_raycast.argtypes = [vp, ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_float]
+        L.or_set_body.argtypes = [vp, ctypes.c_int] + [ctypes.c_float] * 6
+        _lib = L
+    return _lib
+
+
+def _p(a, t):
+    return a.ctypes.data_as(ctypes.POINTER(t))
+
+
+class OracleEnv:
+    """E envs x C cars of the restated reference CarEnv on the CPU."""
+
+    def __init__(self, track_path, num_envs=1, num_cars=1, reset_on_lap=False):
+        self.L = lib()
+        self.E, self.C = num_envs, num_cars
+        self.h = self.L.or_create(track_path.encode(), num_envs, num_cars, int(reset_on_lap))
+        if not self.h:
+            raise FileNotFoundError(track_path)
+
+    def close(self):
+        if self.h:
+            self.L.or_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.close()
+
+    def walls(self):
+        n = self.L.or_num_walls(self.h)
+        d = np.zeros((n, 4), np.float64)
+        f = np.zeros((n, 12), np.float32)
+        self.L.or_walls(self.h, _p(d, ctypes.c_double), _p(f, ctypes.c_float))
+        return d, f
+
+    def segments(self):
+        n = self.L.or_num_segments(self.h)
+        s = np.zeros((n, 13), np.float64)
+        self.L.or_segments(self.h, _p(s, ctypes.c_double))
+        return s
+
+    def total_length(self):
+        return self.L.or_total_length(self.h)
+
+    def reset(self, env=None):
+        envs = range(self.E) if env is None else [env]
+        for e in envs:
+            self.L.or_reset(self.h, e)
+        return self.outputs()
+
+    def step(self, actions):
+        a = np.ascontiguousarray(actions, dtype=np.float32).reshape(self.E * self.C, 2)
+        self.L.or_step(self.h, _p(a, ctypes.c_float))
+        return self.outputs()
+
+    def outputs(self):
+        obs = np.zeros((self.E, self.C, 38), np.float32)
+        rew = np.zeros((self.E, self.C), np.float32)
+        cf = np.zeros((self.E, self.C), np.uint8)
+        ef = np.zeros((self.E, 3), np.int32)
+        self.L.or_outputs(self.h, _p(obs, ctypes.c_float), _p(rew, ctypes.c_float),
+                          _p(cf, ctypes.c_uint8), _p(ef, ctypes.c_int32))
+        return obs, rew, cf, ef
+
+    def car_info(self, idx):
+        o = np.zeros(len(INFO_FIELDS), np.float64)
+        self.L.or_car_info(self.h, idx, _p(o, ctypes.c_double))
+        return dict(zip(INFO_FIELDS, o.tolist()))

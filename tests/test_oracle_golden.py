@@ -1,0 +1,81 @@
+"""The CPU oracle (oracle/, a C restatement of the reference) against golden
+vectors produced by the reference's OWN Python code (oracle/gen_golden.py):
+
+* track loader + wall builder tables for all 8 tracks, bit-exact;
+* full env traces (obs, rewards, terminated/truncated, termination reason and the
+  info fields callers read) bit-exact, step by step.
+
+The golden env traces run the reference CarEnv on the oracle's Box2D restatement
+(the "hybrid oracle"), so these tests pin every part of the path except the
+Box2D internals (contact solver / TOI / raycast), which are parity-unpinned.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from golden_replay import GOLDEN, TRACKS, first_mismatch, load, scenarios
+from oracle_lib import OracleEnv
+
+TRACK_NAMES = sorted(f[:-6] for f in os.listdir(TRACKS) if f.endswith(".track"))
+
+
+@pytest.fixture(scope="module")
+def track_golden():
+    return np.load(os.path.join(GOLDEN, "tracks.npz"))
+
+
+@pytest.mark.parametrize("name", TRACK_NAMES)
+def test_track_tables_bit_exact(name, track_golden):
+    env = OracleEnv(os.path.join(TRACKS, name + ".track"))
+    d, f = env.walls()
+    ref_walls = track_golden[f"{name}__walls"]
+    assert d.shape[0] == ref_walls.shape[0]
+    assert np.array_equal(d, ref_walls[:, :4])             # centre, angle, half length (float64)
+    assert np.all(ref_walls[:, 4] == 0.5)                   # half thickness
+    assert np.array_equal(env.segments(), track_golden[f"{name}__segments"])
+    assert env.total_length() == float(track_golden[f"{name}__total_length"])
+    keys = track_golden[f"{name}__keys"]
+    kid = f[:, 11].astype(np.int64)
+    _, inv = np.unique(keys, return_inverse=True)
+    # same listener key string <=> same key id
+    assert np.array_equal(inv[:, None] == inv[None, :], kid[:, None] == kid[None, :])
+
+
+INFO_MAP = [  # golden info column -> oracle field
+    (0, "lap_count"), (1, "last_lap"), (2, "best_lap"), (3, "is_timing"), (4, "current_lap_time"),
+    (5, "lap_distance"), (6, "speed"), (7, "on_track"), (8, "disabled"), (9, "info_cum_reward"), (10, "cum_impact"),
+]
+
+
+def replay_oracle(d):
+    C = int(d["C"])
+    env = OracleEnv(os.path.join(TRACKS, str(d["track"])), 1, C, bool(d["reset_on_lap"]))
+    obs0 = env.reset()[0][0]
+    O, R, T, TR, RS, I = [], [], [], [], [], []
+    keep = set(d["obs_steps"].tolist()) if "obs_steps" in d else None
+    for k in range(len(d["actions"])):
+        if d["reset"][k]:
+            o, r, cf, ef = env.reset(0)
+            r = np.zeros_like(r)
+            ef = ef.copy(); ef[0, :2] = 0
+        else:
+            o, r, cf, ef = env.step(d["actions"][k][None])
+        if keep is None or k in keep:
+            O.append(o[0])
+            I.append([[env.car_info(i)[f] for _, f in INFO_MAP] for i in range(C)])
+        R.append(r[0]); T.append(bool(ef[0, 0])); TR.append(bool(ef[0, 1])); RS.append(int(ef[0, 2]))
+    return obs0, np.array(O), np.array(R), np.array(T), np.array(TR), np.array(RS), np.array(I)
+
+
+@pytest.mark.parametrize("name", scenarios())
+def test_env_trace_bit_exact(name):
+    d = load(name)
+    obs0, O, R, T, TR, RS, I = replay_oracle(d)
+    assert np.array_equal(obs0, d["obs0"])
+    assert first_mismatch(O, d["obs"]) == -1, f"obs diverge at step {first_mismatch(O, d['obs'])}"
+    assert first_mismatch(R, d["rewards"]) == -1, f"reward diverge at step {first_mismatch(R, d['rewards'])}"
+    assert np.array_equal(T, d["terminated"]) and np.array_equal(TR, d["truncated"])
+    assert np.array_equal(RS, d["reason"])
+    gi = d["info"][:, :, [c for c, _ in INFO_MAP]]
+    assert first_mismatch(I, gi) == -1, f"info diverge at step {first_mismatch(I, gi)}"
