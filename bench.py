@@ -1,0 +1,149 @@
+"""Benchmark: batched CarEnv.step throughput (car-steps/s = envs x cars x steps / s).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--envs E] [--cars C] [--track daytona]
+    torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU, weak scaling)
+
+Workload (BASELINE.json metric "env-steps/sec (cars x envs), daytona 10-car"): E=8192 envs x C=10
+cars on daytona.track per GPU, synthetic uniform U[-1,1]^2 actions pre-generated in HBM, SB3-style
+auto-reset on done.  A "step" = one fused kernel launch over all E*C cars of a rank.
+Prints ONE JSON line on rank 0 (schema: see DESIGN.md "Measurement").
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+ALGO_BYTES_PER_CAR_STEP = 1221      # 2 x 528 B state + 8 B action + 152 B obs + 4 B reward + 1 B flags
+HBM_PEAK_GBS = 8000.0               # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+
+def cpu_baseline(track, cars, budget_s=12.0):
+    """The CPU oracle (C restatement of the reference path, 1 thread) on a bounded sample of the
+    same workload: 16 envs x C cars, uniform actions, as many steps as fit in ~budget_s."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import numpy as np
+    from oracle_lib import OracleEnv
+    E = 16
+    env = OracleEnv(track, E, cars)
+    env.reset()
+    rng = np.random.default_rng(0)
+    acts = rng.uniform(-1, 1, (64, E, cars, 2)).astype(np.float32)
+    steps, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < budget_s:
+        env.step(acts[steps % 64])
+        steps += 1
+    dt = time.perf_counter() - t0
+    env.close()
+    return {"value": E * cars * steps / dt, "unit": "car-steps/s", "cores": 1, "kind": "port",
+            "sample": f"oracle (C restatement of the reference path incl. Box2D subset), {E} envs x {cars} cars x "
+                      f"{steps} steps on {os.path.basename(track)}, uniform actions, 1 host thread"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--envs", type=int, default=8192)
+    ap.add_argument("--cars", type=int, default=10)
+    ap.add_argument("--track", default="daytona")
+    ap.add_argument("--policy", default="uniform", choices=["uniform", "driver"])
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=12.0)
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+    from nascargymnasium_amd.batched import BatchedCarEnv
+    from nascargymnasium_amd.track import track_path
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    E, C, K, W = args.envs, args.cars, args.steps, args.warmup
+    tpath = track_path(args.track)
+    env = BatchedCarEnv(E, C, tpath, device=dev)
+    env.reset()
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(1234 + rank)
+    if args.policy == "uniform":
+        acts = torch.rand((W + K, E, C, 2), generator=gen, device=dev) * 2 - 1     # resident before timing
+    torch.cuda.synchronize()
+
+    def one_step(i):
+        a = acts[i] if args.policy == "uniform" else env.policy_actions(1, seed=rank, step=i)
+        env.step(a, auto_reset=True)
+
+    for i in range(W):
+        one_step(i)
+    torch.cuda.synchronize()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(K)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(K):
+        if args.policy == "uniform":
+            ev[i][0].record()
+            env.step(acts[W + i], auto_reset=True)
+            ev[i][1].record()
+        else:
+            a = env.policy_actions(1, seed=rank, step=W + i)
+            ev[i][0].record()
+            env.step(a, auto_reset=True)
+            ev[i][1].record()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kern_ms = sum(s.elapsed_time(e) for s, e in ev) / K
+    errs = int(((env.car_flags & 128) != 0).sum().item())
+    if world > 1:
+        t = torch.tensor([elapsed, kern_ms], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, kern_ms = float(t[0]), float(t[1])
+    total_car_steps = world * E * C * K
+    value = total_car_steps / elapsed
+    achieved = E * C * ALGO_BYTES_PER_CAR_STEP / (kern_ms * 1e-3) / 1e9
+    traffic = None
+    tfile = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if os.path.exists(tfile):
+        try:
+            tj = json.load(open(tfile))
+            if tj.get("envs") == E and tj.get("cars") == C and tj.get("track") == os.path.basename(tpath):
+                traffic = tj.get("bytes_per_launch")
+        except Exception:
+            traffic = None
+    out = {
+        "metric": "env-steps/sec (cars x envs), daytona 10-car",
+        "value": value, "unit": "car-steps/s", "n_gpus": world, "steps": K, "warmup": W,
+        "ms_per_step": elapsed / K * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "f32+f64", "data": "synthetic",
+        "config": {"workload": f"{os.path.basename(tpath)[:-6]} {C}-car: {E} envs x {C} cars per GPU, "
+                               f"{'uniform U[-1,1]^2 actions resident in HBM' if args.policy == 'uniform' else 'on-device rule driver'}, auto-reset",
+                   "envs_per_gpu": E, "cars_per_env": C, "track": os.path.basename(tpath), "parallelism": f"dp{world} (env shards, no collective)"},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "kernel": "step_kernel", "kernel_ms": kern_ms,
+                     "algo_bytes_per_car_step": ALGO_BYTES_PER_CAR_STEP},
+        "engine_errors": errs,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(tpath, C, args.cpu_budget)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    env.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

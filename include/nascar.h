@@ -1,0 +1,92 @@
+/*
+ * include/nascar.h -- C ABI of the MI355X-native batched CarEnv (libnascar.so).
+ *
+ * Drop-in boundary for the reference's hot path: the Gymnasium CarEnv
+ * step()/reset() of heihachi78/NascarGymnasium (src/car_env.py:678-803,
+ * :316-535), whose per-car internals -- CarPhysics (src/car_physics.py),
+ * Car/TyreManager/Tyre (src/car.py, src/tyre_manager.py, src/tyre.py),
+ * DistanceSensor (src/distance_sensor.py), LapTimer (src/lap_timer.py) and the
+ * Box2D calls they make through box2d-py SWIG -- run here as one fused HIP
+ * kernel over E envs x C cars.  The Python CarEnv / batched VecEnv in
+ * nascargymnasium_amd/ binds these entry points with ctypes.
+ *
+ * Conventions: every buffer argument of nascar_step/nascar_reset is a
+ * caller-owned DEVICE pointer (e.g. torch tensor .data_ptr()); launches are
+ * asynchronous on the caller's HIP stream (hipStream_t passed as void*).
+ * Return code 0 = ok, negative = error; nascar_last_error() has the text.
+ * No C++ exception crosses the ABI.  A handle is not thread-safe.
+ */
+#ifndef NASCAR_H
+#define NASCAR_H
+#include <stdint.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct NascarHandle NascarHandle;
+
+typedef struct NascarConfig {
+    int32_t num_envs;        /* E */
+    int32_t num_cars;        /* C in [1, 10] (src/constants/car_specs.py:50 MAX_CARS); up to 64 allowed */
+    int32_t reset_on_lap;    /* CarEnv(reset_on_lap=...) (src/car_env.py:84) */
+    int32_t device;          /* HIP device ordinal */
+    double start_x, start_y, start_angle;   /* CarEnv start pose (src/car_env.py:114-115, 235-241) */
+} NascarConfig;
+
+/* CarEnv.__init__ (src/car_env.py:79-219): allocate E*C cars of device state. */
+int nascar_create(const NascarConfig* cfg, NascarHandle** out);
+void nascar_destroy(NascarHandle* h);
+const char* nascar_last_error(void);
+
+/* TrackLoader.load_track + CarPhysics._create_track_walls (src/track_generator.py:305-405,
+ * src/car_physics.py:118-339).  Host arrays:
+ *   segments: nseg x 13 float64 [type, length, sx, sy, ex, ey, width, curve_angle, curve_radius,
+ *             left, start_heading, end_heading, banking]   (type: 0 GRID 1 STARTLINE 2 STRAIGHT 3 FINISHLINE 4 CURVE)
+ *   walls:    nwall x 4 float64 [center_x, center_y, angle, half_length] as passed to Box2D
+ * The float32 Box2D body transforms (glibc sinf/cosf), fat AABBs and listener keys
+ * are derived on the host here.  Returns the track id (>= 0). */
+int nascar_add_track(NascarHandle* h, const double* segments, int32_t nseg, double total_length,
+                     const double* walls, int32_t nwall);
+/* per-env track ids (host array of E ints); envs are grouped per track into workgroups. */
+int nascar_set_env_tracks(NascarHandle* h, const int32_t* env_track);
+
+/* CarEnv.reset (src/car_env.py:316-535) for the envs whose env_mask[e] != 0 (device uint8[E];
+ * NULL = all envs).  Writes obs [E*C*38] float32 of the reset envs. */
+int nascar_reset(NascarHandle* h, const uint8_t* env_mask, float* obs, void* stream);
+
+/* CarEnv.step (src/car_env.py:678-803) for all E envs.
+ *   actions:   continuous: [E*C*2] float32 [throttle_brake, steering] (BaseEnv action space);
+ *              discrete:   [E*C] int32 in {0..4} (BaseEnv._discrete_to_continuous, src/base_env.py:227-252)
+ *   obs:       [E*C*38] float32 (src/car_env.py:935-946 layout)
+ *   reward:    [E*C] float32
+ *   car_flags: [E*C] uint8 (bit0 disabled, bit1 just disabled, bit2 collision impulse > 0, bit3 lap completed,
+ *              bit7 engine overflow/error)
+ *   env_flags: [E] uint8 (bit0 terminated, bit1 truncated, bit3 auto-reset done, bits4-6 termination reason)
+ *   auto_reset != 0: envs that terminate/truncate are reset in the same launch; obs then holds the reset
+ *              observation and terminal_obs (if non-NULL, [E*C*38]) the final one (SB3 VecEnv convention). */
+int nascar_step(NascarHandle* h, const void* actions, int32_t discrete, float* obs, float* reward,
+                uint8_t* car_flags, uint8_t* env_flags, int32_t auto_reset, float* terminal_obs, void* stream);
+
+/* Info builder (src/car_env.py:1160-1227, src/lap_timer.py:354-372): per-car float64 [E*C*N_INFO]
+ * (field order: nascargymnasium_amd/_lib.py INFO_FIELDS) written to a device buffer. */
+int nascar_get_info(NascarHandle* h, double* info, void* stream);
+
+/* Raw state snapshot / restore (checkpointing and state-injection parity tests). */
+int64_t nascar_state_bytes(NascarHandle* h);
+int nascar_get_state(NascarHandle* h, void* dst_device, void* stream);
+int nascar_set_state(NascarHandle* h, const void* src_device, void* stream);
+
+/* Synthetic action sources for benchmarks, generated on the device:
+ *   policy 0: counter-based uniform U[-1,1]^2 (key = seed, car, step)
+ *   policy 1: BaseController._fallback_control (game/control/base_controller.py:39-103) from obs */
+int nascar_policy_actions(NascarHandle* h, int32_t policy, uint64_t seed, int64_t step, const float* obs,
+                          float* actions, void* stream);
+
+/* Test hook: the device re-implementation of glibc sinf/cosf used for b2Rot::Set
+ * (device pointers, n floats).  Parity tests compare it with the host libm. */
+int nascar_debug_sincosf(const float* x, float* s, float* c, int32_t n, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,100 @@
+"""ctypes binding of libnascar.so (the C ABI declared in include/nascar.h).
+
+The product path has exactly one implementation -- the HIP kernels in
+libnascar.so.  There is no CPU fallback: if the library is missing or no HIP
+device is visible, the env constructors raise.
+"""
+import ctypes
+import os
+import subprocess
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libnascar.so")
+CSRC = os.path.join(HERE, "csrc")
+
+INFO_FIELDS = ["x", "y", "vx", "vy", "angle", "omega", "speed", "lap_count", "last_lap_time", "best_lap_time",
+               "is_timing", "current_lap_time", "total_distance_traveled", "has_crossed_startline", "disabled",
+               "cumulative_reward", "cumulative_impact_force", "on_track", "engine_rpm", "simulation_time",
+               "n_contacts", "error"]
+N_INFO = len(INFO_FIELDS)
+OBS_DIM = 38
+
+# car flag bits / env flag bits (csrc/nascar_layout.h)
+CF_DISABLED, CF_JUST_DISABLED, CF_COLLISION, CF_LAP, CF_ERROR = 1, 2, 4, 8, 128
+EF_TERMINATED, EF_TRUNCATED, EF_RESET = 1, 2, 8
+REASONS = {0: None, 1: "all_cars_disabled", 2: "all_active_cars_low_reward (threshold: -250.0)",
+           3: "time_limit", 4: "truncated"}
+
+HIPCC_FLAGS = ["--offload-arch=gfx950", "-O3", "-ffp-contract=off", "-fno-fast-math", "-fPIC", "-shared",
+               "-std=c++17", "-Wno-unused-value", "-Wno-unused-result"]
+
+
+class NascarConfig(ctypes.Structure):
+    _fields_ = [("num_envs", ctypes.c_int32), ("num_cars", ctypes.c_int32), ("reset_on_lap", ctypes.c_int32),
+                ("device", ctypes.c_int32), ("start_x", ctypes.c_double), ("start_y", ctypes.c_double),
+                ("start_angle", ctypes.c_double)]
+
+
+def build(verbose=False):
+    """Compile csrc/nascar_kernels.hip for gfx950 into nascargymnasium_amd/libnascar.so (in-tree)."""
+    src = os.path.join(CSRC, "nascar_kernels.hip")
+    cmd = ["hipcc"] + HIPCC_FLAGS + ["-o", LIB_PATH, src]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError("hipcc failed:\n" + r.stderr[-4000:])
+    if verbose:
+        print(" ".join(cmd))
+    return LIB_PATH
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"{LIB_PATH} is missing: run `python -c 'import __graft_entry__ as g; g.build()'` "
+                           "(there is no CPU fallback for the product path)")
+    L = ctypes.CDLL(LIB_PATH)
+    vp, i32, i64, u64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64
+    d_p = ctypes.POINTER(ctypes.c_double)
+    L.nascar_create.argtypes = [ctypes.POINTER(NascarConfig), ctypes.POINTER(vp)]
+    L.nascar_create.restype = ctypes.c_int
+    L.nascar_destroy.argtypes = [vp]
+    L.nascar_destroy.restype = None
+    L.nascar_last_error.restype = ctypes.c_char_p
+    L.nascar_add_track.argtypes = [vp, d_p, i32, ctypes.c_double, d_p, i32]
+    L.nascar_add_track.restype = ctypes.c_int
+    L.nascar_set_env_tracks.argtypes = [vp, ctypes.POINTER(i32)]
+    L.nascar_set_env_tracks.restype = ctypes.c_int
+    L.nascar_reset.argtypes = [vp, vp, vp, vp]
+    L.nascar_reset.restype = ctypes.c_int
+    L.nascar_step.argtypes = [vp, vp, i32, vp, vp, vp, vp, i32, vp, vp]
+    L.nascar_step.restype = ctypes.c_int
+    L.nascar_get_info.argtypes = [vp, vp, vp]
+    L.nascar_get_info.restype = ctypes.c_int
+    L.nascar_state_bytes.argtypes = [vp]
+    L.nascar_state_bytes.restype = i64
+    L.nascar_get_state.argtypes = [vp, vp, vp]
+    L.nascar_get_state.restype = ctypes.c_int
+    L.nascar_set_state.argtypes = [vp, vp, vp]
+    L.nascar_set_state.restype = ctypes.c_int
+    L.nascar_policy_actions.argtypes = [vp, i32, u64, i64, vp, vp, vp]
+    L.nascar_policy_actions.restype = ctypes.c_int
+    L.nascar_debug_sincosf.argtypes = [vp, vp, vp, i32, vp]
+    L.nascar_debug_sincosf.restype = ctypes.c_int
+    _lib = L
+    return L
+
+
+EXPORTED = ["nascar_create", "nascar_destroy", "nascar_last_error", "nascar_add_track", "nascar_set_env_tracks",
+            "nascar_reset", "nascar_step", "nascar_get_info", "nascar_state_bytes", "nascar_get_state",
+            "nascar_set_state", "nascar_policy_actions", "nascar_debug_sincosf"]
+
+
+def check(rc):
+    if rc < 0:
+        raise RuntimeError("libnascar: " + lib().nascar_last_error().decode())
+    return rc

@@ -1,0 +1,143 @@
+"""BatchedCarEnv: E independent reference CarEnvs x C cars stepped by one fused
+HIP kernel per step (libnascar.so), state resident in HBM.
+
+All buffers are torch tensors on the HIP device; ``step`` launches on torch's
+current stream and returns device tensors (no host sync).  This is the engine
+under both the Gymnasium ``CarEnv`` (E=1, nascargymnasium_amd/car_env.py) and
+the SB3-style ``VecCarEnv`` (nascargymnasium_amd/vec_env.py).
+"""
+import ctypes
+from typing import Optional, Sequence, Union
+
+import numpy as np
+import torch
+
+from . import _lib
+from .track import build_walls, load_track, track_path
+
+
+def _ptr(t: Optional[torch.Tensor]):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+def _stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+class BatchedCarEnv:
+    """E envs x C cars of the reference CarEnv on one GPU.
+
+    track_file: one track (name or path) for all envs, or a sequence of E tracks
+    (per-env track index; envs are grouped per track into workgroups).
+    """
+
+    def __init__(self, num_envs: int, num_cars: int = 1, track_file: Union[str, Sequence[str]] = "daytona",
+                 reset_on_lap: bool = False, device: Union[str, int, torch.device] = "cuda",
+                 start_position=None, start_angle: float = 0.0):
+        if not torch.cuda.is_available():
+            raise RuntimeError("BatchedCarEnv needs a HIP device (torch.cuda.is_available() is False); "
+                               "the product path has no CPU fallback")
+        if num_cars < 1 or num_cars > 64:
+            raise ValueError("num_cars must be in [1, 64]")
+        self.E, self.C, self.N = int(num_envs), int(num_cars), int(num_envs) * int(num_cars)
+        self.device = torch.device(device)
+        if self.device.index is None:
+            self.device = torch.device("cuda", torch.cuda.current_device())
+        self.L = _lib.lib()
+        files = [track_file] * self.E if isinstance(track_file, str) else list(track_file)
+        if len(files) != self.E:
+            raise ValueError("need one track per env")
+        uniq = sorted(set(track_path(f) for f in files))
+        self.tracks = [load_track(p) for p in uniq]
+        first = self.tracks[uniq.index(track_path(files[0]))]
+        sx, sy = start_position if start_position is not None else first.start_position
+        cfg = _lib.NascarConfig(self.E, self.C, int(reset_on_lap), self.device.index, float(sx), float(sy),
+                                float(start_angle))
+        h = ctypes.c_void_p()
+        with torch.cuda.device(self.device):
+            _lib.check(self.L.nascar_create(ctypes.byref(cfg), ctypes.byref(h)))
+        self.h = h
+        for t in self.tracks:
+            seg = np.ascontiguousarray(t.segment_table())
+            walls = np.ascontiguousarray(build_walls(t)[:, :4])
+            dp = ctypes.POINTER(ctypes.c_double)
+            _lib.check(self.L.nascar_add_track(self.h, seg.ctypes.data_as(dp), seg.shape[0], float(t.total_length),
+                                               walls.ctypes.data_as(dp), walls.shape[0]))
+        env_track = np.array([uniq.index(track_path(f)) for f in files], np.int32)
+        _lib.check(self.L.nascar_set_env_tracks(self.h, env_track.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))))
+        self.env_track = env_track
+        dev = self.device
+        self.obs = torch.zeros(self.E, self.C, _lib.OBS_DIM, dtype=torch.float32, device=dev)
+        self.reward = torch.zeros(self.E, self.C, dtype=torch.float32, device=dev)
+        self.car_flags = torch.zeros(self.E, self.C, dtype=torch.uint8, device=dev)
+        self.env_flags = torch.zeros(self.E, dtype=torch.uint8, device=dev)
+        self.terminal_obs = torch.zeros_like(self.obs)
+        self._info = torch.zeros(self.E, self.C, _lib.N_INFO, dtype=torch.float64, device=dev)
+        self._actions = torch.zeros(self.E, self.C, 2, dtype=torch.float32, device=dev)
+
+    # ------------------------------------------------------------------ core API
+    def reset(self, env_mask: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """CarEnv.reset for all envs (or those with env_mask[e] != 0, uint8[E] on device)."""
+        with torch.cuda.device(self.device):
+            m = None if env_mask is None else env_mask.to(self.device, torch.uint8).contiguous()
+            _lib.check(self.L.nascar_reset(self.h, _ptr(m), _ptr(self.obs), _stream()))
+        return self.obs
+
+    def step(self, actions: torch.Tensor, auto_reset: bool = False, terminal_obs: bool = False):
+        """CarEnv.step for all envs.  actions: float32 [E, C, 2] (continuous) or int32 [E, C] (discrete)."""
+        discrete = not actions.is_floating_point()
+        a = actions.to(self.device, torch.int32 if discrete else torch.float32).contiguous()
+        if a.numel() != self.N * (1 if discrete else 2):
+            raise ValueError(f"actions must have {self.N * (1 if discrete else 2)} elements, got {tuple(a.shape)}")
+        with torch.cuda.device(self.device):
+            _lib.check(self.L.nascar_step(self.h, _ptr(a), int(discrete), _ptr(self.obs), _ptr(self.reward),
+                                          _ptr(self.car_flags), _ptr(self.env_flags), int(auto_reset),
+                                          _ptr(self.terminal_obs) if terminal_obs else None, _stream()))
+        terminated = (self.env_flags & _lib.EF_TERMINATED) != 0
+        truncated = (self.env_flags & _lib.EF_TRUNCATED) != 0
+        return self.obs, self.reward, terminated, truncated
+
+    def info_tensor(self) -> torch.Tensor:
+        """per-car info [E, C, N_INFO] float64 (fields: _lib.INFO_FIELDS)."""
+        with torch.cuda.device(self.device):
+            _lib.check(self.L.nascar_get_info(self.h, _ptr(self._info), _stream()))
+        return self._info
+
+    def termination_reason(self) -> torch.Tensor:
+        return (self.env_flags >> 4) & 7
+
+    def policy_actions(self, policy: int, seed: int = 0, step: int = 0, obs: Optional[torch.Tensor] = None):
+        """device-generated synthetic actions: 0 uniform U[-1,1]^2, 1 BaseController fallback driver."""
+        o = self.obs if obs is None else obs
+        with torch.cuda.device(self.device):
+            _lib.check(self.L.nascar_policy_actions(self.h, int(policy), int(seed), int(step), _ptr(o),
+                                                    _ptr(self._actions), _stream()))
+        return self._actions
+
+    # ------------------------------------------------------------------ checkpointing
+    def state_bytes(self) -> int:
+        return int(self.L.nascar_state_bytes(self.h))
+
+    def get_state(self) -> torch.Tensor:
+        buf = torch.empty(self.state_bytes(), dtype=torch.uint8, device=self.device)
+        with torch.cuda.device(self.device):
+            _lib.check(self.L.nascar_get_state(self.h, _ptr(buf), _stream()))
+        return buf
+
+    def set_state(self, buf: torch.Tensor):
+        if buf.numel() != self.state_bytes():
+            raise ValueError("state blob size mismatch")
+        with torch.cuda.device(self.device):
+            _lib.check(self.L.nascar_set_state(self.h, _ptr(buf.to(self.device).contiguous()), _stream()))
+
+    def close(self):
+        if getattr(self, "h", None):
+            torch.cuda.synchronize(self.device)
+            self.L.nascar_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -1,0 +1,1045 @@
+// nascar_device.h -- per-car device code of the fused CarEnv step (gfx950).
+//
+// One lane owns one car.  Everything the reference does per car-step
+// (src/car_env.py:_run_single_physics_step -> CarPhysics.step -> Car.update_physics
+// -> b2World::Step -> LapTimer.update, then obs / reward) is restated here on
+// float32 (Box2D) / float64 (Python) values with the reference's operation order,
+// so results match the reference bit for bit (DESIGN.md "Parity").
+//
+// Box2D 2.3 (box2d-py 2.3.8, reference requirements.txt:4) is a third-party
+// dependency; the subset restated is: b2World::Step/Solve/SolveTOI,
+// b2ContactSolver, b2CollidePolygons, b2TimeOfImpact/b2Distance, fat-AABB proxy
+// pairing and b2PolygonShape::RayCast for one dynamic box vs static boxes.
+#pragma once
+#include "nascar_math.h"
+#include "nascar_layout.h"
+
+#pragma clang fp contract(off)
+
+namespace nascar {
+
+// ---------------------------------------------------------------- settings
+#define B2_PI 3.14159265359f
+#define LINEAR_SLOP 0.005f
+#define POLY_RADIUS (2.0f * LINEAR_SLOP)
+#define AABB_EXT 0.1f
+#define AABB_MULT 2.0f
+#define MAX_TRANSLATION 2.0f
+#define MAX_ROTATION (0.5f * B2_PI)
+#define BAUMGARTE 0.2f
+#define TOI_BAUMGARTE 0.75f
+#define MAX_LINEAR_CORRECTION 0.2f
+#define VELOCITY_THRESHOLD 1.0f
+#define TIME_TO_SLEEP 0.5f
+#define LINEAR_SLEEP_TOL 0.01f
+#define ANGULAR_SLEEP_TOL (2.0f / 180.0f * B2_PI)
+#define MAX_SUBSTEPS 8
+#define MAX_TOI_CONTACTS 32
+#define FLT_EPS 1.1920928955078125e-07f
+#define FLT_BIG 3.402823466e+38f
+
+// car fixture (src/car.py:217-239)
+#define CAR_HX ((float)(5.042 / 2.0))
+#define CAR_HY ((float)(1.996 / 2.0))
+#define CAR_INV_MASS (1.0f / 1500.0f)
+#define CAR_I_F ((float)(1500.0 * (5.042 * 5.042 + 1.996 * 1.996) * 0.5 / 12.0))
+#define CAR_INV_I (1.0f / CAR_I_F)
+#define MIX_RESTITUTION 0.25f
+
+// reference constants (src/constants/*.py), same double expressions
+#define CAR_MASS 1500.0
+#define GRAVITY_MS2 9.81
+#define CAR_WHEELBASE 2.794
+#define CAR_MAX_TORQUE 820.0
+#define CAR_MAX_POWER (670.0 * 745.7)
+#define CAR_MAX_SPEED_MS (200.0 * 0.44704)
+#define DRAG_CONSTANT (0.5 * 1.225 * 0.38 * 2.5)
+#define ROLLING_RESISTANCE_FORCE (0.015 * CAR_MASS * GRAVITY_MS2)
+#define MAX_TYRE_LOAD (CAR_MASS * GRAVITY_MS2 * 2.0)
+#define STATIC_LOAD_PER_TYRE (CAR_MASS * GRAVITY_MS2 / 4.0)
+#define PI_D 3.141592653589793
+#define RAD_PER_DEG (PI_D / 180.0)
+#define DEG_PER_RAD (180.0 / PI_D)
+
+// ------------------------------------------------------------------ vectors
+struct V2 { float x, y; };
+struct Rot { float s, c; };
+struct Xf { V2 p; Rot q; };
+struct Aabb { V2 lo, hi; };
+
+__device__ __forceinline__ V2 V(float x, float y) { V2 r; r.x = x; r.y = y; return r; }
+__device__ __forceinline__ V2 vadd(V2 a, V2 b) { return V(a.x + b.x, a.y + b.y); }
+__device__ __forceinline__ V2 vsub(V2 a, V2 b) { return V(a.x - b.x, a.y - b.y); }
+__device__ __forceinline__ V2 vmul(float s, V2 a) { return V(s * a.x, s * a.y); }
+__device__ __forceinline__ V2 vneg(V2 a) { return V(-a.x, -a.y); }
+__device__ __forceinline__ float vdot(V2 a, V2 b) { return a.x * b.x + a.y * b.y; }
+__device__ __forceinline__ float vcross(V2 a, V2 b) { return a.x * b.y - a.y * b.x; }
+__device__ __forceinline__ V2 vcross_vs(V2 a, float s) { return V(s * a.y, -s * a.x); }
+__device__ __forceinline__ V2 vcross_sv(float s, V2 a) { return V(-s * a.y, s * a.x); }
+__device__ __forceinline__ float vlen(V2 a) { return __fsqrt_rn(a.x * a.x + a.y * a.y); }
+__device__ __forceinline__ float vnormalize(V2* a) {
+  float length = vlen(*a);
+  if (length < FLT_EPS) return 0.0f;
+  float inv = __fdiv_rn(1.0f, length);
+  a->x *= inv; a->y *= inv;
+  return length;
+}
+__device__ __forceinline__ V2 rmul(Rot q, V2 v) { return V(q.c * v.x - q.s * v.y, q.s * v.x + q.c * v.y); }
+__device__ __forceinline__ V2 rmulT(Rot q, V2 v) { return V(q.c * v.x + q.s * v.y, -q.s * v.x + q.c * v.y); }
+__device__ __forceinline__ V2 xmul(Xf T, V2 v) {
+  return V((T.q.c * v.x - T.q.s * v.y) + T.p.x, (T.q.s * v.x + T.q.c * v.y) + T.p.y);
+}
+__device__ __forceinline__ V2 xmulT(Xf T, V2 v) {
+  float px = v.x - T.p.x, py = v.y - T.p.y;
+  return V(T.q.c * px + T.q.s * py, -T.q.s * px + T.q.c * py);
+}
+__device__ __forceinline__ Xf xmulT_xx(Xf A, Xf B) {
+  Xf C;
+  C.q.s = A.q.c * B.q.s - A.q.s * B.q.c;
+  C.q.c = A.q.c * B.q.c + A.q.s * B.q.s;
+  C.p = rmulT(A.q, vsub(B.p, A.p));
+  return C;
+}
+__device__ __forceinline__ float fminb(float a, float b) { return a < b ? a : b; }
+__device__ __forceinline__ float fmaxb(float a, float b) { return a > b ? a : b; }
+__device__ __forceinline__ float fclamp(float a, float lo, float hi) { return fmaxb(lo, fminb(a, hi)); }
+__device__ __forceinline__ V2 vmin(V2 a, V2 b) { return V(fminb(a.x, b.x), fminb(a.y, b.y)); }
+__device__ __forceinline__ V2 vmax(V2 a, V2 b) { return V(fmaxb(a.x, b.x), fmaxb(a.y, b.y)); }
+__device__ __forceinline__ Rot rot_set(float a) { Rot q; q.s = dev_sinf(a); q.c = dev_cosf(a); return q; }
+__device__ __forceinline__ V2 zero2() { return V(0.0f, 0.0f); }
+
+// ------------------------------------------------------------------ polygons
+struct Poly { V2 v[4]; V2 n[4]; float radius; };
+__device__ __forceinline__ void make_box(Poly* p, float hx, float hy) {
+  p->radius = POLY_RADIUS;
+  p->v[0] = V(-hx, -hy); p->v[1] = V(hx, -hy); p->v[2] = V(hx, hy); p->v[3] = V(-hx, hy);
+  p->n[0] = V(0.0f, -1.0f); p->n[1] = V(1.0f, 0.0f); p->n[2] = V(0.0f, 1.0f); p->n[3] = V(-1.0f, 0.0f);
+}
+__device__ __forceinline__ Aabb poly_aabb(const Poly* p, Xf xf) {
+  V2 lower = xmul(xf, p->v[0]), upper = lower;
+#pragma unroll
+  for (int i = 1; i < 4; ++i) { V2 v = xmul(xf, p->v[i]); lower = vmin(lower, v); upper = vmax(upper, v); }
+  V2 r = V(p->radius, p->radius);
+  Aabb a; a.lo = vsub(lower, r); a.hi = vadd(upper, r);
+  return a;
+}
+__device__ __forceinline__ bool overlap(Aabb a, Aabb b) {
+  V2 d1 = vsub(b.lo, a.hi), d2 = vsub(a.lo, b.hi);
+  if (d1.x > 0.0f || d1.y > 0.0f) return false;
+  if (d2.x > 0.0f || d2.y > 0.0f) return false;
+  return true;
+}
+__device__ __forceinline__ bool contains(Aabb a, Aabb b) {
+  bool r = true;
+  r = r && a.lo.x <= b.lo.x; r = r && a.lo.y <= b.lo.y;
+  r = r && b.hi.x <= a.hi.x; r = r && b.hi.y <= a.hi.y;
+  return r;
+}
+
+// wall table in LDS (built on the host from the reference wall builder)
+struct LWall {
+  float px, py, qs, qc;   // b2Body transform
+  float hx, hy, ang, rad; // half extents, angle, bounding radius (+ culling margin)
+  float flx, fly, fhx, fhy;  // broadphase fat AABB
+  int key;                // listener key id (src/car_physics.py:747)
+  int pad0, pad1, pad2;
+};
+__device__ __forceinline__ Xf wall_xf(const LWall& w) { Xf t; t.p = V(w.px, w.py); t.q.s = w.qs; t.q.c = w.qc; return t; }
+__device__ __forceinline__ Aabb wall_fat(const LWall& w) { Aabb a; a.lo = V(w.flx, w.fly); a.hi = V(w.fhx, w.fhy); return a; }
+
+// ------------------------------------------------------------------ per-car register state
+struct Car {
+  // b2Body
+  V2 c; float a; V2 v; float w; Xf xf; float sleep; int awake;
+  V2 force; float torque; V2 c0; float a0; float alpha0;
+  Aabb fat; int moved; float invdt0;
+  int nct, overflow;
+  // Car / TyreManager (float64 like the reference's Python)
+  double thr_in, brk_in, str_in, thr, brk, steer;
+  double rpm, pvx, pvy, lfm, slip, bank;
+  double load[4], temp[4], wear[4], fric[4];
+  int acc_len, acc_head;
+  // CarCollisionListener
+  int imp_present, nact; double imp;
+  // LapTimer
+  int lt_timing, lt_has_last, lt_has_best, lt_crossed, lt_has_pos, lt_laps;
+  double lt_start, lt_cur, lt_last, lt_best, lt_px, lt_py, lt_dist;
+  // CarEnv bookkeeping
+  int disabled, just_disabled, has_stuck_start, first_step, prev_laps;
+  double cum_impact, stuck_dur, stuck_sx, stuck_sy, prev_px, prev_py, prog_hist, back, prev_back, imp_at_obs;
+  float cum_reward, cum_reward_info;
+  // per-car global views (AoS lists)
+  DContact* ct;       // [MAXC]
+  int* act_key;       // [MAXC]
+  float* act_n;       // [MAXC][2]
+  double* acc;        // [20] ring (long, lat)
+};
+
+// ------------------------------------------------------------------ listener (src/car_physics.py:693-864)
+__device__ inline void lis_begin(Car& c, int key, V2 n) {
+  int found = -1;
+  for (int i = 0; i < c.nact; ++i) if (c.act_key[i] == key) { found = i; break; }
+  if (found >= 0) { c.act_n[found * 2] = n.x; c.act_n[found * 2 + 1] = n.y; }
+  else if (c.nact < MAXC) { c.act_key[c.nact] = key; c.act_n[c.nact * 2] = n.x; c.act_n[c.nact * 2 + 1] = n.y; c.nact++; }
+  if (!c.imp_present) { c.imp_present = 1; c.imp = 0.0; }
+}
+__device__ inline void lis_end(Car& c, int key) {
+  for (int i = 0; i < c.nact; ++i) if (c.act_key[i] == key) {
+    for (int j = i; j < c.nact - 1; ++j) { c.act_key[j] = c.act_key[j + 1]; c.act_n[j * 2] = c.act_n[j * 2 + 2]; c.act_n[j * 2 + 1] = c.act_n[j * 2 + 3]; }
+    c.nact--; break;
+  }
+  if (c.nact == 0) { c.imp_present = 1; c.imp = 0.0; }
+}
+__device__ inline void lis_post(Car& c, int count, float n0, float n1) {
+  if (count <= 0) return;
+  double total = 0.0;
+  total += (double)n0;
+  if (count > 1) total += (double)n1;
+  if (c.imp_present) c.imp = pymax(c.imp, total);
+}
+
+// ------------------------------------------------------------------ body helpers
+__device__ __forceinline__ void set_awake(Car& c) { if (!c.awake) { c.awake = 1; c.sleep = 0.0f; } }
+__device__ __forceinline__ void sync_transform(Car& c) { c.xf.q = rot_set(c.a); c.xf.p = vsub(c.c, rmul(c.xf.q, zero2())); }
+__device__ __forceinline__ void apply_force(Car& c, V2 f, V2 point) {
+  set_awake(c); c.force = vadd(c.force, f); c.torque += vcross(vsub(point, c.c), f);
+}
+__device__ __forceinline__ void apply_force_center(Car& c, V2 f) { set_awake(c); c.force = vadd(c.force, f); }
+__device__ __forceinline__ void apply_torque(Car& c, float t) { set_awake(c); c.torque += t; }
+
+__device__ __forceinline__ void move_proxy(Car& c, Xf xf1, Xf xf2) {
+  Poly cp; make_box(&cp, CAR_HX, CAR_HY);
+  Aabb a1 = poly_aabb(&cp, xf1), a2 = poly_aabb(&cp, xf2), aabb;
+  aabb.lo = vmin(a1.lo, a2.lo); aabb.hi = vmax(a1.hi, a2.hi);
+  V2 disp = vsub(xf2.p, xf1.p);
+  if (contains(c.fat, aabb)) return;
+  Aabb b = aabb; V2 r = V(AABB_EXT, AABB_EXT);
+  b.lo = vsub(b.lo, r); b.hi = vadd(b.hi, r);
+  V2 d = vmul(AABB_MULT, disp);
+  if (d.x < 0.0f) b.lo.x += d.x; else b.hi.x += d.x;
+  if (d.y < 0.0f) b.lo.y += d.y; else b.hi.y += d.y;
+  c.fat = b; c.moved = 1;
+}
+__device__ __forceinline__ void sync_fixtures(Car& c) {
+  Xf xf1; xf1.q = rot_set(c.a0); xf1.p = vsub(c.c0, rmul(xf1.q, zero2()));
+  move_proxy(c, xf1, c.xf);
+}
+
+// b2BroadPhase::UpdatePairs + b2ContactManager::AddPair (ascending wall proxy id, prepend)
+__device__ inline void find_new_contacts(Car& c, const LWall* W, int nw) {
+  if (!c.moved) return;
+  c.moved = 0;
+  for (int j = 0; j < nw; ++j) {
+    const LWall& wl = W[j];
+    if (!overlap(c.fat, wall_fat(wl))) continue;
+    bool exists = false;
+    for (int i = 0; i < c.nct; ++i) if (c.ct[i].wall == j) { exists = true; break; }
+    if (exists) continue;
+    if (c.nct >= MAXC) { c.overflow = 1; continue; }
+    for (int i = c.nct; i > 0; --i) c.ct[i] = c.ct[i - 1];
+    DContact z;
+    z.wall = j; z.flags = CT_ENABLED; z.mtype = 0; z.pointCount = 0;
+    z.lnx = z.lny = z.lpx = z.lpy = 0.0f;
+    for (int q = 0; q < 2; ++q) { z.pt[q].lx = z.pt[q].ly = z.pt[q].ni = z.pt[q].ti = 0.0f; z.pt[q].id = 0u; }
+    z.toi = 1.0f; z.toiCount = 0;
+    c.ct[0] = z;
+    c.nct++;
+    set_awake(c);
+  }
+}
+__device__ inline void remove_contact(Car& c, int i) {
+  for (int j = i; j < c.nct - 1; ++j) c.ct[j] = c.ct[j + 1];
+  c.nct--;
+}
+
+// ------------------------------------------------------------------ b2CollidePolygons
+struct Clip { V2 v; uint32_t id; };
+__device__ __forceinline__ uint32_t cf_key(int ia, int ib, int ta, int tb) {
+  return (uint32_t)(ia & 255) | ((uint32_t)(ib & 255) << 8) | ((uint32_t)(ta & 255) << 16) | ((uint32_t)(tb & 255) << 24);
+}
+__device__ inline float find_max_separation(int* edgeIndex, const Poly* p1, Xf xf1, const Poly* p2, Xf xf2) {
+  Xf xf = xmulT_xx(xf2, xf1);
+  int best = 0; float maxSep = -FLT_BIG;
+  for (int i = 0; i < 4; ++i) {
+    V2 n = rmul(xf.q, p1->n[i]);
+    V2 v1 = xmul(xf, p1->v[i]);
+    float si = FLT_BIG;
+    for (int j = 0; j < 4; ++j) { float sij = vdot(n, vsub(p2->v[j], v1)); if (sij < si) si = sij; }
+    if (si > maxSep) { maxSep = si; best = i; }
+  }
+  *edgeIndex = best;
+  return maxSep;
+}
+__device__ inline void find_incident_edge(Clip c[2], const Poly* p1, Xf xf1, int edge1, const Poly* p2, Xf xf2) {
+  V2 normal1 = rmulT(xf2.q, rmul(xf1.q, p1->n[edge1]));
+  int index = 0; float minDot = FLT_BIG;
+  for (int i = 0; i < 4; ++i) { float d = vdot(normal1, p2->n[i]); if (d < minDot) { minDot = d; index = i; } }
+  int i1 = index, i2 = i1 + 1 < 4 ? i1 + 1 : 0;
+  c[0].v = xmul(xf2, p2->v[i1]); c[0].id = cf_key(edge1, i1, 1, 0);
+  c[1].v = xmul(xf2, p2->v[i2]); c[1].id = cf_key(edge1, i2, 1, 0);
+}
+__device__ inline int clip_segment(Clip vOut[2], const Clip vIn[2], V2 normal, float offset, int vertexIndexA) {
+  int numOut = 0;
+  float d0 = vdot(normal, vIn[0].v) - offset;
+  float d1 = vdot(normal, vIn[1].v) - offset;
+  if (d0 <= 0.0f) vOut[numOut++] = vIn[0];
+  if (d1 <= 0.0f) vOut[numOut++] = vIn[1];
+  if (d0 * d1 < 0.0f) {
+    float interp = __fdiv_rn(d0, d0 - d1);
+    vOut[numOut].v = vadd(vIn[0].v, vmul(interp, vsub(vIn[1].v, vIn[0].v)));
+    vOut[numOut].id = cf_key(vertexIndexA, (int)((vIn[0].id >> 8) & 255), 0, 1);
+    ++numOut;
+  }
+  return numOut;
+}
+// writes manifold into ct (type, localNormal, localPoint, pointCount, points' localPoint/id; impulses zeroed)
+__device__ inline void collide_polygons(DContact& m, const Poly* pA, Xf xfA, const Poly* pB, Xf xfB) {
+  m.pointCount = 0;
+  float totalRadius = pA->radius + pB->radius;
+  int edgeA = 0; float sepA = find_max_separation(&edgeA, pA, xfA, pB, xfB);
+  if (sepA > totalRadius) return;
+  int edgeB = 0; float sepB = find_max_separation(&edgeB, pB, xfB, pA, xfA);
+  if (sepB > totalRadius) return;
+  const Poly *poly1, *poly2; Xf xf1, xf2; int edge1; int flip;
+  const float k_tol = 0.1f * LINEAR_SLOP;
+  if (sepB > sepA + k_tol) { poly1 = pB; poly2 = pA; xf1 = xfB; xf2 = xfA; edge1 = edgeB; m.mtype = 2; flip = 1; }
+  else { poly1 = pA; poly2 = pB; xf1 = xfA; xf2 = xfB; edge1 = edgeA; m.mtype = 1; flip = 0; }
+  Clip incident[2];
+  find_incident_edge(incident, poly1, xf1, edge1, poly2, xf2);
+  int iv1 = edge1, iv2 = edge1 + 1 < 4 ? edge1 + 1 : 0;
+  V2 v11 = poly1->v[iv1], v12 = poly1->v[iv2];
+  V2 localTangent = vsub(v12, v11);
+  vnormalize(&localTangent);
+  V2 localNormal = vcross_vs(localTangent, 1.0f);
+  V2 planePoint = vmul(0.5f, vadd(v11, v12));
+  V2 tangent = rmul(xf1.q, localTangent);
+  V2 normal = vcross_vs(tangent, 1.0f);
+  v11 = xmul(xf1, v11); v12 = xmul(xf1, v12);
+  float frontOffset = vdot(normal, v11);
+  float sideOffset1 = -vdot(tangent, v11) + totalRadius;
+  float sideOffset2 = vdot(tangent, v12) + totalRadius;
+  Clip cp1[2], cp2[2];
+  int np = clip_segment(cp1, incident, vneg(tangent), sideOffset1, iv1);
+  if (np < 2) return;
+  np = clip_segment(cp2, cp1, tangent, sideOffset2, iv2);
+  if (np < 2) return;
+  m.lnx = localNormal.x; m.lny = localNormal.y; m.lpx = planePoint.x; m.lpy = planePoint.y;
+  int pc = 0;
+  for (int i = 0; i < 2; ++i) {
+    float separation = vdot(normal, cp2[i].v) - frontOffset;
+    if (separation <= totalRadius) {
+      V2 lp = xmulT(xf2, cp2[i].v);
+      uint32_t id = cp2[i].id;
+      if (flip) {
+        uint32_t ia = id & 255, ib = (id >> 8) & 255, ta = (id >> 16) & 255, tb = (id >> 24) & 255;
+        id = cf_key((int)ib, (int)ia, (int)tb, (int)ta);
+      }
+      m.pt[pc].lx = lp.x; m.pt[pc].ly = lp.y; m.pt[pc].id = id; m.pt[pc].ni = 0.0f; m.pt[pc].ti = 0.0f;
+      ++pc;
+    }
+  }
+  m.pointCount = pc;
+}
+
+// b2WorldManifold::Initialize
+__device__ inline void world_manifold(const DContact& m, Xf xfA, Xf xfB, V2* normal, V2 pts[2]) {
+  const float rA = POLY_RADIUS, rB = POLY_RADIUS;
+  if (m.pointCount == 0) return;
+  V2 ln = V(m.lnx, m.lny), lp = V(m.lpx, m.lpy);
+  if (m.mtype == 1) {
+    V2 n = rmul(xfA.q, ln), planePoint = xmul(xfA, lp);
+    for (int i = 0; i < m.pointCount; ++i) {
+      V2 clipPoint = xmul(xfB, V(m.pt[i].lx, m.pt[i].ly));
+      V2 cA = vadd(clipPoint, vmul(rA - vdot(vsub(clipPoint, planePoint), n), n));
+      V2 cB = vsub(clipPoint, vmul(rB, n));
+      pts[i] = vmul(0.5f, vadd(cA, cB));
+    }
+    *normal = n;
+  } else {
+    V2 n = rmul(xfB.q, ln), planePoint = xmul(xfB, lp);
+    for (int i = 0; i < m.pointCount; ++i) {
+      V2 clipPoint = xmul(xfA, V(m.pt[i].lx, m.pt[i].ly));
+      V2 cB = vadd(clipPoint, vmul(rB - vdot(vsub(clipPoint, planePoint), n), n));
+      V2 cA = vsub(clipPoint, vmul(rA, n));
+      pts[i] = vmul(0.5f, vadd(cA, cB));
+    }
+    *normal = vneg(n);
+  }
+}
+
+// b2Contact::Update
+__device__ inline void contact_update(Car& c, int ci, const LWall* W) {
+  DContact& ct = c.ct[ci];
+  DContact old = ct;
+  ct.flags |= CT_ENABLED;
+  bool was = (ct.flags & CT_TOUCH) != 0;
+  Poly pa, pb; make_box(&pa, CAR_HX, CAR_HY);
+  const LWall& wl = W[ct.wall];
+  make_box(&pb, wl.hx, wl.hy);
+  Xf xfB = wall_xf(wl);
+  collide_polygons(ct, &pa, c.xf, &pb, xfB);
+  bool touching = ct.pointCount > 0;
+  for (int i = 0; i < ct.pointCount; ++i) {
+    ct.pt[i].ni = 0.0f; ct.pt[i].ti = 0.0f;
+    for (int j = 0; j < old.pointCount; ++j) {
+      if (old.pt[j].id == ct.pt[i].id) { ct.pt[i].ni = old.pt[j].ni; ct.pt[i].ti = old.pt[j].ti; break; }
+    }
+  }
+  if (touching != was) set_awake(c);
+  if (touching) ct.flags |= CT_TOUCH; else ct.flags &= ~CT_TOUCH;
+  if (!was && touching) {
+    V2 n = zero2(), pts[2];
+    world_manifold(ct, c.xf, xfB, &n, pts);
+    lis_begin(c, wl.key, n);
+  }
+  if (was && !touching) lis_end(c, wl.key);
+}
+
+// b2ContactManager::Collide
+__device__ inline void collide(Car& c, const LWall* W) {
+  int i = 0;
+  while (i < c.nct) {
+    if (!c.awake) { ++i; continue; }
+    const int wall = c.ct[i].wall;
+    if (!overlap(c.fat, wall_fat(W[wall]))) {
+      bool touching = (c.ct[i].flags & CT_TOUCH) != 0;
+      remove_contact(c, i);
+      if (touching) lis_end(c, W[wall].key);
+      continue;
+    }
+    contact_update(c, i, W);
+    ++i;
+  }
+}
+
+// ------------------------------------------------------------------ b2ContactSolver
+struct VCP { V2 rA, rB; float ni, ti, nm, tm, vb; };
+struct VC {
+  VCP p[2]; V2 normal; float nm[4]; float K[4]; int pointCount;
+  V2 cB; float aB; V2 vB; float wB;
+  V2 ln, lp, lps[2]; int pcount, type, ci;
+};
+struct BodyState { V2 c; float a; V2 v; float w; };
+
+__device__ inline void cs_init(VC* vc, int n, const Car& c, const int* cidx, const LWall* W, bool warm, float dtRatio) {
+  for (int i = 0; i < n; ++i) {
+    const DContact& ct = c.ct[cidx[i]];
+    VC& v = vc[i];
+    v.ci = cidx[i];
+    v.pointCount = ct.pointCount;
+    const LWall& wl = W[ct.wall];
+    v.cB = V(wl.px, wl.py); v.aB = wl.ang; v.vB = zero2(); v.wB = 0.0f;
+    v.ln = V(ct.lnx, ct.lny); v.lp = V(ct.lpx, ct.lpy); v.pcount = ct.pointCount; v.type = ct.mtype;
+    v.K[0] = v.K[1] = v.K[2] = v.K[3] = 0.0f; v.nm[0] = v.nm[1] = v.nm[2] = v.nm[3] = 0.0f;
+    for (int j = 0; j < 2; ++j) {
+      v.p[j].ni = v.p[j].ti = 0.0f;
+      v.p[j].rA = v.p[j].rB = zero2(); v.p[j].nm = v.p[j].tm = v.p[j].vb = 0.0f;
+      v.lps[j] = zero2();
+    }
+    for (int j = 0; j < ct.pointCount; ++j) {
+      if (warm) { v.p[j].ni = dtRatio * ct.pt[j].ni; v.p[j].ti = dtRatio * ct.pt[j].ti; }
+      v.lps[j] = V(ct.pt[j].lx, ct.pt[j].ly);
+    }
+  }
+}
+
+__device__ inline void cs_init_velocity(VC* vc, int n, const Car& c, const BodyState& A) {
+  const float mA = CAR_INV_MASS, iA = CAR_INV_I, mB = 0.0f, iB = 0.0f;
+  const float friction_unused = 0.0f; (void)friction_unused;
+  for (int i = 0; i < n; ++i) {
+    VC& v = vc[i];
+    const DContact& m = c.ct[v.ci];
+    V2 cA = A.c; float aA = A.a; V2 vA = A.v; float wA = A.w;
+    V2 cB = v.cB; float aB = v.aB; V2 vB = v.vB; float wB = v.wB;
+    Xf xfA, xfB;
+    xfA.q = rot_set(aA); xfB.q = rot_set(aB);
+    xfA.p = vsub(cA, rmul(xfA.q, zero2()));
+    xfB.p = vsub(cB, rmul(xfB.q, zero2()));
+    V2 normal = zero2(), pts[2];
+    world_manifold(m, xfA, xfB, &normal, pts);
+    v.normal = normal;
+    for (int j = 0; j < v.pointCount; ++j) {
+      VCP& p = v.p[j];
+      p.rA = vsub(pts[j], cA); p.rB = vsub(pts[j], cB);
+      float rnA = vcross(p.rA, v.normal), rnB = vcross(p.rB, v.normal);
+      float kNormal = mA + mB + iA * rnA * rnA + iB * rnB * rnB;
+      p.nm = kNormal > 0.0f ? __fdiv_rn(1.0f, kNormal) : 0.0f;
+      V2 tangent = vcross_vs(v.normal, 1.0f);
+      float rtA = vcross(p.rA, tangent), rtB = vcross(p.rB, tangent);
+      float kTangent = mA + mB + iA * rtA * rtA + iB * rtB * rtB;
+      p.tm = kTangent > 0.0f ? __fdiv_rn(1.0f, kTangent) : 0.0f;
+      p.vb = 0.0f;
+      float vRel = vdot(v.normal, vsub(vsub(vadd(vB, vcross_sv(wB, p.rB)), vA), vcross_sv(wA, p.rA)));
+      if (vRel < -VELOCITY_THRESHOLD) p.vb = -MIX_RESTITUTION * vRel;
+    }
+    if (v.pointCount == 2) {
+      VCP& p1 = v.p[0]; VCP& p2 = v.p[1];
+      float rn1A = vcross(p1.rA, v.normal), rn1B = vcross(p1.rB, v.normal);
+      float rn2A = vcross(p2.rA, v.normal), rn2B = vcross(p2.rB, v.normal);
+      float k11 = mA + mB + iA * rn1A * rn1A + iB * rn1B * rn1B;
+      float k22 = mA + mB + iA * rn2A * rn2A + iB * rn2B * rn2B;
+      float k12 = mA + mB + iA * rn1A * rn2A + iB * rn1B * rn2B;
+      if (k11 * k11 < 1000.0f * (k11 * k22 - k12 * k12)) {
+        v.K[0] = k11; v.K[1] = k12; v.K[2] = k12; v.K[3] = k22;
+        float a = v.K[0], b = v.K[2], cc = v.K[1], d = v.K[3];
+        float det = a * d - b * cc;
+        if (det != 0.0f) det = __fdiv_rn(1.0f, det);
+        v.nm[0] = det * d; v.nm[2] = -det * b; v.nm[1] = -det * cc; v.nm[3] = det * a;
+      } else {
+        v.pointCount = 1;
+      }
+    }
+  }
+}
+
+__device__ inline void cs_warm_start(VC* vc, int n, BodyState& A) {
+  const float mA = CAR_INV_MASS, iA = CAR_INV_I, mB = 0.0f, iB = 0.0f;
+  for (int i = 0; i < n; ++i) {
+    VC& v = vc[i];
+    V2 vA = A.v; float wA = A.w; V2 vB = v.vB; float wB = v.wB;
+    V2 normal = v.normal, tangent = vcross_vs(normal, 1.0f);
+    for (int j = 0; j < v.pointCount; ++j) {
+      VCP& p = v.p[j];
+      V2 P = vadd(vmul(p.ni, normal), vmul(p.ti, tangent));
+      wA -= iA * vcross(p.rA, P);
+      vA = vsub(vA, vmul(mA, P));
+      wB += iB * vcross(p.rB, P);
+      vB = vadd(vB, vmul(mB, P));
+    }
+    A.v = vA; A.w = wA; v.vB = vB; v.wB = wB;
+  }
+}
+
+__device__ __forceinline__ V2 rel_vel(V2 vA, float wA, V2 vB, float wB, const VCP& p) {
+  return vsub(vsub(vadd(vB, vcross_sv(wB, p.rB)), vA), vcross_sv(wA, p.rA));
+}
+
+__device__ inline void cs_solve_velocity(VC* vc, int n, BodyState& A, float friction) {
+  const float mA = CAR_INV_MASS, iA = CAR_INV_I, mB = 0.0f, iB = 0.0f;
+  for (int i = 0; i < n; ++i) {
+    VC& v = vc[i];
+    V2 vA = A.v; float wA = A.w; V2 vB = v.vB; float wB = v.wB;
+    V2 normal = v.normal, tangent = vcross_vs(normal, 1.0f);
+    for (int j = 0; j < v.pointCount; ++j) {
+      VCP& p = v.p[j];
+      V2 dv = rel_vel(vA, wA, vB, wB, p);
+      float vt = vdot(dv, tangent) - 0.0f;
+      float lambda = p.tm * (-vt);
+      float maxFriction = friction * p.ni;
+      float newImpulse = fclamp(p.ti + lambda, -maxFriction, maxFriction);
+      lambda = newImpulse - p.ti;
+      p.ti = newImpulse;
+      V2 P = vmul(lambda, tangent);
+      vA = vsub(vA, vmul(mA, P)); wA -= iA * vcross(p.rA, P);
+      vB = vadd(vB, vmul(mB, P)); wB += iB * vcross(p.rB, P);
+    }
+    if (v.pointCount == 1) {
+      VCP& p = v.p[0];
+      V2 dv = rel_vel(vA, wA, vB, wB, p);
+      float vn = vdot(dv, normal);
+      float lambda = -p.nm * (vn - p.vb);
+      float newImpulse = fmaxb(p.ni + lambda, 0.0f);
+      lambda = newImpulse - p.ni;
+      p.ni = newImpulse;
+      V2 P = vmul(lambda, normal);
+      vA = vsub(vA, vmul(mA, P)); wA -= iA * vcross(p.rA, P);
+      vB = vadd(vB, vmul(mB, P)); wB += iB * vcross(p.rB, P);
+    } else {
+      VCP& cp1 = v.p[0]; VCP& cp2 = v.p[1];
+      V2 a = V(cp1.ni, cp2.ni);
+      V2 dv1 = rel_vel(vA, wA, vB, wB, cp1), dv2 = rel_vel(vA, wA, vB, wB, cp2);
+      float vn1 = vdot(dv1, normal), vn2 = vdot(dv2, normal);
+      V2 b = V(vn1 - cp1.vb, vn2 - cp2.vb);
+      V2 Ka = V(v.K[0] * a.x + v.K[2] * a.y, v.K[1] * a.x + v.K[3] * a.y);
+      b = vsub(b, Ka);
+      V2 x;
+      bool ok = false;
+      x = vneg(V(v.nm[0] * b.x + v.nm[2] * b.y, v.nm[1] * b.x + v.nm[3] * b.y));
+      if (x.x >= 0.0f && x.y >= 0.0f) ok = true;
+      if (!ok) {
+        x.x = -cp1.nm * b.x; x.y = 0.0f;
+        vn2 = v.K[1] * x.x + b.y;
+        if (x.x >= 0.0f && vn2 >= 0.0f) ok = true;
+      }
+      if (!ok) {
+        x.x = 0.0f; x.y = -cp2.nm * b.y;
+        vn1 = v.K[2] * x.y + b.x;
+        if (x.y >= 0.0f && vn1 >= 0.0f) ok = true;
+      }
+      if (!ok) {
+        x.x = 0.0f; x.y = 0.0f; vn1 = b.x; vn2 = b.y;
+        if (vn1 >= 0.0f && vn2 >= 0.0f) ok = true;
+      }
+      if (ok) {
+        V2 d = vsub(x, a);
+        V2 P1 = vmul(d.x, normal), P2 = vmul(d.y, normal);
+        vA = vsub(vA, vmul(mA, vadd(P1, P2)));
+        wA -= iA * (vcross(cp1.rA, P1) + vcross(cp2.rA, P2));
+        vB = vadd(vB, vmul(mB, vadd(P1, P2)));
+        wB += iB * (vcross(cp1.rB, P1) + vcross(cp2.rB, P2));
+        cp1.ni = x.x; cp2.ni = x.y;
+      }
+    }
+    A.v = vA; A.w = wA; v.vB = vB; v.wB = wB;
+  }
+}
+
+__device__ inline void cs_store(const VC* vc, int n, Car& c) {
+  for (int i = 0; i < n; ++i) {
+    DContact& m = c.ct[vc[i].ci];
+    for (int j = 0; j < vc[i].pointCount; ++j) { m.pt[j].ni = vc[i].p[j].ni; m.pt[j].ti = vc[i].p[j].ti; }
+  }
+}
+
+__device__ inline int cs_solve_position(VC* vc, int n, BodyState& A, int toi) {
+  float minSep = 0.0f;
+  const float mA = CAR_INV_MASS, iA = CAR_INV_I, mB = 0.0f, iB = 0.0f;
+  for (int i = 0; i < n; ++i) {
+    VC& v = vc[i];
+    V2 cA = A.c; float aA = A.a; V2 cB = v.cB; float aB = v.aB;
+    for (int j = 0; j < v.pcount; ++j) {
+      Xf xfA, xfB;
+      xfA.q = rot_set(aA); xfB.q = rot_set(aB);
+      xfA.p = vsub(cA, rmul(xfA.q, zero2()));
+      xfB.p = vsub(cB, rmul(xfB.q, zero2()));
+      V2 normal, point; float sep;
+      if (v.type == 1) {
+        V2 nn = rmul(xfA.q, v.ln), planePoint = xmul(xfA, v.lp), clipPoint = xmul(xfB, v.lps[j]);
+        sep = vdot(vsub(clipPoint, planePoint), nn) - POLY_RADIUS - POLY_RADIUS;
+        point = clipPoint; normal = nn;
+      } else {
+        V2 nn = rmul(xfB.q, v.ln), planePoint = xmul(xfB, v.lp), clipPoint = xmul(xfA, v.lps[j]);
+        sep = vdot(vsub(clipPoint, planePoint), nn) - POLY_RADIUS - POLY_RADIUS;
+        point = clipPoint; normal = vneg(nn);
+      }
+      V2 rA = vsub(point, cA), rB = vsub(point, cB);
+      minSep = fminb(minSep, sep);
+      float C = fclamp((toi ? TOI_BAUMGARTE : BAUMGARTE) * (sep + LINEAR_SLOP), -MAX_LINEAR_CORRECTION, 0.0f);
+      float rnA = vcross(rA, normal), rnB = vcross(rB, normal);
+      float K = mA + mB + iA * rnA * rnA + iB * rnB * rnB;
+      float impulse = K > 0.0f ? __fdiv_rn(-C, K) : 0.0f;
+      V2 P = vmul(impulse, normal);
+      cA = vsub(cA, vmul(mA, P)); aA -= iA * vcross(rA, P);
+      cB = vadd(cB, vmul(mB, P)); aB += iB * vcross(rB, P);
+    }
+    A.c = cA; A.a = aA; v.cB = cB; v.aB = aB;
+  }
+  return toi ? (minSep >= -1.5f * LINEAR_SLOP) : (minSep >= -3.0f * LINEAR_SLOP);
+}
+
+__device__ inline void report(Car& c, const VC* vc, int n) {
+  for (int i = 0; i < n; ++i) lis_post(c, vc[i].pointCount, vc[i].p[0].ni, vc[i].p[1].ni);
+}
+
+__device__ inline void integrate_positions(BodyState& A, float h) {
+  V2 cc = A.c; float a = A.a; V2 v = A.v; float w = A.w;
+  V2 translation = vmul(h, v);
+  if (vdot(translation, translation) > MAX_TRANSLATION * MAX_TRANSLATION) {
+    float ratio = __fdiv_rn(MAX_TRANSLATION, vlen(translation));
+    v = vmul(ratio, v);
+  }
+  float rotation = h * w;
+  if (rotation * rotation > MAX_ROTATION * MAX_ROTATION) {
+    float ratio = __fdiv_rn(MAX_ROTATION, fabsf(rotation));
+    w *= ratio;
+  }
+  cc = vadd(cc, vmul(h, v));
+  a += h * w;
+  A.c = cc; A.a = a; A.v = v; A.w = w;
+}
+
+// b2World::Solve (single dynamic body island)
+__device__ inline void solve(Car& c, const LWall* W, int nw, float dt, float dtRatio, float friction) {
+  if (!c.awake) return;
+  int cidx[MAX_ISLAND]; int n = 0;
+  for (int i = 0; i < c.nct; ++i) {
+    int fl = c.ct[i].flags;
+    if (!(fl & CT_ENABLED) || !(fl & CT_TOUCH)) continue;
+    if (n == MAX_ISLAND) { c.overflow = 2; break; }
+    cidx[n++] = i;
+  }
+  float h = dt;
+  BodyState A;
+  c.c0 = c.c; c.a0 = c.a;
+  {
+    V2 v = c.v; float wv = c.w;
+    V2 g = vadd(vmul(1.0f, zero2()), vmul(CAR_INV_MASS, c.force));
+    v = vadd(v, vmul(h, g));
+    wv += h * CAR_INV_I * c.torque;
+    A.c = c.c; A.a = c.a; A.v = v; A.w = wv;
+  }
+  VC vc[MAX_ISLAND];
+  cs_init(vc, n, c, cidx, W, true, dtRatio);
+  cs_init_velocity(vc, n, c, A);
+  cs_warm_start(vc, n, A);
+  for (int it = 0; it < 6; ++it) cs_solve_velocity(vc, n, A, friction);
+  cs_store(vc, n, c);
+  integrate_positions(A, h);
+  int positionSolved = 0;
+  for (int it = 0; it < 4; ++it) { if (cs_solve_position(vc, n, A, 0)) { positionSolved = 1; break; } }
+  c.c = A.c; c.a = A.a; c.v = A.v; c.w = A.w;
+  sync_transform(c);
+  report(c, vc, n);
+  {
+    float minSleepTime = FLT_BIG;
+    const float linTolSqr = LINEAR_SLEEP_TOL * LINEAR_SLEEP_TOL;
+    const float angTolSqr = ANGULAR_SLEEP_TOL * ANGULAR_SLEEP_TOL;
+    if (c.w * c.w > angTolSqr || vdot(c.v, c.v) > linTolSqr) { c.sleep = 0.0f; minSleepTime = 0.0f; }
+    else { c.sleep += h; minSleepTime = fminb(minSleepTime, c.sleep); }
+    if (minSleepTime >= TIME_TO_SLEEP && positionSolved) {
+      c.awake = 0; c.sleep = 0.0f; c.v = zero2(); c.w = 0.0f; c.force = zero2(); c.torque = 0.0f;
+    }
+  }
+  sync_fixtures(c);
+  find_new_contacts(c, W, nw);
+}
+
+// ------------------------------------------------------------------ GJK / TOI
+struct SV { V2 wA, wB, w; float a; int iA, iB; };
+struct Simplex { SV v[3]; int count; };
+struct SCache { float metric; int count; int iA[3], iB[3]; };
+
+__device__ __forceinline__ int support(const Poly* p, V2 d) {
+  int best = 0; float bestValue = vdot(p->v[0], d);
+  for (int i = 1; i < 4; ++i) { float value = vdot(p->v[i], d); if (value > bestValue) { best = i; bestValue = value; } }
+  return best;
+}
+__device__ inline float simplex_metric(const Simplex& s) {
+  if (s.count == 1) return 0.0f;
+  if (s.count == 2) return vlen(vsub(s.v[0].w, s.v[1].w));
+  if (s.count == 3) return vcross(vsub(s.v[1].w, s.v[0].w), vsub(s.v[2].w, s.v[0].w));
+  return 0.0f;
+}
+__device__ inline float gjk_distance(SCache& cache, const Poly* pA, Xf tA, const Poly* pB, Xf tB) {
+  Simplex s;
+  s.count = cache.count;
+  for (int i = 0; i < s.count; ++i) {
+    SV& v = s.v[i];
+    v.iA = cache.iA[i]; v.iB = cache.iB[i];
+    v.wA = xmul(tA, pA->v[v.iA]); v.wB = xmul(tB, pB->v[v.iB]);
+    v.w = vsub(v.wB, v.wA); v.a = 0.0f;
+  }
+  if (s.count > 1) {
+    float metric1 = cache.metric, metric2 = simplex_metric(s);
+    if (metric2 < 0.5f * metric1 || 2.0f * metric1 < metric2 || metric2 < FLT_EPS) s.count = 0;
+  }
+  if (s.count == 0) {
+    SV& v = s.v[0];
+    v.iA = 0; v.iB = 0;
+    v.wA = xmul(tA, pA->v[0]); v.wB = xmul(tB, pB->v[0]);
+    v.w = vsub(v.wB, v.wA); v.a = 1.0f;
+    s.count = 1;
+  }
+  int saveA[3], saveB[3], saveCount = 0, iter = 0;
+  while (iter < 20) {
+    saveCount = s.count;
+    for (int i = 0; i < saveCount; ++i) { saveA[i] = s.v[i].iA; saveB[i] = s.v[i].iB; }
+    if (s.count == 2) {
+      V2 w1 = s.v[0].w, w2 = s.v[1].w, e12 = vsub(w2, w1);
+      float d12_2 = -vdot(w1, e12);
+      if (d12_2 <= 0.0f) { s.v[0].a = 1.0f; s.count = 1; }
+      else {
+        float d12_1 = vdot(w2, e12);
+        if (d12_1 <= 0.0f) { s.v[1].a = 1.0f; s.count = 1; s.v[0] = s.v[1]; }
+        else { float inv = __fdiv_rn(1.0f, d12_1 + d12_2); s.v[0].a = d12_1 * inv; s.v[1].a = d12_2 * inv; s.count = 2; }
+      }
+    } else if (s.count == 3) {
+      V2 w1 = s.v[0].w, w2 = s.v[1].w, w3 = s.v[2].w;
+      V2 e12 = vsub(w2, w1);
+      float d12_1 = vdot(w2, e12), d12_2 = -vdot(w1, e12);
+      V2 e13 = vsub(w3, w1);
+      float d13_1 = vdot(w3, e13), d13_2 = -vdot(w1, e13);
+      V2 e23 = vsub(w3, w2);
+      float d23_1 = vdot(w3, e23), d23_2 = -vdot(w2, e23);
+      float n123 = vcross(e12, e13);
+      float d123_1 = n123 * vcross(w2, w3), d123_2 = n123 * vcross(w3, w1), d123_3 = n123 * vcross(w1, w2);
+      if (d12_2 <= 0.0f && d13_2 <= 0.0f) { s.v[0].a = 1.0f; s.count = 1; }
+      else if (d12_1 > 0.0f && d12_2 > 0.0f && d123_3 <= 0.0f) {
+        float inv = __fdiv_rn(1.0f, d12_1 + d12_2); s.v[0].a = d12_1 * inv; s.v[1].a = d12_2 * inv; s.count = 2;
+      } else if (d13_1 > 0.0f && d13_2 > 0.0f && d123_2 <= 0.0f) {
+        float inv = __fdiv_rn(1.0f, d13_1 + d13_2); s.v[0].a = d13_1 * inv; s.v[2].a = d13_2 * inv; s.count = 2; s.v[1] = s.v[2];
+      } else if (d12_1 <= 0.0f && d23_2 <= 0.0f) { s.v[1].a = 1.0f; s.count = 1; s.v[0] = s.v[1]; }
+      else if (d13_1 <= 0.0f && d23_1 <= 0.0f) { s.v[2].a = 1.0f; s.count = 1; s.v[0] = s.v[2]; }
+      else if (d23_1 > 0.0f && d23_2 > 0.0f && d123_1 <= 0.0f) {
+        float inv = __fdiv_rn(1.0f, d23_1 + d23_2); s.v[1].a = d23_1 * inv; s.v[2].a = d23_2 * inv; s.count = 2; s.v[0] = s.v[2];
+      } else {
+        float inv = __fdiv_rn(1.0f, d123_1 + d123_2 + d123_3);
+        s.v[0].a = d123_1 * inv; s.v[1].a = d123_2 * inv; s.v[2].a = d123_3 * inv; s.count = 3;
+      }
+    }
+    if (s.count == 3) break;
+    V2 d;
+    if (s.count == 1) d = vneg(s.v[0].w);
+    else {
+      V2 e12 = vsub(s.v[1].w, s.v[0].w);
+      float sgn = vcross(e12, vneg(s.v[0].w));
+      d = sgn > 0.0f ? vcross_sv(1.0f, e12) : vcross_vs(e12, 1.0f);
+    }
+    if (vdot(d, d) < FLT_EPS * FLT_EPS) break;
+    SV& vx = s.v[s.count];
+    vx.iA = support(pA, rmulT(tA.q, vneg(d)));
+    vx.wA = xmul(tA, pA->v[vx.iA]);
+    vx.iB = support(pB, rmulT(tB.q, d));
+    vx.wB = xmul(tB, pB->v[vx.iB]);
+    vx.w = vsub(vx.wB, vx.wA);
+    ++iter;
+    bool dup = false;
+    for (int i = 0; i < saveCount; ++i) if (vx.iA == saveA[i] && vx.iB == saveB[i]) { dup = true; break; }
+    if (dup) break;
+    ++s.count;
+  }
+  V2 wa = zero2(), wb = zero2();
+  if (s.count == 1) { wa = s.v[0].wA; wb = s.v[0].wB; }
+  else if (s.count == 2) {
+    wa = vadd(vmul(s.v[0].a, s.v[0].wA), vmul(s.v[1].a, s.v[1].wA));
+    wb = vadd(vmul(s.v[0].a, s.v[0].wB), vmul(s.v[1].a, s.v[1].wB));
+  } else if (s.count == 3) {
+    wa = vadd(vadd(vmul(s.v[0].a, s.v[0].wA), vmul(s.v[1].a, s.v[1].wA)), vmul(s.v[2].a, s.v[2].wA));
+    wb = wa;
+  }
+  cache.metric = simplex_metric(s);
+  cache.count = s.count;
+  for (int i = 0; i < s.count; ++i) { cache.iA[i] = s.v[i].iA; cache.iB[i] = s.v[i].iB; }
+  return vlen(vsub(wa, wb));
+}
+
+struct Sweep { V2 c0, c; float a0, a, alpha0; };
+__device__ __forceinline__ Xf sweep_xf(const Sweep& s, float beta) {
+  Xf xf;
+  xf.p = vadd(vmul(1.0f - beta, s.c0), vmul(beta, s.c));
+  float angle = (1.0f - beta) * s.a0 + beta * s.a;
+  xf.q = rot_set(angle);
+  xf.p = vsub(xf.p, rmul(xf.q, zero2()));
+  return xf;
+}
+__device__ __forceinline__ void sweep_normalize(Sweep& s) {
+  float twoPi = 2.0f * B2_PI;
+  float d = twoPi * floorf(__fdiv_rn(s.a0, twoPi));
+  s.a0 -= d; s.a -= d;
+}
+
+enum { SF_POINTS, SF_FACEA, SF_FACEB };
+struct SepFn { Sweep sA, sB; int type; V2 lp, axis; };
+__device__ inline void sep_init(SepFn& f, const SCache& cache, const Poly* pA, const Sweep& sA, const Poly* pB, const Sweep& sB, float t1) {
+  f.sA = sA; f.sB = sB;
+  Xf xfA = sweep_xf(f.sA, t1), xfB = sweep_xf(f.sB, t1);
+  if (cache.count == 1) {
+    f.type = SF_POINTS;
+    V2 pointA = xmul(xfA, pA->v[cache.iA[0]]), pointB = xmul(xfB, pB->v[cache.iB[0]]);
+    f.axis = vsub(pointB, pointA);
+    vnormalize(&f.axis);
+    f.lp = zero2();
+  } else if (cache.iA[0] == cache.iA[1]) {
+    f.type = SF_FACEB;
+    V2 lB1 = pB->v[cache.iB[0]], lB2 = pB->v[cache.iB[1]];
+    f.axis = vcross_vs(vsub(lB2, lB1), 1.0f);
+    vnormalize(&f.axis);
+    V2 normal = rmul(xfB.q, f.axis);
+    f.lp = vmul(0.5f, vadd(lB1, lB2));
+    V2 pointB = xmul(xfB, f.lp), pointA = xmul(xfA, pA->v[cache.iA[0]]);
+    float s = vdot(vsub(pointA, pointB), normal);
+    if (s < 0.0f) f.axis = vneg(f.axis);
+  } else {
+    f.type = SF_FACEA;
+    V2 lA1 = pA->v[cache.iA[0]], lA2 = pA->v[cache.iA[1]];
+    f.axis = vcross_vs(vsub(lA2, lA1), 1.0f);
+    vnormalize(&f.axis);
+    V2 normal = rmul(xfA.q, f.axis);
+    f.lp = vmul(0.5f, vadd(lA1, lA2));
+    V2 pointA = xmul(xfA, f.lp), pointB = xmul(xfB, pB->v[cache.iB[0]]);
+    float s = vdot(vsub(pointB, pointA), normal);
+    if (s < 0.0f) f.axis = vneg(f.axis);
+  }
+}
+__device__ inline float sep_find_min(const SepFn& f, const Poly* pA, const Poly* pB, int* iA, int* iB, float t) {
+  Xf xfA = sweep_xf(f.sA, t), xfB = sweep_xf(f.sB, t);
+  if (f.type == SF_POINTS) {
+    V2 axisA = rmulT(xfA.q, f.axis), axisB = rmulT(xfB.q, vneg(f.axis));
+    *iA = support(pA, axisA); *iB = support(pB, axisB);
+    V2 pointA = xmul(xfA, pA->v[*iA]), pointB = xmul(xfB, pB->v[*iB]);
+    return vdot(vsub(pointB, pointA), f.axis);
+  } else if (f.type == SF_FACEA) {
+    V2 normal = rmul(xfA.q, f.axis), pointA = xmul(xfA, f.lp);
+    V2 axisB = rmulT(xfB.q, vneg(normal));
+    *iA = -1; *iB = support(pB, axisB);
+    V2 pointB = xmul(xfB, pB->v[*iB]);
+    return vdot(vsub(pointB, pointA), normal);
+  } else {
+    V2 normal = rmul(xfB.q, f.axis), pointB = xmul(xfB, f.lp);
+    V2 axisA = rmulT(xfA.q, vneg(normal));
+    *iB = -1; *iA = support(pA, axisA);
+    V2 pointA = xmul(xfA, pA->v[*iA]);
+    return vdot(vsub(pointA, pointB), normal);
+  }
+}
+__device__ inline float sep_eval(const SepFn& f, const Poly* pA, const Poly* pB, int iA, int iB, float t) {
+  Xf xfA = sweep_xf(f.sA, t), xfB = sweep_xf(f.sB, t);
+  if (f.type == SF_POINTS) {
+    V2 pointA = xmul(xfA, pA->v[iA]), pointB = xmul(xfB, pB->v[iB]);
+    return vdot(vsub(pointB, pointA), f.axis);
+  } else if (f.type == SF_FACEA) {
+    V2 normal = rmul(xfA.q, f.axis), pointA = xmul(xfA, f.lp), pointB = xmul(xfB, pB->v[iB]);
+    return vdot(vsub(pointB, pointA), normal);
+  } else {
+    V2 normal = rmul(xfB.q, f.axis), pointB = xmul(xfB, f.lp), pointA = xmul(xfA, pA->v[iA]);
+    return vdot(vsub(pointA, pointB), normal);
+  }
+}
+enum { TOI_UNKNOWN, TOI_FAILED, TOI_OVERLAPPED, TOI_TOUCHING, TOI_SEPARATED };
+__device__ inline float time_of_impact(int* state, const Poly* pA, const Sweep& sweepA, const Poly* pB, const Sweep& sweepB, float tMax) {
+  *state = TOI_UNKNOWN;
+  float out_t = tMax;
+  Sweep sA = sweepA, sB = sweepB;
+  sweep_normalize(sA); sweep_normalize(sB);
+  float totalRadius = pA->radius + pB->radius;
+  float target = fmaxb(LINEAR_SLOP, totalRadius - 3.0f * LINEAR_SLOP);
+  float tolerance = 0.25f * LINEAR_SLOP;
+  float t1 = 0.0f;
+  int iter = 0;
+  SCache cache; cache.count = 0; cache.metric = 0.0f;
+  for (;;) {
+    Xf xfA = sweep_xf(sA, t1), xfB = sweep_xf(sB, t1);
+    float distance = gjk_distance(cache, pA, xfA, pB, xfB);
+    if (distance <= 0.0f) { *state = TOI_OVERLAPPED; out_t = 0.0f; break; }
+    if (distance < target + tolerance) { *state = TOI_TOUCHING; out_t = t1; break; }
+    SepFn fcn;
+    sep_init(fcn, cache, pA, sA, pB, sB, t1);
+    bool done = false;
+    float t2 = tMax;
+    int pushBackIter = 0;
+    for (;;) {
+      int indexA, indexB;
+      float s2 = sep_find_min(fcn, pA, pB, &indexA, &indexB, t2);
+      if (s2 > target + tolerance) { *state = TOI_SEPARATED; out_t = tMax; done = true; break; }
+      if (s2 > target - tolerance) { t1 = t2; break; }
+      float s1 = sep_eval(fcn, pA, pB, indexA, indexB, t1);
+      if (s1 < target - tolerance) { *state = TOI_FAILED; out_t = t1; done = true; break; }
+      if (s1 <= target + tolerance) { *state = TOI_TOUCHING; out_t = t1; done = true; break; }
+      int rootIterCount = 0;
+      float a1 = t1, a2 = t2;
+      for (;;) {
+        float t;
+        if (rootIterCount & 1) t = a1 + __fdiv_rn((target - s1) * (a2 - a1), s2 - s1);
+        else t = 0.5f * (a1 + a2);
+        ++rootIterCount;
+        float s = sep_eval(fcn, pA, pB, indexA, indexB, t);
+        if (fabsf(s - target) < tolerance) { t2 = t; break; }
+        if (s > target) { a1 = t; s1 = s; } else { a2 = t; s2 = s; }
+        if (rootIterCount == 50) break;
+      }
+      ++pushBackIter;
+      if (pushBackIter == 8) break;
+    }
+    ++iter;
+    if (done) break;
+    if (iter == 20) { *state = TOI_FAILED; out_t = t1; break; }
+  }
+  return out_t;
+}
+
+__device__ inline void island_solve_toi(Car& c, const LWall* W, const int* cidx, int n, float subdt, float friction) {
+  BodyState A; A.c = c.c; A.a = c.a; A.v = c.v; A.w = c.w;
+  VC vc[MAX_ISLAND];
+  cs_init(vc, n, c, cidx, W, false, 1.0f);
+  for (int it = 0; it < 20; ++it) { if (cs_solve_position(vc, n, A, 1)) break; }
+  c.c0 = A.c; c.a0 = A.a;
+  cs_init_velocity(vc, n, c, A);
+  for (int it = 0; it < 6; ++it) cs_solve_velocity(vc, n, A, friction);
+  integrate_positions(A, subdt);
+  c.c = A.c; c.a = A.a; c.v = A.v; c.w = A.w;
+  sync_transform(c);
+  report(c, vc, n);
+}
+
+// b2World::SolveTOI
+__device__ inline void solve_toi(Car& c, const LWall* W, int nw, float dt, float friction) {
+  Poly pa; make_box(&pa, CAR_HX, CAR_HY);
+  c.alpha0 = 0.0f;
+  for (int i = 0; i < c.nct; ++i) { c.ct[i].flags &= ~(CT_TOI | CT_ISLAND); c.ct[i].toiCount = 0; c.ct[i].toi = 1.0f; }
+  for (;;) {
+    int minC = -1; float minAlpha = 1.0f;
+    for (int i = 0; i < c.nct; ++i) {
+      DContact& ct = c.ct[i];
+      if (!(ct.flags & CT_ENABLED)) continue;
+      if (ct.toiCount > MAX_SUBSTEPS) continue;
+      float alpha = 1.0f;
+      if (ct.flags & CT_TOI) alpha = ct.toi;
+      else {
+        if (!c.awake) continue;
+        float alpha0 = c.alpha0;
+        const LWall& wl = W[ct.wall];
+        Poly pb; make_box(&pb, wl.hx, wl.hy);
+        Sweep sA; sA.c0 = c.c0; sA.c = c.c; sA.a0 = c.a0; sA.a = c.a; sA.alpha0 = c.alpha0;
+        Sweep sB; sB.c0 = V(wl.px, wl.py); sB.c = sB.c0; sB.a0 = wl.ang; sB.a = wl.ang; sB.alpha0 = 0.0f;
+        int state;
+        float beta = time_of_impact(&state, &pa, sA, &pb, sB, 1.0f);
+        if (state == TOI_TOUCHING) alpha = fminb(alpha0 + (1.0f - alpha0) * beta, 1.0f);
+        else alpha = 1.0f;
+        ct.toi = alpha; ct.flags |= CT_TOI;
+      }
+      if (alpha < minAlpha) { minC = i; minAlpha = alpha; }
+    }
+    if (minC < 0 || 1.0f - 10.0f * FLT_EPS < minAlpha) break;
+    V2 bc0 = c.c0, bc = c.c; float ba0 = c.a0, ba = c.a, balpha0 = c.alpha0;
+    {
+      float beta = __fdiv_rn(minAlpha - c.alpha0, 1.0f - c.alpha0);
+      c.c0 = vadd(c.c0, vmul(beta, vsub(c.c, c.c0)));
+      c.a0 += beta * (c.a - c.a0);
+      c.alpha0 = minAlpha;
+      c.c = c.c0; c.a = c.a0;
+      sync_transform(c);
+    }
+    contact_update(c, minC, W);
+    c.ct[minC].flags &= ~CT_TOI;
+    ++c.ct[minC].toiCount;
+    if (!(c.ct[minC].flags & CT_ENABLED) || !(c.ct[minC].flags & CT_TOUCH)) {
+      c.ct[minC].flags &= ~CT_ENABLED;
+      c.c0 = bc0; c.c = bc; c.a0 = ba0; c.a = ba; c.alpha0 = balpha0;
+      sync_transform(c);
+      continue;
+    }
+    set_awake(c);
+    int cidx[MAX_ISLAND]; int n = 0;
+    cidx[n++] = minC; c.ct[minC].flags |= CT_ISLAND;
+    for (int i = 0; i < c.nct; ++i) {
+      if (n == MAX_TOI_CONTACTS) break;
+      if (n == MAX_ISLAND) {   // more touching contacts than the island buffer: flag, keep going exactly-as-far-as-possible
+        if (!(c.ct[i].flags & CT_ISLAND)) { c.overflow = 2; }
+        break;
+      }
+      if (c.ct[i].flags & CT_ISLAND) continue;
+      contact_update(c, i, W);
+      if (!(c.ct[i].flags & CT_ENABLED)) continue;
+      if (!(c.ct[i].flags & CT_TOUCH)) continue;
+      c.ct[i].flags |= CT_ISLAND;
+      cidx[n++] = i;
+    }
+    float subdt = (1.0f - minAlpha) * dt;
+    island_solve_toi(c, W, cidx, n, subdt, friction);
+    sync_fixtures(c);
+    for (int i = 0; i < c.nct; ++i) c.ct[i].flags &= ~(CT_TOI | CT_ISLAND);
+    find_new_contacts(c, W, nw);
+  }
+}
+
+__device__ inline void b2_step(Car& c, const LWall* W, int nw, float dt, float friction) {
+  float inv_dt = dt > 0.0f ? __fdiv_rn(1.0f, dt) : 0.0f;
+  float dtRatio = c.invdt0 * dt;
+  collide(c, W);
+  solve(c, W, nw, dt, dtRatio, friction);
+  solve_toi(c, W, nw, dt, friction);
+  c.invdt0 = inv_dt;
+  c.force = zero2(); c.torque = 0.0f;
+}
+
+// b2Body::SetTransform
+__device__ inline void set_transform(Car& c, const LWall* W, int nw, V2 pos, float angle) {
+  c.xf.q = rot_set(angle);
+  c.xf.p = pos;
+  c.c = xmul(c.xf, zero2()); c.a = angle;
+  c.c0 = c.c; c.a0 = angle;
+  move_proxy(c, c.xf, c.xf);
+  find_new_contacts(c, W, nw);
+}
+
+}  // namespace nascar

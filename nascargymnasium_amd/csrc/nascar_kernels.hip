@@ -1,0 +1,1147 @@
+// nascar_kernels.hip -- fused batched CarEnv step for MI355X (gfx950) + the C ABI.
+//
+// Execution model: one workgroup = floor(256 / C) whole envs of ONE track
+// (C cars each, one lane per car).  The track's ~730 wall boxes are staged once
+// per workgroup into LDS and shared by the Box2D broadphase/narrowphase, the 16
+// distance-sensor rays of every car and the on-track query.  Env-level coupling
+// (lap-reset pending, termination, auto-reset) is reduced through LDS between
+// phases separated by __syncthreads().  All per-car state lives in HBM as SoA
+// (nascar_layout.h) and is read/written once per step.
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/nascar.h"
+#include "nascar_device.h"
+
+#pragma clang fp contract(off)
+
+using namespace nascar;
+
+#define BLOCK 256
+#define MAX_SEG 64
+
+// ------------------------------------------------------------------ device-side tables
+struct DSeg {   // per segment, float64 (src/track_generator.py TrackSegment)
+  double sx, sy, ex, ey, width, banking, la, chord;  // la: banking lateral assist (src/car.py:527-533)
+};
+struct TrackDev {
+  LWall* walls; int nwall;
+  DSeg* segs; int nseg;
+  double* prefix;      // cumulative chord length before segment k (src/car_env.py:1593-1600)
+  double total_length; int startline; int has_banking;
+};
+
+struct Params {
+  int E, C, N, epb, nblocks, reset_on_lap;
+  float dt_f; double dt_d; float friction;
+  double start_x, start_y; float start_angle;
+  float* f32; double* f64; int* i32; double* acc;
+  DContact* ct; int* act_key; float* act_n;
+  double* env_time; int* env_i32;
+  const int* blk_track; const int* blk_env;
+  const TrackDev* tracks;
+};
+
+#define F32P(P, f) ((P).f32 + (size_t)F32_##f * (P).N)
+#define F64P(P, f) ((P).f64 + (size_t)F64_##f * (P).N)
+#define I32P(P, f) ((P).i32 + (size_t)I32_##f * (P).N)
+
+// ------------------------------------------------------------------ load / store of one car
+__device__ inline void car_load(const Params& P, int n, Car& c) {
+  c.c = V(F32P(P, cx)[n], F32P(P, cy)[n]); c.a = F32P(P, a)[n];
+  c.v = V(F32P(P, vx)[n], F32P(P, vy)[n]); c.w = F32P(P, w)[n];
+  c.xf.q.s = F32P(P, qs)[n]; c.xf.q.c = F32P(P, qc)[n]; c.xf.p = V(F32P(P, xpx)[n], F32P(P, xpy)[n]);
+  c.sleep = F32P(P, sleep)[n]; c.invdt0 = F32P(P, invdt0)[n];
+  c.fat.lo = V(F32P(P, flox)[n], F32P(P, floy)[n]); c.fat.hi = V(F32P(P, fhix)[n], F32P(P, fhiy)[n]);
+  c.cum_reward = F32P(P, cum_reward)[n]; c.cum_reward_info = F32P(P, cum_reward_info)[n];
+  c.rpm = F64P(P, rpm)[n]; c.pvx = F64P(P, pvx)[n]; c.pvy = F64P(P, pvy)[n];
+  c.lfm = F64P(P, lfm)[n]; c.slip = F64P(P, slip)[n]; c.bank = F64P(P, bank)[n];
+  c.load[0] = F64P(P, load0)[n]; c.load[1] = F64P(P, load1)[n]; c.load[2] = F64P(P, load2)[n]; c.load[3] = F64P(P, load3)[n];
+  c.temp[0] = F64P(P, temp0)[n]; c.temp[1] = F64P(P, temp1)[n]; c.temp[2] = F64P(P, temp2)[n]; c.temp[3] = F64P(P, temp3)[n];
+  c.wear[0] = F64P(P, wear0)[n]; c.wear[1] = F64P(P, wear1)[n]; c.wear[2] = F64P(P, wear2)[n]; c.wear[3] = F64P(P, wear3)[n];
+  c.imp = F64P(P, imp)[n];
+  c.lt_start = F64P(P, lt_start)[n]; c.lt_cur = F64P(P, lt_cur)[n]; c.lt_last = F64P(P, lt_last)[n];
+  c.lt_best = F64P(P, lt_best)[n]; c.lt_px = F64P(P, lt_px)[n]; c.lt_py = F64P(P, lt_py)[n]; c.lt_dist = F64P(P, lt_dist)[n];
+  c.cum_impact = F64P(P, cum_impact)[n]; c.stuck_dur = F64P(P, stuck_dur)[n];
+  c.stuck_sx = F64P(P, stuck_sx)[n]; c.stuck_sy = F64P(P, stuck_sy)[n];
+  c.prev_px = F64P(P, prev_px)[n]; c.prev_py = F64P(P, prev_py)[n];
+  c.prog_hist = F64P(P, prog_hist)[n]; c.back = F64P(P, back)[n]; c.prev_back = F64P(P, prev_back)[n];
+  c.imp_at_obs = F64P(P, imp_at_obs)[n];
+  c.awake = I32P(P, awake)[n]; c.nct = I32P(P, nct)[n]; c.overflow = I32P(P, overflow)[n];
+  c.acc_len = I32P(P, acc_len)[n]; c.acc_head = I32P(P, acc_head)[n];
+  c.imp_present = I32P(P, imp_present)[n]; c.nact = I32P(P, nact)[n];
+  c.lt_timing = I32P(P, lt_timing)[n]; c.lt_has_last = I32P(P, lt_has_last)[n]; c.lt_has_best = I32P(P, lt_has_best)[n];
+  c.lt_crossed = I32P(P, lt_crossed)[n]; c.lt_has_pos = I32P(P, lt_has_pos)[n]; c.lt_laps = I32P(P, lt_laps)[n];
+  c.disabled = I32P(P, disabled)[n]; c.has_stuck_start = I32P(P, has_stuck_start)[n];
+  c.first_step = I32P(P, first_step)[n]; c.prev_laps = I32P(P, prev_laps)[n];
+  c.just_disabled = 0;
+  c.force = zero2(); c.torque = 0.0f; c.c0 = c.c; c.a0 = c.a; c.alpha0 = 0.0f; c.moved = 0;
+  c.ct = P.ct + (size_t)n * MAXC; c.act_key = P.act_key + (size_t)n * MAXC; c.act_n = P.act_n + (size_t)n * MAXC * 2;
+  c.acc = nullptr;
+}
+__device__ inline void car_store(const Params& P, int n, const Car& c) {
+  F32P(P, cx)[n] = c.c.x; F32P(P, cy)[n] = c.c.y; F32P(P, a)[n] = c.a;
+  F32P(P, vx)[n] = c.v.x; F32P(P, vy)[n] = c.v.y; F32P(P, w)[n] = c.w;
+  F32P(P, qs)[n] = c.xf.q.s; F32P(P, qc)[n] = c.xf.q.c; F32P(P, xpx)[n] = c.xf.p.x; F32P(P, xpy)[n] = c.xf.p.y;
+  F32P(P, sleep)[n] = c.sleep; F32P(P, invdt0)[n] = c.invdt0;
+  F32P(P, flox)[n] = c.fat.lo.x; F32P(P, floy)[n] = c.fat.lo.y; F32P(P, fhix)[n] = c.fat.hi.x; F32P(P, fhiy)[n] = c.fat.hi.y;
+  F32P(P, cum_reward)[n] = c.cum_reward; F32P(P, cum_reward_info)[n] = c.cum_reward_info;
+  F64P(P, rpm)[n] = c.rpm; F64P(P, pvx)[n] = c.pvx; F64P(P, pvy)[n] = c.pvy;
+  F64P(P, lfm)[n] = c.lfm; F64P(P, slip)[n] = c.slip; F64P(P, bank)[n] = c.bank;
+  F64P(P, load0)[n] = c.load[0]; F64P(P, load1)[n] = c.load[1]; F64P(P, load2)[n] = c.load[2]; F64P(P, load3)[n] = c.load[3];
+  F64P(P, temp0)[n] = c.temp[0]; F64P(P, temp1)[n] = c.temp[1]; F64P(P, temp2)[n] = c.temp[2]; F64P(P, temp3)[n] = c.temp[3];
+  F64P(P, wear0)[n] = c.wear[0]; F64P(P, wear1)[n] = c.wear[1]; F64P(P, wear2)[n] = c.wear[2]; F64P(P, wear3)[n] = c.wear[3];
+  F64P(P, imp)[n] = c.imp;
+  F64P(P, lt_start)[n] = c.lt_start; F64P(P, lt_cur)[n] = c.lt_cur; F64P(P, lt_last)[n] = c.lt_last;
+  F64P(P, lt_best)[n] = c.lt_best; F64P(P, lt_px)[n] = c.lt_px; F64P(P, lt_py)[n] = c.lt_py; F64P(P, lt_dist)[n] = c.lt_dist;
+  F64P(P, cum_impact)[n] = c.cum_impact; F64P(P, stuck_dur)[n] = c.stuck_dur;
+  F64P(P, stuck_sx)[n] = c.stuck_sx; F64P(P, stuck_sy)[n] = c.stuck_sy;
+  F64P(P, prev_px)[n] = c.prev_px; F64P(P, prev_py)[n] = c.prev_py;
+  F64P(P, prog_hist)[n] = c.prog_hist; F64P(P, back)[n] = c.back; F64P(P, prev_back)[n] = c.prev_back;
+  F64P(P, imp_at_obs)[n] = c.imp_at_obs;
+  I32P(P, awake)[n] = c.awake; I32P(P, nct)[n] = c.nct; I32P(P, overflow)[n] = c.overflow;
+  I32P(P, acc_len)[n] = c.acc_len; I32P(P, acc_head)[n] = c.acc_head;
+  I32P(P, imp_present)[n] = c.imp_present; I32P(P, nact)[n] = c.nact;
+  I32P(P, lt_timing)[n] = c.lt_timing; I32P(P, lt_has_last)[n] = c.lt_has_last; I32P(P, lt_has_best)[n] = c.lt_has_best;
+  I32P(P, lt_crossed)[n] = c.lt_crossed; I32P(P, lt_has_pos)[n] = c.lt_has_pos; I32P(P, lt_laps)[n] = c.lt_laps;
+  I32P(P, disabled)[n] = c.disabled; I32P(P, has_stuck_start)[n] = c.has_stuck_start;
+  I32P(P, first_step)[n] = c.first_step; I32P(P, prev_laps)[n] = c.prev_laps;
+}
+
+// ------------------------------------------------------------------ tyres (src/tyre.py, src/tyre_manager.py)
+__device__ inline double tyre_grip(double T, double wear) {
+  double tg;
+  if (85.0 <= T && T <= 105.0) tg = 1.5;
+  else {
+    double dev = T < 85.0 ? 85.0 - T : T - 105.0;
+    double g = 1.5 - dev * 0.02;
+    tg = pymax(0.8, g);
+  }
+  double wf = 1.0 - (wear / 100.0) * (1.0 - 0.5);
+  return tg * wf;
+}
+__device__ inline double total_grip(const Car& c) {
+  double tg = 0.0, tw = 0.0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) { tg += tyre_grip(c.temp[i], c.wear[i]) * c.load[i]; tw += c.load[i]; }
+  return tw > 0 ? tg / tw : 0.0;
+}
+__device__ inline void tyre_update(Car& c, int i, double dt, double load, double ff, double speed, double lat, double slip) {
+  c.load[i] = load;
+  double ns = pymin(speed / CAR_MAX_SPEED_MS, 2.0);
+  double sf = 1.0 + P2(ns);
+  double fp = fabs(ff) * 0.040 * sf;
+  double ah = 0.0;
+  if (speed > 50.0) ah = P2(speed) * 0.0002;
+  double th = (fp + ah) * dt / 125.0;
+  double td = c.temp[i] - 25.0;
+  double ce = 0.01;
+  if (speed > 50.0) { double cr = pymin(0.8, speed / 100.0); ce *= (1.0 - cr * 0.5); }
+  double cool = td * ce;
+  double tdec = cool * dt;
+  c.temp[i] += th - tdec;
+  c.temp[i] = pymax(25.0, pymin(120.0, c.temp[i]));
+  double T = c.temp[i];
+  double fwr = fabs(ff) * 0.00001;
+  double tm;
+  if (85.0 <= T && T <= 105.0) tm = 1.0;
+  else if (T > 105.0) tm = 1.0 + ((T - 105.0) / 20.0);
+  else tm = 1.0 + ((85.0 - T) / 30.0);
+  double lf = load / STATIC_LOAD_PER_TYRE;
+  double lm = pymax(0.5, lf);
+  double wf = pymax(1.0, T / 80.0);
+  double skmh = speed * 3.6;
+  double swf = 1.0 + (skmh / 400.0) * 3.0;
+  swf = pymin(swf, 3.0);
+  double lat_g = fabs(lat) / 9.81;
+  double cwf;
+  if (lat_g > 2.0) { double ex = lat_g - 2.0; cwf = 1.0 + (ex * 1.5); cwf = pymin(cwf, 2.5); }
+  else cwf = 1.0;
+  double slwf = 1.0 + (fabs(slip) / 45.0) * (3.0 - 1.0);
+  slwf = pymin(slwf, 3.0);
+  double tot = tm * lm * wf * swf * cwf * slwf;
+  double rate = fwr * tot;
+  c.wear[i] += rate * dt;
+  c.wear[i] = pymin(100.0, c.wear[i]);
+}
+__device__ inline void weight_transfer(double lon, double lat, double speed, double out[4]) {
+  double sw = CAR_MASS * GRAVITY_MS2, sfl = sw * 0.5, srl = sw * 0.5;
+  double aero = 0.0;
+  if (speed > 50.0) {
+    double sf = P2(speed / 50.0);
+    double calc = 0.12 * sf * CAR_MASS * GRAVITY_MS2;
+    double mx = 1.5 * CAR_MASS * GRAVITY_MS2;
+    aero = pymin(calc, mx);
+  }
+  double ar = aero * 0.6, af = aero * (1.0 - 0.6);
+  double bf = sfl + af, br = srl + ar, te = sw + aero;
+  double rl = lon * te * 0.02;
+  double mf = bf * 0.95, mb = br * 0.95;
+  double lt = rl > 0 ? pymin(rl, mf) : pymax(rl, -mb);
+  double ft = bf - lt, rt = br + lt;
+  double rlat = lat * te * 0.01;
+  double mltf = (ft / 2.0) - 200.0, mltr = (rt / 2.0) - 200.0;
+  double mlt = pymin(mltf, mltr);
+  double latt = mlt > 0 ? pymax(-mlt, pymin(mlt, rlat)) : 0.0;
+  double raw[4] = {ft / 2.0 - latt / 2.0, ft / 2.0 + latt / 2.0, rt / 2.0 - latt / 2.0, rt / 2.0 + latt / 2.0};
+  double con[4], deficit = 0.0, excess = 0.0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    if (raw[i] < 50.0) { con[i] = 50.0; deficit += 50.0 - raw[i]; }
+    else { con[i] = raw[i]; excess += raw[i] - 50.0; }
+  }
+  if (deficit > 0.0 && excess > 0.0) {
+    double fct = deficit / excess;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      if (raw[i] >= 50.0) { double e = con[i] - 50.0; out[i] = pymax(50.0, con[i] - e * fct); }
+      else out[i] = con[i];
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) out[i] = con[i];
+  }
+}
+__device__ inline void lateral_heating(const Car& c, double ff[4], double speed) {
+  if (speed < 2.0) return;
+  double shm = 1.0;
+  if (c.slip > 5.0) { double ex = c.slip - 5.0; shm = 2.2 + (0.04 * P2(ex)); shm = pymin(shm, 8.0); }
+  double base = c.lfm * 0.05 * shm;
+  double flh = base * 0.5 / 2.0, rlh = base * 0.5 / 2.0;
+  if (fabs(c.steer) > 0.01 && speed > 3.0) {
+    int of, orr, inf, inr;
+    if (c.steer < 0) { of = 0; orr = 2; inf = 1; inr = 3; }
+    else { of = 1; orr = 3; inf = 0; inr = 2; }
+    double ofb = c.load[of] * 0.001, orb = c.load[orr] * 0.001;
+    ff[of] += flh * 1.5 + ofb;
+    ff[orr] += rlh * 1.5 + orb;
+    ff[inf] += flh * 0.5;
+    ff[inr] += rlh * 0.5;
+  } else { ff[0] += flh; ff[1] += flh; ff[2] += rlh; ff[3] += rlh; }
+}
+__device__ inline void update_friction(Car& c, double df) {
+  double speed = (double)vlen(c.v);
+  double rear, front;
+  if (c.thr > 0.01 && speed > 50.0) { double fa = pymin(0.3, speed / 200.0); rear = df * (1.0 - fa); front = df * fa / 2.0; }
+  else { rear = c.thr > 0.01 ? df : 0.0; front = 0.0; }
+  double bf = 0.0;
+  if (c.brk > 0.01) {
+    double mbf = CAR_MASS * 14.0 * c.brk, base = mbf / 4.0;
+    if (speed <= 1.0) { double sf = 0.05 + (1.0 - 0.05) * (speed / 1.0); bf = base * sf; }
+    else bf = base;
+  }
+  double rf = 0.0;
+  if (speed > 0.1) rf = ROLLING_RESISTANCE_FORCE / 4.0;
+  double ff[4] = {front + bf + rf, front + bf + rf, rear / 2.0 + bf + rf, rear / 2.0 + bf + rf};
+  lateral_heating(c, ff, speed);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) c.fric[i] = ff[i];
+}
+__device__ __forceinline__ V2 OV(double x, double y) { return V((float)x, (float)y); }
+
+// Car.update_physics (src/car.py:329-387) and helpers (:389-892)
+__device__ inline void car_update_physics(const Params& P, Car& c, int n, const TrackDev& T) {
+  const double dt = P.dt_d;
+  c.thr = c.thr_in; c.brk = c.brk_in; c.steer = c.str_in * (45.0 * RAD_PER_DEG);
+  {
+    double target = 1000.0 + (800.0 * c.thr_in);
+    double diff = target - c.rpm;
+    c.rpm += diff * pymin(1.0, dt * 3000.0 / fabs(diff + 0.1));
+    c.rpm = pymax(600.0, pymin(9500.0, c.rpm));
+  }
+  V2 fwd = V(c.xf.q.c * 1.0f - c.xf.q.s * 0.0f, c.xf.q.s * 1.0f + c.xf.q.c * 0.0f);
+  {  // _apply_engine_force (:389-449)
+    double speed = (double)vlen(c.v);
+    double rpm = c.rpm < 1000.0 ? 1000.0 : (c.rpm > 9000.0 ? 9000.0 : c.rpm);
+    double tf = rpm <= 5500.0 ? 0.7 + 0.3 * (rpm - 1000.0) / (5500.0 - 1000.0) : 1.0 - 0.6 * (rpm - 5500.0) / (9000.0 - 5500.0);
+    double torque = CAR_MAX_TORQUE * tf * c.thr;
+    double wheel = torque * 7.5;
+    double tlf = wheel / 0.35;
+    double ef;
+    if (speed > 12.0) {
+      double plf = (CAR_MAX_POWER * c.thr) / speed;
+      if (speed <= 25.0) {
+        double nsd = (speed - 12.0) / (25.0 - 12.0);
+        double ex = 1.0 - exp(-2.0 * nsd);
+        double blend = pymax(0.05, pymin(0.75, ex));
+        ef = tlf * (1.0 - blend) + plf * blend;
+      } else ef = tlf * (1.0 - 0.75) + plf * 0.75;
+    } else ef = tlf;
+    double grip = total_grip(c);
+    double sfac = 1.0 - pymin(0.4, fabs(c.steer) * 1.5);
+    double mx = CAR_MASS * GRAVITY_MS2 * grip * sfac;
+    ef = pymin(ef, mx);
+    double Fx = ef * (double)fwd.x, Fy = ef * (double)fwd.y;
+    double rff = pymin(2000.0, fabs(ef) / 2.0);
+    update_friction(c, rff);
+    float lx = (float)(-CAR_WHEELBASE / 2), ly = 0.0f;
+    V2 pt = V((c.xf.q.c * lx - c.xf.q.s * ly) + c.xf.p.x, (c.xf.q.s * lx + c.xf.q.c * ly) + c.xf.p.y);
+    apply_force(c, OV(Fx, Fy), pt);
+  }
+  if (c.brk > 0.01) {  // _apply_brake_force (:451-469)
+    double sfac = 1.0 - pymin(0.3, fabs(c.steer) * 1.5);
+    double mbf = CAR_MASS * 14.0 * sfac;
+    double bf = mbf * c.brk;
+    double speed = (double)vlen(c.v);
+    if (speed > 0.1) {
+      double dx = -(double)c.v.x / speed, dy = -(double)c.v.y / speed;
+      apply_force_center(c, OV(bf * dx, bf * dy));
+      update_friction(c, 0.0);
+    }
+  }
+  {  // drag (:471-484)
+    double speed = (double)vlen(c.v);
+    if (speed > 0.1) {
+      double mag = DRAG_CONSTANT * speed * speed;
+      double dx = -(double)c.v.x / speed, dy = -(double)c.v.y / speed;
+      apply_force_center(c, OV(mag * dx, mag * dy));
+    }
+  }
+  {  // rolling (:486-500)
+    double speed = (double)vlen(c.v);
+    if (speed > 0.1) {
+      double rr = ROLLING_RESISTANCE_FORCE;
+      double dx = -(double)c.v.x / speed, dy = -(double)c.v.y / speed;
+      apply_force_center(c, OV(rr * dx, rr * dy));
+    }
+  }
+  double alon, alat;
+  {  // _get_acceleration (:832-892); history ring in HBM, summed oldest -> newest like Python's sum()
+    double cvx = c.v.x, cvy = c.v.y;
+    double ax = (cvx - c.pvx) / dt, ay = (cvy - c.pvy) / dt;
+    float rtx = c.xf.q.c * 0.0f - c.xf.q.s * 1.0f, rty = c.xf.q.s * 0.0f + c.xf.q.c * 1.0f;
+    double lon = ax * fwd.x + ay * fwd.y, lat = ax * rtx + ay * rty;
+    lon = pymax(-12.0, pymin(12.0, lon));
+    lat = pymax(-12.0, pymin(12.0, lat));
+    double* acc = P.acc;
+    const size_t N = P.N;
+    int slot;
+    if (c.acc_len == 10) { slot = c.acc_head; c.acc_head = (c.acc_head + 1) % 10; }
+    else { slot = (c.acc_head + c.acc_len) % 10; c.acc_len++; }
+    acc[(size_t)(2 * slot) * N + n] = lon; acc[(size_t)(2 * slot + 1) * N + n] = lat;
+    double s0 = 0.0, s1 = 0.0;
+    for (int k = 0; k < c.acc_len; ++k) {
+      int idx = (c.acc_head + k) % 10;
+      s0 += acc[(size_t)(2 * idx) * N + n]; s1 += acc[(size_t)(2 * idx + 1) * N + n];
+    }
+    alon = s0 / c.acc_len; alat = s1 / c.acc_len;
+    c.pvx = cvx; c.pvy = cvy;
+  }
+  {  // TyreManager.update (src/tyre_manager.py:78-97)
+    double speed = (double)vlen(c.v);
+    double loads[4];
+    weight_transfer(alon, alat, speed, loads);
+    double fr[4] = {c.fric[0], c.fric[1], c.fric[2], c.fric[3]};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) c.load[i] = loads[i];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) tyre_update(c, i, dt, loads[i], fr[i], speed, alat, c.slip);
+  }
+  {  // _apply_lateral_tire_forces (:635-700)
+    double speed = (double)vlen(c.v);
+    if (speed > 0.05) {
+      c.lfm = 0.0; c.slip = 0.0;
+      double cs = (double)vlen(c.v);
+      if (!(cs < 0.05)) {
+        double fx = fwd.x, fy = fwd.y;
+        double vnx = (double)c.v.x / cs, vny = (double)c.v.y / cs;
+        double cr = vnx * fy - vny * fx, dt_ = vnx * fx + vny * fy;
+        double sr = atan2(fabs(cr), dt_);
+        c.slip = fabs(sr) * DEG_PER_RAD;
+        double dvx = fx * cs, dvy = fy * cs;
+        double ex = dvx - (double)c.v.x, ey = dvy - (double)c.v.y;
+        double aff = CAR_MASS * 5.0;
+        double cx = ex * aff, cy = ey * aff;
+        double grip = total_grip(c);
+        double pbf = CAR_MASS * GRAVITY_MS2 * grip * 1.0;
+        double mf = pymin(30000.0 * grip, pbf);
+        double fm = PH(P2(cx) + P2(cy));
+        if (fm > mf) { double sc = mf / fm; cx = cx * sc; cy = cy * sc; fm = mf; }
+        c.lfm = fm;
+        apply_force_center(c, OV(cx, cy));
+      }
+    }
+  }
+  apply_torque(c, (float)(-(double)c.w * CAR_MASS * 4.0));   // _apply_angular_damping (:502-507)
+  if (!(fabs(c.bank) < 0.1)) {  // _apply_banking_forces (:509-566)
+    double speed = (double)vlen(c.v);
+    if (!(speed < 1.0)) {
+      // lateral assist per segment precomputed on the host with the reference's math.sin
+      double la = 0.0; bool found = false;
+      for (int k = 0; k < T.nseg; ++k) if (T.segs[k].banking == c.bank) { la = T.segs[k].la; found = true; break; }
+      if (!found) { double br = c.bank * RAD_PER_DEG; la = (CAR_MASS * 9.81) * sin(fabs(br)) * 0.3; }
+      if (!(fabs(la) < 1.0) && speed > 5.0) {
+        double vx = (double)c.v.x / speed, vy = (double)c.v.y / speed;
+        double fdx = -vy, fdy = vx;
+        double sg = copysign(1.0, c.bank);
+        apply_force_center(c, OV(fdx * la * sg, fdy * la * sg));
+      }
+    }
+  }
+  if (fabs(c.steer) > 0.01) {  // _apply_steering_torque (:568-584)
+    double speed = (double)vlen(c.v);
+    if (speed > 0.1) {
+      double dav = speed * tan(c.steer) / CAR_WHEELBASE;
+      double err = dav - (double)c.w;
+      apply_torque(c, (float)(err * CAR_MASS * 0.8));
+    }
+  }
+}
+
+// ------------------------------------------------------------------ track lookups
+__device__ inline double banking_at(const TrackDev& T, double px, double py) {
+  double best = INFINITY; int bi = -1;
+  for (int k = 0; k < T.nseg; ++k) {
+    const DSeg& s = T.segs[k];
+    double ll = P2(s.ex - s.sx) + P2(s.ey - s.sy), d;
+    if (ll == 0) d = sqrt(P2(px - s.sx) + P2(py - s.sy));
+    else {
+      double tt = ((px - s.sx) * (s.ex - s.sx) + (py - s.sy) * (s.ey - s.sy)) / ll;
+      tt = pymax(0.0, pymin(1.0, tt));
+      double qx = s.sx + tt * (s.ex - s.sx), qy = s.sy + tt * (s.ey - s.sy);
+      d = sqrt(P2(px - qx) + P2(py - qy));
+    }
+    if (d < best) { best = d; bi = k; }
+  }
+  return bi >= 0 ? T.segs[bi].banking : 0.0;
+}
+__device__ inline double track_progress(const TrackDev& T, double px, double py) {
+  double best = INFINITY; int bi = 0; double bx = 0, by = 0;
+  for (int k = 0; k < T.nseg; ++k) {
+    const DSeg& s = T.segs[k];
+    double dx = s.ex - s.sx, dy = s.ey - s.sy, ll = dx * dx + dy * dy, qx, qy;
+    if (ll < 1e-6) { qx = s.sx; qy = s.sy; }
+    else {
+      double tt = pymax(0.0, pymin(1.0, ((px - s.sx) * dx + (py - s.sy) * dy) / ll));
+      qx = s.sx + tt * dx; qy = s.sy + tt * dy;
+    }
+    double d2 = P2(px - qx) + P2(py - qy);
+    if (d2 < best) { best = d2; bi = k; bx = qx; by = qy; }
+  }
+  const DSeg& s = T.segs[bi];
+  return T.prefix[bi] + sqrt(P2(bx - s.sx) + P2(by - s.sy));
+}
+__device__ inline bool on_startline(const TrackDev& T, double px, double py) {
+  const DSeg& s = T.segs[T.startline];
+  double dx = s.ex - s.sx, dy = s.ey - s.sy, ll = dx * dx + dy * dy, d;
+  if (ll < 1e-6) d = sqrt(P2(px - s.sx) + P2(py - s.sy));
+  else {
+    double tt = pymax(0.0, pymin(1.0, ((px - s.sx) * dx + (py - s.sy) * dy) / ll));
+    double qx = s.sx + tt * dx, qy = s.sy + tt * dy;
+    d = sqrt(P2(px - qx) + P2(py - qy));
+  }
+  return d <= (s.width / 2.0);
+}
+// LapTimer.update (src/lap_timer.py:95-272)
+__device__ inline bool lap_update(const TrackDev& T, Car& c, double px, double py, double sim) {
+  if (c.lt_timing) c.lt_cur = sim - c.lt_start;
+  if (c.lt_has_pos) {
+    double dx = px - c.lt_px, dy = py - c.lt_py, d = sqrt(dx * dx + dy * dy);
+    if (d < 50.0) c.lt_dist += d;
+  }
+  bool done = false;
+  if (T.startline >= 0 && c.lt_has_pos) {
+    bool now = on_startline(T, px, py), before = on_startline(T, c.lt_px, c.lt_py);
+    if (now && !before) {
+      if (c.lt_crossed && c.lt_timing) {
+        double minlap = T.total_length > 0 ? T.total_length * 0.95 : 100.0;
+        if (c.lt_cur < 10.0) {
+        } else if (c.lt_dist < minlap) {
+        } else {
+          double ct = c.lt_cur;
+          c.lt_last = ct; c.lt_has_last = 1;
+          if (!c.lt_has_best || ct < c.lt_best) { c.lt_best = ct; c.lt_has_best = 1; }
+          c.lt_start = sim; c.lt_cur = 0.0; c.lt_timing = 1;
+          c.lt_laps += 1; c.lt_dist = 0.0;
+          done = true;
+        }
+      } else if (!c.lt_crossed) {
+        c.lt_crossed = 1; c.lt_timing = 1; c.lt_start = sim; c.lt_cur = 0.0; c.lt_dist = 0.0;
+      }
+    }
+  }
+  c.lt_px = px; c.lt_py = py; c.lt_has_pos = 1;
+  return done;
+}
+
+// ------------------------------------------------------------------ distance sensors (src/distance_sensor.py:71-117)
+// 16 rays x walls in LDS; a conservative bounding-circle cull skips walls the exact
+// b2PolygonShape::RayCast test provably rejects or cannot make the minimum.
+__device__ inline void sensor_rays(const LWall* W, int nw, V2 p1, double px, double py, double ang, float out[16]) {
+  V2 p2[16]; float dxf[16], dyf[16], best[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    double sa = -((double)i * (360.0 / 16) * RAD_PER_DEG) + ang;
+    double dx = cos(sa), dy = sin(sa);
+    p2[i] = OV(px + dx * 250.0, py + dy * 250.0);
+    dxf[i] = (float)dx; dyf[i] = (float)dy; best[i] = 2.0f;
+  }
+  const float MARGIN = 0.25f;
+  for (int j = 0; j < nw; ++j) {
+    const LWall wl = W[j];
+    float rx = wl.px - p1.x, ry = wl.py - p1.y;
+    float R = wl.rad + MARGIN;
+    if (rx * rx + ry * ry > (250.0f + R) * (250.0f + R)) continue;
+    Rot q; q.s = wl.qs; q.c = wl.qc;
+    V2 l1 = rmulT(q, V(p1.x - wl.px, p1.y - wl.py));
+    const float hx = wl.hx, hy = wl.hy;
+    // numerators of the 4 faces depend only on p1 (b2Dot(normal_i, vertex_i - p1))
+    const float n0 = 0.0f * ((-hx) - l1.x) + (-1.0f) * ((-hy) - l1.y);
+    const float n1 = 1.0f * (hx - l1.x) + 0.0f * ((-hy) - l1.y);
+    const float n2 = 0.0f * (hx - l1.x) + 1.0f * (hy - l1.y);
+    const float n3 = (-1.0f) * ((-hx) - l1.x) + 0.0f * (hy - l1.y);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      float tc = rx * dxf[i] + ry * dyf[i];
+      float perp = fabsf(rx * dyf[i] - ry * dxf[i]);
+      if (perp > R || tc < -R || (tc - R) > 250.0f * best[i]) continue;
+      V2 l2 = rmulT(q, V(p2[i].x - wl.px, p2[i].y - wl.py));
+      V2 d = vsub(l2, l1);
+      float lower = 0.0f, upper = 1.0f; int index = -1; bool ok = true;
+      const float num[4] = {n0, n1, n2, n3};
+      const float den[4] = {0.0f * d.x + (-1.0f) * d.y, 1.0f * d.x + 0.0f * d.y, 0.0f * d.x + 1.0f * d.y, (-1.0f) * d.x + 0.0f * d.y};
+#pragma unroll
+      for (int f = 0; f < 4; ++f) {
+        if (!ok) break;
+        if (den[f] == 0.0f) { if (num[f] < 0.0f) ok = false; }
+        else if (den[f] < 0.0f && num[f] < lower * den[f]) { lower = __fdiv_rn(num[f], den[f]); index = f; }
+        else if (den[f] > 0.0f && num[f] < upper * den[f]) { upper = __fdiv_rn(num[f], den[f]); }
+        if (upper < lower) ok = false;
+      }
+      if (ok && index >= 0 && lower < best[i]) best[i] = lower;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    double hd = best[i] <= 1.0f ? (double)best[i] * 250.0 : 250.0;
+    float d32 = (float)hd;
+    float v = __fdiv_rn(d32, 250.0f);
+    out[i] = v < 0.0f ? 0.0f : (v > 1.0f ? 1.0f : v);
+  }
+}
+
+// CarPhysics._check_wall_collision AABB query (src/car_physics.py:470-524)
+__device__ inline bool query_on_wall(const LWall* W, int nw, double px, double py, double radius) {
+  Aabb q; q.lo = V((float)(px - radius), (float)(py - radius)); q.hi = V((float)(px + radius), (float)(py + radius));
+  V2 center = V((float)px, (float)py);
+  for (int j = 0; j < nw; ++j) {
+    const LWall& wl = W[j];
+    if (!overlap(wall_fat(wl), q)) continue;
+    Xf xf = wall_xf(wl);
+    Poly p; make_box(&p, wl.hx, wl.hy);
+    V2 pl = rmulT(xf.q, vsub(center, xf.p));
+    bool inside = true;
+    for (int i = 0; i < 4; ++i) { if (vdot(p.n[i], vsub(pl, p.v[i])) > 0.0f) { inside = false; break; } }
+    if (inside) return true;
+    for (int i = 0; i < 4; ++i) {
+      V2 v = xmul(xf, p.v[i]);
+      double dx = px - (double)v.x, dy = py - (double)v.y;
+      if (PH(dx * dx + dy * dy) < radius) return true;
+    }
+  }
+  return false;
+}
+
+// CarEnv._get_multi_obs for one car (src/car_env.py:891-956)
+__device__ inline void car_obs(const Car& c, const LWall* W, int nw, float* o) {
+  double px = c.xf.p.x, py = c.xf.p.y, vx = c.v.x, vy = c.v.y, ang = c.a, av = c.w;
+  o[0] = (float)npclip(px / 10000.0, -1, 1); o[1] = (float)npclip(py / 10000.0, -1, 1);
+  o[2] = (float)npclip(vx / 111.1, -1, 1); o[3] = (float)npclip(vy / 111.1, -1, 1);
+  o[4] = (float)npclip(PH(P2(vx) + P2(vy)) / 111.1, 0, 1);
+  o[5] = (float)npclip(ang / PI_D, -1, 1); o[6] = (float)npclip(av / 10.0, -1, 1);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    o[7 + i] = (float)npclip(c.load[i] / MAX_TYRE_LOAD, 0, 1);
+    o[11 + i] = (float)npclip(c.temp[i] / 200.0, 0, 1);
+    o[15 + i] = (float)npclip(c.wear[i] / 100.0, 0, 1);
+  }
+  double ci = c.imp_present ? c.imp : 0.0, imp = 0.0, ca = 0.0;
+  if (!(ci < 100.0)) {   // CarPhysics.get_collision_data (src/car_physics.py:386-425)
+    imp = ci;
+    if (c.nact > 0) {
+      double na = atan2((double)c.act_n[1], (double)c.act_n[0]);
+      double a = na - (double)c.a;
+      while (a > PI_D) a -= 2 * PI_D;
+      while (a < -PI_D) a += 2 * PI_D;
+      ca = a;
+    }
+  }
+  o[19] = (float)npclip(imp / 50000.0, 0, 1); o[20] = (float)npclip(ca / PI_D, -1, 1);
+  o[21] = (float)npclip(c.cum_impact / 250000.0, 0, 1);
+  sensor_rays(W, nw, c.xf.p, px, py, ang, o + 22);
+}
+
+// ------------------------------------------------------------------ reset (src/car_env.py:316-535)
+__device__ inline void car_reset(const Params& P, Car& c, int n, bool fresh, const LWall* W, int nw, const TrackDev& T) {
+  V2 p = OV(P.start_x, P.start_y); float a = P.start_angle;
+  if (fresh) {   // Car() + CarPhysics(car, track): new b2World (src/car_physics.py:74-107)
+    c.xf.q = rot_set(a); c.xf.p = p;
+    c.c = xmul(c.xf, zero2()); c.a = a; c.c0 = c.c; c.a0 = a;
+    c.v = zero2(); c.w = 0.0f; c.sleep = 0.0f; c.awake = 1; c.invdt0 = 0.0f;
+    c.force = zero2(); c.torque = 0.0f; c.alpha0 = 0.0f;
+    Poly cp; make_box(&cp, CAR_HX, CAR_HY);
+    Aabb ab = poly_aabb(&cp, c.xf);
+    V2 r = V(AABB_EXT, AABB_EXT);
+    c.fat.lo = vsub(ab.lo, r); c.fat.hi = vadd(ab.hi, r);
+    c.nct = 0; c.overflow = 0; c.moved = 1;
+    find_new_contacts(c, W, nw);
+    c.bank = 0.0;
+  } else {       // CarPhysics.reset_car + Car.reset (src/car_physics.py:550-571, src/car.py:1027-1058)
+    set_transform(c, W, nw, p, c.a);
+    set_transform(c, W, nw, c.xf.p, a);
+    set_transform(c, W, nw, p, c.a);
+    set_transform(c, W, nw, c.xf.p, a);
+    c.v = zero2(); c.w = 0.0f;
+  }
+  c.rpm = 1000.0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) { c.temp[i] = 80.0; c.wear[i] = 0.0; c.load[i] = (CAR_MASS * GRAVITY_MS2 * 0.5) / 2.0; }
+  c.pvx = c.pvy = 0.0; c.acc_len = 0; c.acc_head = 0; c.lfm = 0.0; c.slip = 0.0;
+  c.nact = 0; c.imp_present = 0; c.imp = 0.0;
+  c.lt_timing = 0; c.lt_start = 0.0; c.lt_cur = 0.0; c.lt_has_last = c.lt_has_best = 0; c.lt_last = c.lt_best = 0.0;
+  c.lt_crossed = 0; c.lt_has_pos = 0; c.lt_px = c.lt_py = 0.0; c.lt_laps = 0; c.lt_dist = 0.0;
+  c.disabled = 0; c.just_disabled = 0; c.cum_impact = 0.0; c.stuck_dur = 0.0; c.has_stuck_start = 0;
+  c.stuck_sx = c.stuck_sy = 0.0;
+  c.prev_px = c.xf.p.x; c.prev_py = c.xf.p.y;
+  c.back = c.prev_back = 0.0; c.first_step = 1; c.prev_laps = 0; c.cum_reward = 0.0f; c.cum_reward_info = 0.0f;
+  c.prog_hist = track_progress(T, c.xf.p.x, c.xf.p.y);
+  c.imp_at_obs = 0.0;
+}
+
+// ------------------------------------------------------------------ the fused step
+extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+
+__device__ inline void stage_track(const TrackDev& T, LWall* sw) {
+  for (int j = threadIdx.x; j < T.nwall; j += blockDim.x) sw[j] = T.walls[j];
+}
+
+__global__ void __launch_bounds__(BLOCK) step_kernel(Params P, const void* actions, int discrete, float* obs, float* reward,
+                                                     uint8_t* car_flags, uint8_t* env_flags, int auto_reset, float* terminal_obs) {
+  LWall* sw = (LWall*)smem;
+  __shared__ int s_laps_old[BLOCK], s_dis_old[BLOCK], s_laps_new[BLOCK], s_dis_new[BLOCK], s_lapdone[BLOCK];
+  __shared__ int s_dis_final[BLOCK], s_below[BLOCK];
+  __shared__ int s_envdone[BLOCK / 1];
+  const int tid = threadIdx.x, C = P.C;
+  const int el = tid / C, car = tid - el * C;
+  const int slot = blockIdx.x * P.epb + el;
+  const int env = (el < P.epb) ? P.blk_env[slot] : -1;
+  const int n = env >= 0 ? env * C + car : 0;
+  const TrackDev T = P.tracks[P.blk_track[blockIdx.x]];
+  stage_track(T, sw);
+  __syncthreads();
+  const int nw = T.nwall;
+  Car c;
+  bool lapdone = false;
+  double sim = 0.0;
+  if (env >= 0) {
+    car_load(P, n, c);
+    sim = P.env_time[env];
+    s_laps_old[tid] = c.lt_laps; s_dis_old[tid] = c.disabled;
+    // actions (BaseEnv._convert_to_internal_action / _discrete_to_continuous, np.float32)
+    float tb, st;
+    if (discrete) {
+      int a = ((const int*)actions)[n];
+      tb = a == 1 ? 1.0f : (a == 2 ? -1.0f : 0.0f);
+      st = a == 3 ? -1.0f : (a == 4 ? 1.0f : 0.0f);
+    } else {
+      tb = ((const float*)actions)[2 * n]; st = ((const float*)actions)[2 * n + 1];
+    }
+    float a0, a1, a2 = st;
+    if (tb >= 0) { a0 = tb; a1 = 0.0f; } else { a0 = 0.0f; a1 = -tb; }
+    if (c.disabled) { a0 = 0.0f; a1 = 0.0f; a2 = 0.0f; }
+    c.thr_in = pymax(0.0, pymin(1.0, (double)a0));
+    c.brk_in = pymax(0.0, pymin(1.0, (double)a1));
+    c.str_in = pymax(-1.0, pymin(1.0, (double)a2));
+    car_update_physics(P, c, n, T);
+    b2_step(c, sw, nw, P.dt_f, P.friction);
+    c.bank = T.has_banking ? banking_at(T, c.xf.p.x, c.xf.p.y) : 0.0;
+    if (!c.disabled) {   // _run_single_physics_step (src/car_env.py:582-638)
+      double imp = c.imp_present ? c.imp : 0.0;
+      if (imp > 50000.0) { c.disabled = 1; c.just_disabled = 1; }
+      if (imp > 100.0) c.cum_impact += imp;
+      if (c.cum_impact > 250000.0 && !c.disabled) { c.disabled = 1; c.just_disabled = 1; }
+      double speed = (double)vlen(c.v);
+      if (speed < 0.5) c.stuck_dur = c.stuck_dur + P.dt_d;
+      else { c.stuck_dur = 0.0; c.has_stuck_start = 0; }
+    }
+    lapdone = lap_update(T, c, c.xf.p.x, c.xf.p.y, sim);
+    s_laps_new[tid] = c.lt_laps; s_dis_new[tid] = c.disabled; s_lapdone[tid] = lapdone;
+  }
+  __syncthreads();
+  // env pass 1: lap-reset pending (src/car_env.py:672-676 with _all_active_cars_completed_lap :1640-1669,
+  // evaluated in car order with cars > i not yet updated)
+  if (env >= 0 && car == 0) {
+    int pend = P.env_i32[E_PENDING * P.E + env];
+    if (P.reset_on_lap) {
+      const int b = tid;
+      for (int i = 0; i < C; ++i) {
+        if (!s_lapdone[b + i]) continue;
+        bool any = false, all = true;
+        for (int j = 0; j < C; ++j) {
+          int dis = j <= i ? s_dis_new[b + j] : s_dis_old[b + j];
+          int laps = j <= i ? s_laps_new[b + j] : s_laps_old[b + j];
+          if (dis) continue;
+          any = true;
+          if (laps < 1) all = false;
+        }
+        if (any && all) pend = 1;
+      }
+    }
+    P.env_i32[E_PENDING * P.E + env] = pend;
+  }
+  float o[38];
+  float rew = 0.0f;
+  if (env >= 0) {
+    // _check_and_disable_cars (src/car_env.py:805-888)
+    if (!c.disabled) {
+      double speed = (double)vlen(c.v);
+      if (speed < 0.5 && c.stuck_dur > 0) {
+        double px = c.xf.p.x, py = c.xf.p.y;
+        if (!c.has_stuck_start) { c.has_stuck_start = 1; c.stuck_sx = px; c.stuck_sy = py; }
+        double dx = px - c.stuck_sx, dy = py - c.stuck_sy;
+        double moved = PH(P2(dx) + P2(dy));
+        if (c.stuck_dur > 10.0) {
+          bool dis = false;
+          if (moved < 1.0) dis = true;
+          else if (c.stuck_dur > 15.0) dis = true;
+          if (dis) { c.disabled = 1; c.just_disabled = 1; }
+        }
+      } else { c.stuck_dur = 0.0; c.has_stuck_start = 0; }
+    }
+    car_obs(c, sw, nw, o);
+    // _calculate_multi_rewards (src/car_env.py:980-1113)
+    if (c.disabled && !c.just_disabled) rew = 0.0f;
+    else {
+      double r = c.just_disabled ? 10.0 : 0.0;
+      if (!c.disabled) r -= 0.05;
+      if (!c.disabled) { double imp = c.imp_present ? c.imp : 0.0; if (fabs(imp) > 0) r -= 0.5; }
+      double px = c.xf.p.x, py = c.xf.p.y;
+      double dx = px - c.prev_px, dy = py - c.prev_py;
+      r += PH(P2(dx) + P2(dy)) * 0.15;
+      c.prev_px = px; c.prev_py = py;
+      if (!c.first_step) {
+        double prog = track_progress(T, px, py);
+        double L = T.total_length, pd = prog - c.prog_hist;
+        if (pd > L / 2) pd -= L; else if (pd < -L / 2) pd += L;
+        if (pd < 0) {
+          c.back += fabs(pd);
+          if (c.back > 200.0 && !c.disabled) { c.disabled = 1; c.just_disabled = 1; }
+          if (c.back > 25.0) {
+            double ce = pymax(0.0, c.back - 25.0), pe = pymax(0.0, c.prev_back - 25.0);
+            double nb = ce - pe;
+            if (nb > 0) r -= nb * 0.05;
+          }
+        } else { c.back = 0.0; c.prev_back = 0.0; }
+        c.prog_hist = prog;
+      } else {
+        c.prog_hist = track_progress(T, px, py);
+        c.first_step = 0;
+      }
+      if (c.lt_laps > c.prev_laps) { r += 0.0 * (c.lt_laps - c.prev_laps); c.prev_laps = c.lt_laps; }
+      if (!c.disabled) c.prev_back = c.back;
+      rew = (float)r;
+    }
+    s_dis_final[tid] = c.disabled;
+    s_below[tid] = (!c.disabled && c.cum_reward < -250.0f) ? 1 : 0;
+  }
+  __syncthreads();
+  // env pass 2: termination (src/car_env.py:1115-1158, 791-794)
+  if (env >= 0 && car == 0) {
+    const double st = P.env_time[env] + P.dt_d;
+    P.env_time[env] = st;
+    int ndis = 0, active = 0, below = 0, term = 0, trunc = 0, reason = P.env_i32[E_REASON * P.E + env];
+    for (int j = 0; j < C; ++j) { ndis += s_dis_final[tid + j]; if (!s_dis_final[tid + j]) { active++; below += s_below[tid + j]; } }
+    if (ndis >= C) { term = 1; reason = 1; }
+    else if (active > 0 && below == active) { term = 1; reason = 2; }
+    else if (P.reset_on_lap && st > 60.0) { term = 1; reason = 3; }
+    else if (st > 180.0) { trunc = 1; reason = 4; }
+    if (P.env_i32[E_PENDING * P.E + env]) { P.env_i32[E_PENDING * P.E + env] = 0; term = 1; }
+    P.env_i32[E_REASON * P.E + env] = reason;
+    P.env_i32[E_TERMINATED * P.E + env] = term;
+    P.env_i32[E_TRUNCATED * P.E + env] = trunc;
+    int done = term | trunc;
+    s_envdone[el] = done;
+    if (env_flags) env_flags[env] = (uint8_t)((term ? EF_TERMINATED : 0) | (trunc ? EF_TRUNCATED : 0) |
+                                              ((auto_reset && done) ? EF_RESET : 0) | ((reason & 7) << 4));
+  }
+  __syncthreads();
+  if (env >= 0) {
+    c.imp_at_obs = c.imp_present ? c.imp : 0.0;
+    const bool collided = c.imp_at_obs != 0.0;
+    c.cum_reward_info = c.cum_reward;
+    c.imp = 0.0; c.imp_present = 1;                  // src/car_env.py:775-779
+    c.cum_reward = c.cum_reward + rew;                // float32 accumulation (NEP 50)
+    uint8_t flags = (uint8_t)((c.disabled ? CF_DISABLED : 0) | (c.just_disabled ? CF_JUST_DISABLED : 0) |
+                              (collided ? CF_COLLISION : 0) | (lapdone ? CF_LAP : 0) | (c.overflow ? CF_ERROR : 0));
+    c.just_disabled = 0;
+    reward[n] = rew;
+    if (car_flags) car_flags[n] = flags;
+    const bool reset_now = auto_reset && s_envdone[el];
+    float* orow = obs + (size_t)n * 38;
+    if (reset_now) {
+      if (terminal_obs) { float* t = terminal_obs + (size_t)n * 38; for (int i = 0; i < 38; ++i) t[i] = o[i]; }
+      car_reset(P, c, n, false, sw, nw, T);
+      car_obs(c, sw, nw, o);
+    } else if (terminal_obs) {
+      float* t = terminal_obs + (size_t)n * 38; for (int i = 0; i < 38; ++i) t[i] = o[i];
+    }
+    for (int i = 0; i < 38; ++i) orow[i] = o[i];
+    car_store(P, n, c);
+    if (reset_now && car == 0) {
+      P.env_time[env] = 0.0;
+      P.env_i32[E_PENDING * P.E + env] = 0; P.env_i32[E_REASON * P.E + env] = 0;
+      P.env_i32[E_TERMINATED * P.E + env] = 0; P.env_i32[E_TRUNCATED * P.E + env] = 0;
+    }
+  }
+}
+
+__global__ void __launch_bounds__(BLOCK) reset_kernel(Params P, const uint8_t* mask, float* obs) {
+  LWall* sw = (LWall*)smem;
+  const int tid = threadIdx.x, C = P.C;
+  const int el = tid / C, car = tid - el * C;
+  const int slot = blockIdx.x * P.epb + el;
+  int env = (el < P.epb) ? P.blk_env[slot] : -1;
+  if (env >= 0 && mask && !mask[env]) env = -1;
+  const TrackDev T = P.tracks[P.blk_track[blockIdx.x]];
+  stage_track(T, sw);
+  __syncthreads();
+  if (env >= 0) {
+    const int n = env * C + car;
+    const bool fresh = P.env_i32[E_CREATED * P.E + env] == 0;
+    Car c;
+    car_load(P, n, c);
+    car_reset(P, c, n, fresh, sw, T.nwall, T);
+    float o[38];
+    car_obs(c, sw, T.nwall, o);
+    for (int i = 0; i < 38; ++i) obs[(size_t)n * 38 + i] = o[i];
+    car_store(P, n, c);
+  }
+  __syncthreads();   // every lane of an env has read E_CREATED before its car 0 writes it
+  if (env >= 0 && car == 0) {
+    P.env_time[env] = 0.0;
+    P.env_i32[E_CREATED * P.E + env] = 1; P.env_i32[E_PENDING * P.E + env] = 0; P.env_i32[E_REASON * P.E + env] = 0;
+    P.env_i32[E_TERMINATED * P.E + env] = 0; P.env_i32[E_TRUNCATED * P.E + env] = 0;
+  }
+}
+
+__global__ void __launch_bounds__(BLOCK) info_kernel(Params P, double* info) {
+  LWall* sw = (LWall*)smem;
+  const int tid = threadIdx.x, C = P.C;
+  const int el = tid / C, car = tid - el * C;
+  const int slot = blockIdx.x * P.epb + el;
+  const int env = (el < P.epb) ? P.blk_env[slot] : -1;
+  const TrackDev T = P.tracks[P.blk_track[blockIdx.x]];
+  stage_track(T, sw);
+  __syncthreads();
+  if (env < 0) return;
+  const int n = env * C + car;
+  Car c;
+  car_load(P, n, c);
+  double* o = info + (size_t)n * N_INFO;
+  o[INFO_X] = c.xf.p.x; o[INFO_Y] = c.xf.p.y; o[INFO_VX] = c.v.x; o[INFO_VY] = c.v.y; o[INFO_ANGLE] = c.a; o[INFO_OMEGA] = c.w;
+  o[INFO_SPEED] = (double)vlen(c.v); o[INFO_LAP_COUNT] = c.lt_laps;
+  o[INFO_LAST_LAP] = c.lt_has_last ? c.lt_last : NAN; o[INFO_BEST_LAP] = c.lt_has_best ? c.lt_best : NAN;
+  o[INFO_IS_TIMING] = c.lt_timing; o[INFO_CUR_LAP_TIME] = c.lt_cur; o[INFO_LAP_DIST] = c.lt_dist;
+  o[INFO_HAS_CROSSED] = c.lt_crossed; o[INFO_DISABLED] = c.disabled; o[INFO_CUM_REWARD] = c.cum_reward_info;
+  o[INFO_CUM_IMPACT] = c.cum_impact;
+  o[INFO_ON_TRACK] = query_on_wall(sw, T.nwall, c.xf.p.x, c.xf.p.y, 0.5) ? 0.0 : 1.0;
+  o[INFO_RPM] = c.rpm; o[INFO_SIM_TIME] = P.env_time[env]; o[INFO_NCT] = c.nct; o[INFO_ERROR] = c.overflow;
+}
+
+// ------------------------------------------------------------------ synthetic action sources (bench)
+__device__ __forceinline__ uint32_t mix32(uint64_t x) {   // splitmix64 finaliser
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  x ^= x >> 31;
+  return (uint32_t)(x >> 32);
+}
+__global__ void policy_kernel(int N, int policy, uint64_t seed, int64_t step, const float* obs, float* act, float* ctl) {
+  const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= N) return;
+  if (policy == 0) {
+    uint64_t key = (seed * 0x100000001B3ull) ^ ((uint64_t)n << 24) ^ (uint64_t)step * 0x9E3779B1ull;
+    act[2 * n] = (float)(mix32(key) >> 8) * (2.0f / 16777216.0f) - 1.0f;
+    act[2 * n + 1] = (float)(mix32(key ^ 0xABCDEF12345ull) >> 8) * (2.0f / 16777216.0f) - 1.0f;
+    return;
+  }
+  // BaseController._fallback_control (game/control/base_controller.py:39-103); state per car in ctl[4*n..]
+  const float* o = obs + (size_t)n * 38;
+  float* s = ctl + 4 * (size_t)n;   // throttle_brake, steering, last_forward, speed_limit
+  float fwd = o[22], spd = o[4];
+  if (s[2] >= fwd) s[3] = fwd;
+  if (s[2] < fwd) s[3] = 1.0f;
+  if (spd < s[3] * 0.95f) s[0] += 0.1f;
+  if (spd > s[3] * 1.05f) s[0] -= 0.1f;
+  float r = o[22 + 15], l = o[22 + 1];
+  if (r > l) s[1] = 1.0f - (l / r);
+  else if (l > r) s[1] = (1.0f - (r / l)) * -1.0f;
+  else s[1] *= 0.9f;
+  if (fabsf(s[1]) > 0.25f) s[0] *= 0.5f;
+  s[0] = fmaxf(fminf(s[0], 1.0f), -1.0f); s[1] = fmaxf(fminf(s[1], 1.0f), -1.0f);
+  s[2] = fwd;
+  act[2 * n] = s[0]; act[2 * n + 1] = s[1];
+}
+
+// =================================================================== host side / C ABI
+static thread_local std::string g_err;
+static int fail(const char* fmt, ...) {
+  char buf[512];
+  va_list ap; va_start(ap, fmt); vsnprintf(buf, sizeof buf, fmt, ap); va_end(ap);
+  g_err = buf;
+  return -1;
+}
+#define HIPCHK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) return fail("%s failed: %s", #x, hipGetErrorString(e_)); } while (0)
+
+struct HostTrack {
+  std::vector<LWall> walls; std::vector<DSeg> segs; std::vector<double> prefix;
+  double total_length; int startline, has_banking;
+  LWall* d_walls = nullptr; DSeg* d_segs = nullptr; double* d_prefix = nullptr;
+};
+
+struct NascarHandle {
+  NascarConfig cfg;
+  int N, E, C, epb;
+  void* arena = nullptr; size_t arena_bytes = 0;
+  size_t off_f32, off_f64, off_i32, off_acc, off_ct, off_key, off_n, off_time, off_ei32;
+  std::vector<HostTrack> tracks;
+  TrackDev* d_tracks = nullptr;
+  int* d_blk_track = nullptr; int* d_blk_env = nullptr; int nblocks = 0;
+  std::vector<int> env_track;
+  float* d_ctl = nullptr;    // rule-driver state for nascar_policy_actions
+  size_t max_lds = 0;
+  bool dirty_tracks = true;
+};
+
+static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+extern "C" const char* nascar_last_error(void) { return g_err.c_str(); }
+
+extern "C" int nascar_create(const NascarConfig* cfg, NascarHandle** out) {
+  if (!cfg || !out) return fail("null argument");
+  if (cfg->num_envs < 1) return fail("num_envs must be >= 1");
+  if (cfg->num_cars < 1 || cfg->num_cars > 64) return fail("num_cars must be in [1, 64]");
+  HIPCHK(hipSetDevice(cfg->device));
+  NascarHandle* h = new NascarHandle();
+  h->cfg = *cfg;
+  h->E = cfg->num_envs; h->C = cfg->num_cars; h->N = h->E * h->C;
+  h->epb = BLOCK / h->C;
+  size_t N = h->N, E = h->E, o = 0;
+  h->off_f32 = o; o = align256(o + sizeof(float) * N_F32 * N);
+  h->off_f64 = o; o = align256(o + sizeof(double) * N_F64 * N);
+  h->off_i32 = o; o = align256(o + sizeof(int) * N_I32 * N);
+  h->off_acc = o; o = align256(o + sizeof(double) * 20 * N);
+  h->off_ct = o; o = align256(o + sizeof(DContact) * MAXC * N);
+  h->off_key = o; o = align256(o + sizeof(int) * MAXC * N);
+  h->off_n = o; o = align256(o + sizeof(float) * 2 * MAXC * N);
+  h->off_time = o; o = align256(o + sizeof(double) * E);
+  h->off_ei32 = o; o = align256(o + sizeof(int) * N_EI32 * E);
+  h->arena_bytes = o;
+  hipError_t e = hipMalloc(&h->arena, o);
+  if (e != hipSuccess) { delete h; return fail("hipMalloc(%zu) failed: %s", o, hipGetErrorString(e)); }
+  hipMemset(h->arena, 0, o);
+  hipMalloc(&h->d_ctl, sizeof(float) * 4 * N);
+  hipMemset(h->d_ctl, 0, sizeof(float) * 4 * N);
+  h->env_track.assign(E, 0);
+  *out = h;
+  return 0;
+}
+
+extern "C" void nascar_destroy(NascarHandle* h) {
+  if (!h) return;
+  hipFree(h->arena); hipFree(h->d_ctl);
+  for (auto& t : h->tracks) { hipFree(t.d_walls); hipFree(t.d_segs); hipFree(t.d_prefix); }
+  hipFree(h->d_tracks); hipFree(h->d_blk_track); hipFree(h->d_blk_env);
+  delete h;
+}
+
+// wall table exactly as Box2D sees it (float32 transform via glibc sinf/cosf, fat AABB, key)
+extern "C" int nascar_add_track(NascarHandle* h, const double* segments, int32_t nseg, double total_length,
+                                const double* walls, int32_t nwall) {
+  if (!h || !segments || !walls) return fail("null argument");
+  if (nseg < 1 || nseg > MAX_SEG) return fail("segment count %d out of range", nseg);
+  if (nwall < 1) return fail("track has no walls");
+  HostTrack t;
+  t.total_length = total_length;
+  t.startline = -1; t.has_banking = 0;
+  double pre = 0.0;
+  for (int k = 0; k < nseg; ++k) {
+    const double* s = segments + 13 * k;
+    DSeg d;
+    d.sx = s[2]; d.sy = s[3]; d.ex = s[4]; d.ey = s[5]; d.width = s[6]; d.banking = s[12];
+    double br = d.banking * (M_PI / 180.0);
+    d.la = (1500.0 * 9.81) * sin(fabs(br)) * 0.3;     // src/car.py:527-533
+    d.chord = sqrt(pow(d.ex - d.sx, 2.0) + pow(d.ey - d.sy, 2.0));
+    t.prefix.push_back(pre);
+    pre += d.chord;
+    t.segs.push_back(d);
+    if (t.startline < 0 && (int)s[0] == 1) t.startline = k;
+    if (fabs(d.banking) >= 0.1) t.has_banking = 1;
+  }
+  std::unordered_map<std::string, int> keys;
+  for (int j = 0; j < nwall; ++j) {
+    const double* w = walls + 4 * j;
+    LWall L;
+    memset(&L, 0, sizeof L);
+    L.px = (float)w[0]; L.py = (float)w[1]; L.ang = (float)w[2];
+    L.qs = sinf(L.ang); L.qc = cosf(L.ang);
+    L.hx = (float)w[3]; L.hy = (float)(1.0 / 2);
+    L.rad = sqrtf(L.hx * L.hx + L.hy * L.hy) + 0.02f;
+    float lx = 0, ly = 0, ux = 0, uy = 0;
+    const float vx[4] = {-L.hx, L.hx, L.hx, -L.hx}, vy[4] = {-L.hy, -L.hy, L.hy, L.hy};
+    for (int i = 0; i < 4; ++i) {
+      float x = (L.qc * vx[i] - L.qs * vy[i]) + L.px;
+      float y = (L.qs * vx[i] + L.qc * vy[i]) + L.py;
+      if (i == 0) { lx = ux = x; ly = uy = y; }
+      else { lx = x < lx ? x : lx; ly = y < ly ? y : ly; ux = ux > x ? ux : x; uy = uy > y ? uy : y; }
+    }
+    const float r = 2.0f * 0.005f;
+    L.flx = (lx - r) - 0.1f; L.fly = (ly - r) - 0.1f; L.fhx = (ux + r) + 0.1f; L.fhy = (uy + r) + 0.1f;
+    char kbuf[96];
+    snprintf(kbuf, sizeof kbuf, "wall_%.1f_%.1f", (double)L.px, (double)L.py);
+    auto it = keys.find(kbuf);
+    if (it == keys.end()) { int id = (int)keys.size(); keys.emplace(kbuf, id); L.key = id; }
+    else L.key = it->second;
+    t.walls.push_back(L);
+  }
+  size_t lds = sizeof(LWall) * t.walls.size();
+  if (lds > 150 * 1024) return fail("track has %d walls; LDS staging limit is %zu", nwall, (size_t)(150 * 1024 / sizeof(LWall)));
+  HIPCHK(hipMalloc(&t.d_walls, sizeof(LWall) * t.walls.size()));
+  HIPCHK(hipMemcpy(t.d_walls, t.walls.data(), sizeof(LWall) * t.walls.size(), hipMemcpyHostToDevice));
+  HIPCHK(hipMalloc(&t.d_segs, sizeof(DSeg) * t.segs.size()));
+  HIPCHK(hipMemcpy(t.d_segs, t.segs.data(), sizeof(DSeg) * t.segs.size(), hipMemcpyHostToDevice));
+  HIPCHK(hipMalloc(&t.d_prefix, sizeof(double) * t.prefix.size()));
+  HIPCHK(hipMemcpy(t.d_prefix, t.prefix.data(), sizeof(double) * t.prefix.size(), hipMemcpyHostToDevice));
+  h->tracks.push_back(t);
+  h->max_lds = std::max(h->max_lds, lds);
+  h->dirty_tracks = true;
+  return (int)h->tracks.size() - 1;
+}
+
+extern "C" int nascar_set_env_tracks(NascarHandle* h, const int32_t* env_track) {
+  if (!h || !env_track) return fail("null argument");
+  for (int e = 0; e < h->E; ++e) {
+    if (env_track[e] < 0 || env_track[e] >= (int)h->tracks.size()) return fail("env %d: bad track id %d", e, env_track[e]);
+    h->env_track[e] = env_track[e];
+  }
+  h->dirty_tracks = true;
+  return 0;
+}
+
+static int prepare(NascarHandle* h) {
+  if (h->tracks.empty()) return fail("no track loaded (nascar_add_track)");
+  if (!h->dirty_tracks) return 0;
+  std::vector<TrackDev> td;
+  for (auto& t : h->tracks) {
+    TrackDev d;
+    d.walls = t.d_walls; d.nwall = (int)t.walls.size(); d.segs = t.d_segs; d.nseg = (int)t.segs.size();
+    d.prefix = t.d_prefix; d.total_length = t.total_length; d.startline = t.startline; d.has_banking = t.has_banking;
+    td.push_back(d);
+  }
+  hipFree(h->d_tracks);
+  HIPCHK(hipMalloc(&h->d_tracks, sizeof(TrackDev) * td.size()));
+  HIPCHK(hipMemcpy(h->d_tracks, td.data(), sizeof(TrackDev) * td.size(), hipMemcpyHostToDevice));
+  // workgroups hold whole envs of one track: group envs by track, pad each group to a block
+  std::vector<int> blk_track, blk_env;
+  for (int tr = 0; tr < (int)h->tracks.size(); ++tr) {
+    std::vector<int> envs;
+    for (int e = 0; e < h->E; ++e) if (h->env_track[e] == tr) envs.push_back(e);
+    for (size_t i = 0; i < envs.size(); i += h->epb) {
+      blk_track.push_back(tr);
+      for (int k = 0; k < h->epb; ++k) blk_env.push_back(i + k < envs.size() ? envs[i + k] : -1);
+    }
+  }
+  h->nblocks = (int)blk_track.size();
+  hipFree(h->d_blk_track); hipFree(h->d_blk_env);
+  HIPCHK(hipMalloc(&h->d_blk_track, sizeof(int) * blk_track.size()));
+  HIPCHK(hipMalloc(&h->d_blk_env, sizeof(int) * blk_env.size()));
+  HIPCHK(hipMemcpy(h->d_blk_track, blk_track.data(), sizeof(int) * blk_track.size(), hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(h->d_blk_env, blk_env.data(), sizeof(int) * blk_env.size(), hipMemcpyHostToDevice));
+  h->dirty_tracks = false;
+  return 0;
+}
+
+static Params make_params(NascarHandle* h) {
+  Params P;
+  P.E = h->E; P.C = h->C; P.N = h->N; P.epb = h->epb; P.nblocks = h->nblocks; P.reset_on_lap = h->cfg.reset_on_lap;
+  P.dt_d = 1.0 / 60.0; P.dt_f = (float)P.dt_d;
+  P.friction = sqrtf(0.7f * 0.333f);
+  P.start_x = h->cfg.start_x; P.start_y = h->cfg.start_y; P.start_angle = (float)h->cfg.start_angle;
+  char* a = (char*)h->arena;
+  P.f32 = (float*)(a + h->off_f32); P.f64 = (double*)(a + h->off_f64); P.i32 = (int*)(a + h->off_i32);
+  P.acc = (double*)(a + h->off_acc); P.ct = (DContact*)(a + h->off_ct); P.act_key = (int*)(a + h->off_key);
+  P.act_n = (float*)(a + h->off_n); P.env_time = (double*)(a + h->off_time); P.env_i32 = (int*)(a + h->off_ei32);
+  P.blk_track = h->d_blk_track; P.blk_env = h->d_blk_env; P.tracks = h->d_tracks;
+  return P;
+}
+
+extern "C" int nascar_reset(NascarHandle* h, const uint8_t* env_mask, float* obs, void* stream) {
+  if (!h || !obs) return fail("null argument");
+  if (prepare(h)) return -1;
+  Params P = make_params(h);
+  hipLaunchKernelGGL(reset_kernel, dim3(h->nblocks), dim3(BLOCK), h->max_lds, (hipStream_t)stream, P, env_mask, obs);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+extern "C" int nascar_step(NascarHandle* h, const void* actions, int32_t discrete, float* obs, float* reward,
+                           uint8_t* car_flags, uint8_t* env_flags, int32_t auto_reset, float* terminal_obs, void* stream) {
+  if (!h || !actions || !obs || !reward) return fail("null argument");
+  if (prepare(h)) return -1;
+  Params P = make_params(h);
+  hipLaunchKernelGGL(step_kernel, dim3(h->nblocks), dim3(BLOCK), h->max_lds, (hipStream_t)stream, P, actions, discrete,
+                     obs, reward, car_flags, env_flags, auto_reset, terminal_obs);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+extern "C" int nascar_get_info(NascarHandle* h, double* info, void* stream) {
+  if (!h || !info) return fail("null argument");
+  if (prepare(h)) return -1;
+  Params P = make_params(h);
+  hipLaunchKernelGGL(info_kernel, dim3(h->nblocks), dim3(BLOCK), h->max_lds, (hipStream_t)stream, P, info);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+extern "C" int64_t nascar_state_bytes(NascarHandle* h) { return h ? (int64_t)h->arena_bytes : -1; }
+extern "C" int nascar_get_state(NascarHandle* h, void* dst, void* stream) {
+  if (!h || !dst) return fail("null argument");
+  HIPCHK(hipMemcpyAsync(dst, h->arena, h->arena_bytes, hipMemcpyDeviceToDevice, (hipStream_t)stream));
+  return 0;
+}
+extern "C" int nascar_set_state(NascarHandle* h, const void* src, void* stream) {
+  if (!h || !src) return fail("null argument");
+  HIPCHK(hipMemcpyAsync(h->arena, src, h->arena_bytes, hipMemcpyDeviceToDevice, (hipStream_t)stream));
+  return 0;
+}
+
+extern "C" int nascar_policy_actions(NascarHandle* h, int32_t policy, uint64_t seed, int64_t step, const float* obs,
+                                     float* actions, void* stream) {
+  if (!h || !actions) return fail("null argument");
+  if (policy == 1 && !obs) return fail("policy 1 needs obs");
+  int nb = (h->N + 255) / 256;
+  hipLaunchKernelGGL(policy_kernel, dim3(nb), dim3(256), 0, (hipStream_t)stream, h->N, policy, seed, step, obs, actions, h->d_ctl);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+// ------------------------------------------------------------------ test hook: b2Rot::Set numerics
+__global__ void sincos_kernel(const float* x, float* s, float* c, int n) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) { s[i] = dev_sinf(x[i]); c[i] = dev_cosf(x[i]); }
+}
+extern "C" int nascar_debug_sincosf(const float* x, float* s, float* c, int32_t n, void* stream) {
+  if (!x || !s || !c || n < 0) return fail("bad argument");
+  hipLaunchKernelGGL(sincos_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, x, s, c, n);
+  HIPCHK(hipGetLastError());
+  return 0;
+}

@@ -1032,4 +1032,3 @@ EXPORT void hb_set_angular_velocity(void *w_, float av) {
     if (av * av > 0.0f) { if (!w->awake) { w->awake = 1; w->sleepTime = 0.0f; } }
     w->w = av;
 }
-EXPORT void 

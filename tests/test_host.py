@@ -1,0 +1,51 @@
+"""CPU tests of the product's host side: track pipeline vs the reference's golden
+tables, loader error behaviour, and the C-ABI library exports."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+from golden_replay import GOLDEN, TRACKS
+from nascargymnasium_amd.track import build_walls, load_track
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+NAMES = sorted(f[:-6] for f in os.listdir(TRACKS) if f.endswith(".track"))
+
+
+@pytest.mark.parametrize("name", NAMES)
+def test_python_track_pipeline_bit_exact(name):
+    g = np.load(os.path.join(GOLDEN, "tracks.npz"))
+    t = load_track(os.path.join(TRACKS, name + ".track"))
+    assert np.array_equal(t.segment_table(), g[f"{name}__segments"])
+    assert t.total_length == float(g[f"{name}__total_length"])
+    assert np.array_equal(build_walls(t), g[f"{name}__walls"])
+
+
+def test_loader_errors(tmp_path):
+    with pytest.raises(FileNotFoundError):
+        load_track(str(tmp_path / "missing.track"))
+    p = tmp_path / "bad.track"
+    p.write_text("WIDTH 12\nGRID\nZIGZAG 3\n")
+    with pytest.raises(ValueError, match="Unknown command"):
+        load_track(str(p))
+    p.write_text("GRID\nLEFT 400 100\n")
+    with pytest.raises(ValueError, match="Curve angle"):
+        load_track(str(p))
+    p.write_text("grid  # comment\nstartline\nstraight 10 5 # banked\n")
+    t = load_track(str(p))
+    assert [s.segment_type for s in t.segments] == ["GRID", "STARTLINE", "STRAIGHT"]
+    assert t.segments[2].banking_angle == 5.0
+
+
+def test_capi_library_exports_every_declared_symbol():
+    from nascargymnasium_amd import _lib
+    if not os.path.exists(_lib.LIB_PATH):
+        _lib.build()
+    hdr = open(os.path.join(ROOT, "include", "nascar.h")).read()
+    declared = set(re.findall(r"\b(nascar_[a-z_]+)\s*\(", hdr))
+    assert declared == set(_lib.EXPORTED)
+    L = ctypes.CDLL(_lib.LIB_PATH)
+    for sym in declared:
+        assert hasattr(L, sym), sym
