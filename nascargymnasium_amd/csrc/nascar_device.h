@@ -76,11 +76,11 @@ __device__ __forceinline__ float vdot(V2 a, V2 b) { return a.x * b.x + a.y * b.y
 __device__ __forceinline__ float vcross(V2 a, V2 b) { return a.x * b.y - a.y * b.x; }
 __device__ __forceinline__ V2 vcross_vs(V2 a, float s) { return V(s * a.y, -s * a.x); }
 __device__ __forceinline__ V2 vcross_sv(float s, V2 a) { return V(-s * a.y, s * a.x); }
-__device__ __forceinline__ float vlen(V2 a) { return __fsqrt_rn(a.x * a.x + a.y * a.y); }
+__device__ __forceinline__ float vlen(V2 a) { return fsqrt_cr(a.x * a.x + a.y * a.y); }
 __device__ __forceinline__ float vnormalize(V2* a) {
   float length = vlen(*a);
   if (length < FLT_EPS) return 0.0f;
-  float inv = __fdiv_rn(1.0f, length);
+  float inv = fdiv_cr(1.0f, length);
   a->x *= inv; a->y *= inv;
   return length;
 }
@@ -285,7 +285,7 @@ __device__ inline int clip_segment(Clip vOut[2], const Clip vIn[2], V2 normal, f
   if (d0 <= 0.0f) vOut[numOut++] = vIn[0];
   if (d1 <= 0.0f) vOut[numOut++] = vIn[1];
   if (d0 * d1 < 0.0f) {
-    float interp = __fdiv_rn(d0, d0 - d1);
+    float interp = fdiv_cr(d0, d0 - d1);
     vOut[numOut].v = vadd(vIn[0].v, vmul(interp, vsub(vIn[1].v, vIn[0].v)));
     vOut[numOut].id = cf_key(vertexIndexA, (int)((vIn[0].id >> 8) & 255), 0, 1);
     ++numOut;
@@ -463,11 +463,11 @@ __device__ inline void cs_init_velocity(VC* vc, int n, const Car& c, const BodyS
       p.rA = vsub(pts[j], cA); p.rB = vsub(pts[j], cB);
       float rnA = vcross(p.rA, v.normal), rnB = vcross(p.rB, v.normal);
       float kNormal = mA + mB + iA * rnA * rnA + iB * rnB * rnB;
-      p.nm = kNormal > 0.0f ? __fdiv_rn(1.0f, kNormal) : 0.0f;
+      p.nm = kNormal > 0.0f ? fdiv_cr(1.0f, kNormal) : 0.0f;
       V2 tangent = vcross_vs(v.normal, 1.0f);
       float rtA = vcross(p.rA, tangent), rtB = vcross(p.rB, tangent);
       float kTangent = mA + mB + iA * rtA * rtA + iB * rtB * rtB;
-      p.tm = kTangent > 0.0f ? __fdiv_rn(1.0f, kTangent) : 0.0f;
+      p.tm = kTangent > 0.0f ? fdiv_cr(1.0f, kTangent) : 0.0f;
       p.vb = 0.0f;
       float vRel = vdot(v.normal, vsub(vsub(vadd(vB, vcross_sv(wB, p.rB)), vA), vcross_sv(wA, p.rA)));
       if (vRel < -VELOCITY_THRESHOLD) p.vb = -MIX_RESTITUTION * vRel;
@@ -483,7 +483,7 @@ __device__ inline void cs_init_velocity(VC* vc, int n, const Car& c, const BodyS
         v.K[0] = k11; v.K[1] = k12; v.K[2] = k12; v.K[3] = k22;
         float a = v.K[0], b = v.K[2], cc = v.K[1], d = v.K[3];
         float det = a * d - b * cc;
-        if (det != 0.0f) det = __fdiv_rn(1.0f, det);
+        if (det != 0.0f) det = fdiv_cr(1.0f, det);
         v.nm[0] = det * d; v.nm[2] = -det * b; v.nm[1] = -det * cc; v.nm[3] = det * a;
       } else {
         v.pointCount = 1;
@@ -617,7 +617,7 @@ __device__ inline int cs_solve_position(VC* vc, int n, BodyState& A, int toi) {
       float C = fclamp((toi ? TOI_BAUMGARTE : BAUMGARTE) * (sep + LINEAR_SLOP), -MAX_LINEAR_CORRECTION, 0.0f);
       float rnA = vcross(rA, normal), rnB = vcross(rB, normal);
       float K = mA + mB + iA * rnA * rnA + iB * rnB * rnB;
-      float impulse = K > 0.0f ? __fdiv_rn(-C, K) : 0.0f;
+      float impulse = K > 0.0f ? fdiv_cr(-C, K) : 0.0f;
       V2 P = vmul(impulse, normal);
       cA = vsub(cA, vmul(mA, P)); aA -= iA * vcross(rA, P);
       cB = vadd(cB, vmul(mB, P)); aB += iB * vcross(rB, P);
@@ -635,12 +635,12 @@ __device__ inline void integrate_positions(BodyState& A, float h) {
   V2 cc = A.c; float a = A.a; V2 v = A.v; float w = A.w;
   V2 translation = vmul(h, v);
   if (vdot(translation, translation) > MAX_TRANSLATION * MAX_TRANSLATION) {
-    float ratio = __fdiv_rn(MAX_TRANSLATION, vlen(translation));
+    float ratio = fdiv_cr(MAX_TRANSLATION, vlen(translation));
     v = vmul(ratio, v);
   }
   float rotation = h * w;
   if (rotation * rotation > MAX_ROTATION * MAX_ROTATION) {
-    float ratio = __fdiv_rn(MAX_ROTATION, fabsf(rotation));
+    float ratio = fdiv_cr(MAX_ROTATION, fabsf(rotation));
     w *= ratio;
   }
   cc = vadd(cc, vmul(h, v));
@@ -741,7 +741,7 @@ __device__ inline float gjk_distance(SCache& cache, const Poly* pA, Xf tA, const
       else {
         float d12_1 = vdot(w2, e12);
         if (d12_1 <= 0.0f) { s.v[1].a = 1.0f; s.count = 1; s.v[0] = s.v[1]; }
-        else { float inv = __fdiv_rn(1.0f, d12_1 + d12_2); s.v[0].a = d12_1 * inv; s.v[1].a = d12_2 * inv; s.count = 2; }
+        else { float inv = fdiv_cr(1.0f, d12_1 + d12_2); s.v[0].a = d12_1 * inv; s.v[1].a = d12_2 * inv; s.count = 2; }
       }
     } else if (s.count == 3) {
       V2 w1 = s.v[0].w, w2 = s.v[1].w, w3 = s.v[2].w;
@@ -755,15 +755,15 @@ __device__ inline float gjk_distance(SCache& cache, const Poly* pA, Xf tA, const
       float d123_1 = n123 * vcross(w2, w3), d123_2 = n123 * vcross(w3, w1), d123_3 = n123 * vcross(w1, w2);
       if (d12_2 <= 0.0f && d13_2 <= 0.0f) { s.v[0].a = 1.0f; s.count = 1; }
       else if (d12_1 > 0.0f && d12_2 > 0.0f && d123_3 <= 0.0f) {
-        float inv = __fdiv_rn(1.0f, d12_1 + d12_2); s.v[0].a = d12_1 * inv; s.v[1].a = d12_2 * inv; s.count = 2;
+        float inv = fdiv_cr(1.0f, d12_1 + d12_2); s.v[0].a = d12_1 * inv; s.v[1].a = d12_2 * inv; s.count = 2;
       } else if (d13_1 > 0.0f && d13_2 > 0.0f && d123_2 <= 0.0f) {
-        float inv = __fdiv_rn(1.0f, d13_1 + d13_2); s.v[0].a = d13_1 * inv; s.v[2].a = d13_2 * inv; s.count = 2; s.v[1] = s.v[2];
+        float inv = fdiv_cr(1.0f, d13_1 + d13_2); s.v[0].a = d13_1 * inv; s.v[2].a = d13_2 * inv; s.count = 2; s.v[1] = s.v[2];
       } else if (d12_1 <= 0.0f && d23_2 <= 0.0f) { s.v[1].a = 1.0f; s.count = 1; s.v[0] = s.v[1]; }
       else if (d13_1 <= 0.0f && d23_1 <= 0.0f) { s.v[2].a = 1.0f; s.count = 1; s.v[0] = s.v[2]; }
       else if (d23_1 > 0.0f && d23_2 > 0.0f && d123_1 <= 0.0f) {
-        float inv = __fdiv_rn(1.0f, d23_1 + d23_2); s.v[1].a = d23_1 * inv; s.v[2].a = d23_2 * inv; s.count = 2; s.v[0] = s.v[2];
+        float inv = fdiv_cr(1.0f, d23_1 + d23_2); s.v[1].a = d23_1 * inv; s.v[2].a = d23_2 * inv; s.count = 2; s.v[0] = s.v[2];
       } else {
-        float inv = __fdiv_rn(1.0f, d123_1 + d123_2 + d123_3);
+        float inv = fdiv_cr(1.0f, d123_1 + d123_2 + d123_3);
         s.v[0].a = d123_1 * inv; s.v[1].a = d123_2 * inv; s.v[2].a = d123_3 * inv; s.count = 3;
       }
     }
@@ -814,7 +814,7 @@ __device__ __forceinline__ Xf sweep_xf(const Sweep& s, float beta) {
 }
 __device__ __forceinline__ void sweep_normalize(Sweep& s) {
   float twoPi = 2.0f * B2_PI;
-  float d = twoPi * floorf(__fdiv_rn(s.a0, twoPi));
+  float d = twoPi * floorf(fdiv_cr(s.a0, twoPi));
   s.a0 -= d; s.a -= d;
 }
 
@@ -919,7 +919,7 @@ __device__ inline float time_of_impact(int* state, const Poly* pA, const Sweep& 
       float a1 = t1, a2 = t2;
       for (;;) {
         float t;
-        if (rootIterCount & 1) t = a1 + __fdiv_rn((target - s1) * (a2 - a1), s2 - s1);
+        if (rootIterCount & 1) t = a1 + fdiv_cr((target - s1) * (a2 - a1), s2 - s1);
         else t = 0.5f * (a1 + a2);
         ++rootIterCount;
         float s = sep_eval(fcn, pA, pB, indexA, indexB, t);
@@ -982,7 +982,7 @@ __device__ inline void solve_toi(Car& c, const LWall* W, int nw, float dt, float
     if (minC < 0 || 1.0f - 10.0f * FLT_EPS < minAlpha) break;
     V2 bc0 = c.c0, bc = c.c; float ba0 = c.a0, ba = c.a, balpha0 = c.alpha0;
     {
-      float beta = __fdiv_rn(minAlpha - c.alpha0, 1.0f - c.alpha0);
+      float beta = fdiv_cr(minAlpha - c.alpha0, 1.0f - c.alpha0);
       c.c0 = vadd(c.c0, vmul(beta, vsub(c.c, c.c0)));
       c.a0 += beta * (c.a - c.a0);
       c.alpha0 = minAlpha;
@@ -1023,7 +1023,7 @@ __device__ inline void solve_toi(Car& c, const LWall* W, int nw, float dt, float
 }
 
 __device__ inline void b2_step(Car& c, const LWall* W, int nw, float dt, float friction) {
-  float inv_dt = dt > 0.0f ? __fdiv_rn(1.0f, dt) : 0.0f;
+  float inv_dt = dt > 0.0f ? fdiv_cr(1.0f, dt) : 0.0f;
   float dtRatio = c.invdt0 * dt;
   collide(c, W);
   solve(c, W, nw, dt, dtRatio, friction);

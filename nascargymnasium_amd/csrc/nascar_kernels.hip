@@ -28,6 +28,14 @@ using namespace nascar;
 #define BLOCK 256
 #define MAX_SEG 64
 
+#ifdef NASCAR_DEBUG
+__device__ double* g_dbg = nullptr;   // debug build only: intermediate taps of one car
+__device__ int g_dbg_car = -1;
+#define DBG(n, slot, val) do { if ((n) == g_dbg_car && g_dbg) g_dbg[slot] = (double)(val); } while (0)
+#else
+#define DBG(n, slot, val) do { } while (0)
+#endif
+
 // ------------------------------------------------------------------ device-side tables
 struct DSeg {   // per segment, float64 (src/track_generator.py TrackSegment)
   double sx, sy, ex, ey, width, banking, la, chord;  // la: banking lateral assist (src/car.py:527-533)
@@ -282,6 +290,8 @@ __device__ inline void car_update_physics(const Params& P, Car& c, int n, const 
     double Fx = ef * (double)fwd.x, Fy = ef * (double)fwd.y;
     double rff = pymin(2000.0, fabs(ef) / 2.0);
     update_friction(c, rff);
+    DBG(n, 0, ef); DBG(n, 1, Fx); DBG(n, 2, Fy); DBG(n, 3, speed); DBG(n, 4, c.rpm); DBG(n, 5, total_grip(c));
+
     float lx = (float)(-CAR_WHEELBASE / 2), ly = 0.0f;
     V2 pt = V((c.xf.q.c * lx - c.xf.q.s * ly) + c.xf.p.x, (c.xf.q.s * lx + c.xf.q.c * ly) + c.xf.p.y);
     apply_force(c, OV(Fx, Fy), pt);
@@ -333,6 +343,8 @@ __device__ inline void car_update_physics(const Params& P, Car& c, int n, const 
       s0 += acc[(size_t)(2 * idx) * N + n]; s1 += acc[(size_t)(2 * idx + 1) * N + n];
     }
     alon = s0 / c.acc_len; alat = s1 / c.acc_len;
+    DBG(n, 6, alon); DBG(n, 7, alat);
+
     c.pvx = cvx; c.pvy = cvy;
   }
   {  // TyreManager.update (src/tyre_manager.py:78-97)
@@ -340,6 +352,8 @@ __device__ inline void car_update_physics(const Params& P, Car& c, int n, const 
     double loads[4];
     weight_transfer(alon, alat, speed, loads);
     double fr[4] = {c.fric[0], c.fric[1], c.fric[2], c.fric[3]};
+    DBG(n, 8, fr[0]); DBG(n, 9, fr[2]);
+
 #pragma unroll
     for (int i = 0; i < 4; ++i) c.load[i] = loads[i];
 #pragma unroll
@@ -364,12 +378,15 @@ __device__ inline void car_update_physics(const Params& P, Car& c, int n, const 
         double pbf = CAR_MASS * GRAVITY_MS2 * grip * 1.0;
         double mf = pymin(30000.0 * grip, pbf);
         double fm = PH(P2(cx) + P2(cy));
+        DBG(n, 10, cs); DBG(n, 11, cx); DBG(n, 12, cy); DBG(n, 13, fm); DBG(n, 14, c.slip);
+
         if (fm > mf) { double sc = mf / fm; cx = cx * sc; cy = cy * sc; fm = mf; }
         c.lfm = fm;
         apply_force_center(c, OV(cx, cy));
       }
     }
   }
+  DBG(n, 15, c.force.x); DBG(n, 16, c.force.y); DBG(n, 17, c.torque);
   apply_torque(c, (float)(-(double)c.w * CAR_MASS * 4.0));   // _apply_angular_damping (:502-507)
   if (!(fabs(c.bank) < 0.1)) {  // _apply_banking_forces (:509-566)
     double speed = (double)vlen(c.v);
@@ -512,8 +529,8 @@ __device__ inline void sensor_rays(const LWall* W, int nw, V2 p1, double px, dou
       for (int f = 0; f < 4; ++f) {
         if (!ok) break;
         if (den[f] == 0.0f) { if (num[f] < 0.0f) ok = false; }
-        else if (den[f] < 0.0f && num[f] < lower * den[f]) { lower = __fdiv_rn(num[f], den[f]); index = f; }
-        else if (den[f] > 0.0f && num[f] < upper * den[f]) { upper = __fdiv_rn(num[f], den[f]); }
+        else if (den[f] < 0.0f && num[f] < lower * den[f]) { lower = fdiv_cr(num[f], den[f]); index = f; }
+        else if (den[f] > 0.0f && num[f] < upper * den[f]) { upper = fdiv_cr(num[f], den[f]); }
         if (upper < lower) ok = false;
       }
       if (ok && index >= 0 && lower < best[i]) best[i] = lower;
@@ -523,7 +540,7 @@ __device__ inline void sensor_rays(const LWall* W, int nw, V2 p1, double px, dou
   for (int i = 0; i < 16; ++i) {
     double hd = best[i] <= 1.0f ? (double)best[i] * 250.0 : 250.0;
     float d32 = (float)hd;
-    float v = __fdiv_rn(d32, 250.0f);
+    float v = fdiv_cr(d32, 250.0f);
     out[i] = v < 0.0f ? 0.0f : (v > 1.0f ? 1.0f : v);
   }
 }
@@ -1145,3 +1162,11 @@ extern "C" int nascar_debug_sincosf(const float* x, float* s, float* c, int32_t 
   HIPCHK(hipGetLastError());
   return 0;
 }
+
+#ifdef NASCAR_DEBUG
+extern "C" int nascar_debug_tap(double* dev_buf, int32_t car) {
+  HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_dbg), &dev_buf, sizeof(dev_buf)));
+  HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_dbg_car), &car, sizeof(car)));
+  return 0;
+}
+#endif

@@ -16,6 +16,13 @@
 
 namespace nascar {
 
+// Correctly rounded float32 sqrt / divide (what x86 sqrtss / divss give Box2D).
+// On gfx950 `sqrtf` and `/` lower to the IEEE sequences (v_sqrt + fma fix-up,
+// v_div_scale/fmas/fixup); `__fsqrt_rn` lowers to a bare v_sqrt_f32 (~1 ulp),
+// which broke parity -- never use it here.
+__device__ __forceinline__ float fsqrt_cr(float x) { return sqrtf(x); }
+__device__ __forceinline__ float fdiv_cr(float a, float b) { return a / b; }
+
 struct SinCosTable {
   double sign[4], hpi_inv, hpi, c0, c1, s1, c2, s2, c3, s3, c4;
 };

@@ -41,6 +41,10 @@ static const double CAR_MAX_TORQUE = 820.0;
 #define DEG_PER_RAD (180.0 / PI_)       /* CPython math.degrees: x * (180/pi) */
 #define PHYS_DT (1.0 / 60.0)
 
+EXPORT double or_dbg[32];
+EXPORT int or_dbg_car = -1;
+static int g_cur_car = -2;
+#define ODBG(slot, val) do { if (g_cur_car == or_dbg_car) or_dbg[slot] = (double)(val); } while (0)
 static inline double pymin(double a, double b) { return b < a ? b : a; }
 static inline double pymax(double a, double b) { return b > a ? b : a; }
 static inline double npclip(double x, double lo, double hi) { return x < lo ? lo : (x > hi ? hi : x); }
@@ -470,6 +474,8 @@ static void car_update_physics(ocar *c, double dt) {
         double Fx = ef * fx, Fy = ef * fy;
         double rff = pymin(2000.0, fabs(ef) / 2.0);
         update_friction(c, rff);
+        ODBG(0, ef); ODBG(1, Fx); ODBG(2, Fy); ODBG(3, speed); ODBG(4, c->rpm); ODBG(5, total_grip(c));
+
         /* GetWorldPoint((-wheelbase/2, 0)) in float32 */
         float lx = (float)(-CAR_WHEELBASE / 2), ly = 0.0f;
         ov2 pt; pt.x = (w->xf.q.c * lx - w->xf.q.s * ly) + w->xf.p.x; pt.y = (w->xf.q.s * lx + w->xf.q.c * ly) + w->xf.p.y;
@@ -521,6 +527,8 @@ static void car_update_physics(ocar *c, double dt) {
         double s0 = 0.0, s1 = 0.0;
         for (int k = 0; k < c->acc_len; ++k) { int idx = (c->acc_head + k) % 10; s0 += c->acc[idx][0]; s1 += c->acc[idx][1]; }
         alon = s0 / c->acc_len; alat = s1 / c->acc_len;
+        ODBG(6, alon); ODBG(7, alat);
+
         c->pvx = cvx; c->pvy = cvy;
     }
     /* TyreManager.update (src/tyre_manager.py:78-97) */
@@ -529,6 +537,8 @@ static void car_update_physics(ocar *c, double dt) {
         double loads[4];
         weight_transfer(c, alon, alat, speed, loads);
         double fr[4]; memcpy(fr, c->fric, sizeof fr);
+        ODBG(8, fr[0]); ODBG(9, fr[2]);
+
         for (int i = 0; i < 4; ++i) c->load[i] = loads[i];
         for (int i = 0; i < 4; ++i) tyre_update(c, i, dt, loads[i], fr[i], speed, alat, c->slip);
     }
@@ -552,6 +562,8 @@ static void car_update_physics(ocar *c, double dt) {
                 double pbf = CAR_MASS * GRAVITY_MS2 * grip * 1.0;
                 double mf = pymin(30000.0 * grip, pbf);
                 double fm = pow(P2(cx) + P2(cy), 0.5);
+                ODBG(10, cs); ODBG(11, cx); ODBG(12, cy); ODBG(13, fm); ODBG(14, c->slip);
+
                 if (fm > mf) { double sc = mf / fm; cx = cx * sc; cy = cy * sc; fm = mf; }
                 c->lfm = fm;
                 ob_apply_force_center(w, OV(cx, cy));
@@ -559,6 +571,8 @@ static void car_update_physics(ocar *c, double dt) {
         }
     }
     /* _apply_angular_damping (:502-507) */
+    ODBG(15, w->force.x); ODBG(16, w->force.y); ODBG(17, w->torque);
+
     ob_apply_torque(w, (float)(-(double)w->w * CAR_MASS * 4.0));
     /* _apply_banking_forces (:509-566); the lateral assist per segment is host-precomputed
        in the product, here it is evaluated as the reference does */
@@ -794,7 +808,9 @@ static void env_step(oenv *e, int env, const float *act) {
         c->thr_in = pymax(0.0, pymin(1.0, (double)a0));
         c->brk_in = pymax(0.0, pymin(1.0, (double)a1));
         c->str_in = pymax(-1.0, pymin(1.0, (double)a2));
+        g_cur_car = env * C + k;
         car_update_physics(c, dt);
+        g_cur_car = -2;
         olistener L = { c, lis_begin, lis_end, lis_post };
         ob_step(&c->w, &t->W, &L, (float)dt, 6, 4);
         if (t->has_banking) c->bank = banking_at(t, c->w.xf.p.x, c->w.xf.p.y);
@@ -1031,4 +1047,19 @@ EXPORT void hb_set_angular_velocity(void *w_, float av) {
     oworld *w = w_;
     if (av * av > 0.0f) { if (!w->awake) { w->awake = 1; w->sleepTime = 0.0f; } }
     w->w = av;
+}
+
+/* full per-car state in the GPU arena field order (tests/gpu_state.py F32, F64, I32 lists) */
+EXPORT void or_car_state(void *h, int idx, double *o) {
+    oenv *e = h; ocar *c = &e->car[idx]; oworld *w = &c->w;
+    double v[] = {
+        w->c.x, w->c.y, w->a, w->v.x, w->v.y, w->w, w->xf.q.s, w->xf.q.c, w->xf.p.x, w->xf.p.y, w->sleepTime, w->inv_dt0,
+        w->fat.lo.x, w->fat.lo.y, w->fat.hi.x, w->fat.hi.y, c->cum_reward, c->cum_reward_info,
+        c->rpm, c->pvx, c->pvy, c->lfm, c->slip, c->bank, c->load[0], c->load[1], c->load[2], c->load[3],
+        c->temp[0], c->temp[1], c->temp[2], c->temp[3], c->wear[0], c->wear[1], c->wear[2], c->wear[3], c->imp,
+        c->lt_start, c->lt_cur, c->lt_last, c->lt_best, c->lt_px, c->lt_py, c->lt_dist, c->cum_impact, c->stuck_dur,
+        c->stuck_sx, c->stuck_sy, c->prev_px, c->prev_py, c->prog_hist, c->back, c->prev_back, c->imp_at_obs,
+        w->awake, w->nct, w->overflow, c->acc_len, c->acc_head, c->imp_present, c->nact, c->lt_timing, c->lt_has_last,
+        c->lt_has_best, c->lt_crossed, c->lt_has_pos, c->lt_laps, c->disabled, c->has_stuck_start, c->first_step, c->prev_laps };
+    memcpy(o, v, sizeof v);
 }

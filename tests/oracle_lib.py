@@ -121,3 +121,11 @@ class OracleEnv:
         o = np.zeros(len(INFO_FIELDS), np.float64)
         self.L.or_car_info(self.h, idx, _p(o, ctypes.c_double))
         return dict(zip(INFO_FIELDS, o.tolist()))
+
+
+def car_state(env, idx, n_fields=71):
+    L = lib()
+    L.or_car_state.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_double)]
+    o = np.zeros(n_fields, np.float64)
+    L.or_car_state(env.h, idx, _p(o, ctypes.c_double))
+    return o

@@ -1,0 +1,79 @@
+"""GPU-vs-oracle state diff: step both with the same seeded actions and report the
+first state fields that differ (run on the GPU box).  TEST INFRASTRUCTURE."""
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+import gpu_state  # noqa: E402
+from oracle_lib import OracleEnv, car_state, lib as olib  # noqa: E402
+from nascargymnasium_amd import _lib  # noqa: E402
+DBG_CAR = int(os.environ.get("DBG_CAR", "-1"))
+if DBG_CAR >= 0:
+    _lib.LIB_PATH = os.path.join(ROOT, "tools", "libnascar_dbg.so")
+from nascargymnasium_amd.batched import BatchedCarEnv  # noqa: E402
+import ctypes  # noqa: E402
+
+track = sys.argv[1] if len(sys.argv) > 1 else "daytona"
+E, C, steps = int(sys.argv[2]) if len(sys.argv) > 2 else 4, int(sys.argv[3]) if len(sys.argv) > 3 else 3, \
+    int(sys.argv[4]) if len(sys.argv) > 4 else 60
+path = os.path.join(ROOT, "nascargymnasium_amd", "tracks", track + ".track")
+names = gpu_state.F32 + gpu_state.F64 + gpu_state.I32
+env = BatchedCarEnv(E, C, path, device="cuda:0")
+orc = OracleEnv(path, E, C)
+env.reset(); orc.reset()
+if DBG_CAR >= 0:
+    gbuf = torch.zeros(32, dtype=torch.float64, device="cuda:0")
+    L = _lib.lib()
+    L.nascar_debug_tap.argtypes = [ctypes.c_void_p, ctypes.c_int32]
+    L.nascar_debug_tap(ctypes.c_void_p(gbuf.data_ptr()), DBG_CAR)
+    OL = olib()
+    ctypes.c_int.in_dll(OL, "or_dbg_car").value = DBG_CAR
+    obuf = (ctypes.c_double * 32).in_dll(OL, "or_dbg")
+rng = np.random.default_rng(0)
+shown = 0
+
+
+def diff(k, tag):
+    global shown
+    st = gpu_state.decode(env.get_state().cpu().numpy(), E * C)
+    for n in range(E * C):
+        o = car_state(orc, n, len(names))
+        bad = []
+        for i, f in enumerate(names):
+            g = float(st[f][n])
+            if not (g == o[i] or (np.isnan(g) and np.isnan(o[i]))):
+                bad.append((f, g, o[i]))
+        if bad:
+            print(f"[{tag} step {k}] car {n}: {len(bad)} fields differ")
+            for f, g, oo in bad[:12]:
+                print(f"    {f:16s} gpu {g!r:>24} ({float(g).hex()})  oracle {oo!r:>24} ({float(oo).hex()})")
+            shown += 1
+            if shown > 6:
+                sys.exit(0)
+            return True
+    return False
+
+
+diff(-1, "reset")
+for k in range(steps):
+    a = rng.uniform(-1, 1, (E, C, 2)).astype(np.float32)
+    go = env.step(torch.from_numpy(a).cuda())[0].cpu().numpy()
+    oo = orc.step(a)[0]
+    if DBG_CAR >= 0:
+        g = gbuf.cpu().numpy(); o = np.array(obuf[:])
+        print(f"--- taps car {DBG_CAR} step {k}")
+        for i in range(18):
+            flag = "" if (g[i] == o[i]) else "   <<<"
+            print(f"  {i:2d} gpu {g[i]!r:>26} oracle {o[i]!r:>26}{flag}")
+    if diff(k, "step") or not np.array_equal(go, oo):
+        bad = np.argwhere(go != oo)
+        print("obs mismatch idx", bad[:10].tolist())
+        for b in bad[:6]:
+            print("   ", tuple(b), go[tuple(b)], oo[tuple(b)])
+        break
+print("done")
