@@ -93,12 +93,12 @@ def main():
     for i in range(K):
         if args.policy == "uniform":
             ev[i][0].record()
-            env.step(acts[W + i], auto_reset=True)
+            env.launch_step(acts[W + i], auto_reset=True)
             ev[i][1].record()
         else:
             a = env.policy_actions(1, seed=rank, step=W + i)
             ev[i][0].record()
-            env.step(a, auto_reset=True)
+            env.launch_step(a, auto_reset=True)
             ev[i][1].record()
     torch.cuda.synchronize()
     if world > 1:

@@ -85,6 +85,14 @@ class BatchedCarEnv:
 
     def step(self, actions: torch.Tensor, auto_reset: bool = False, terminal_obs: bool = False):
         """CarEnv.step for all envs.  actions: float32 [E, C, 2] (continuous) or int32 [E, C] (discrete)."""
+        self.launch_step(actions, auto_reset, terminal_obs)
+        terminated = (self.env_flags & _lib.EF_TERMINATED) != 0
+        truncated = (self.env_flags & _lib.EF_TRUNCATED) != 0
+        return self.obs, self.reward, terminated, truncated
+
+    def launch_step(self, actions: torch.Tensor, auto_reset: bool = False, terminal_obs: bool = False):
+        """Enqueue exactly one step_kernel launch on the current stream (no other device work when
+        `actions` is already a contiguous float32/int32 tensor on this device)."""
         discrete = not actions.is_floating_point()
         a = actions.to(self.device, torch.int32 if discrete else torch.float32).contiguous()
         if a.numel() != self.N * (1 if discrete else 2):
@@ -93,9 +101,6 @@ class BatchedCarEnv:
             _lib.check(self.L.nascar_step(self.h, _ptr(a), int(discrete), _ptr(self.obs), _ptr(self.reward),
                                           _ptr(self.car_flags), _ptr(self.env_flags), int(auto_reset),
                                           _ptr(self.terminal_obs) if terminal_obs else None, _stream()))
-        terminated = (self.env_flags & _lib.EF_TERMINATED) != 0
-        truncated = (self.env_flags & _lib.EF_TRUNCATED) != 0
-        return self.obs, self.reward, terminated, truncated
 
     def info_tensor(self) -> torch.Tensor:
         """per-car info [E, C, N_INFO] float64 (fields: _lib.INFO_FIELDS)."""

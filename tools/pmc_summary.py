@@ -1,0 +1,84 @@
+"""Summarise a tools/profile_session.sh run.
+
+    python tools/pmc_summary.py <out_dir> <tag>
+
+Reads the rocprofv3 CSVs under <out_dir>/{kt,fetch,write}, and writes
+  profiles/<tag>_kernel_stats.csv     (rocprofv3 --stats summary, copied verbatim)
+  profiles/<tag>_pmc_step_kernel.json (per-launch FETCH_SIZE / WRITE_SIZE of step_kernel)
+  profiles/pmc_traffic.json           (read by bench.py for roofline.traffic)
+HBM bytes per launch = (2 * FETCH_SIZE + WRITE_SIZE) * 1024: FETCH_SIZE/WRITE_SIZE are in KiB and
+gfx950 FETCH_SIZE tallies half the bytes of a wide coalesced read (MI355X_MICROARCH.md "HBM").
+"""
+import csv
+import glob
+import json
+import os
+import shutil
+import sys
+from collections import defaultdict
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+KERNEL = "step_kernel"
+
+
+def _find(d, suffix):
+    hits = sorted(glob.glob(os.path.join(d, "**", "*" + suffix), recursive=True))
+    return hits[-1] if hits else None
+
+
+def _bench_line(log):
+    for line in open(log):
+        line = line.strip()
+        if line.startswith("{") and '"metric"' in line:
+            return json.loads(line)
+    return None
+
+
+def _per_dispatch(path, counter):
+    vals = defaultdict(float)
+    for row in csv.DictReader(open(path)):
+        if KERNEL not in row.get("Kernel_Name", "") or row.get("Counter_Name") != counter:
+            continue
+        vals[row["Dispatch_Id"]] += float(row["Counter_Value"])
+    return list(vals.values())
+
+
+def main():
+    out, tag = sys.argv[1], sys.argv[2]
+    prof = os.path.join(ROOT, "profiles")
+    os.makedirs(prof, exist_ok=True)
+    res = {"tag": tag}
+    stats = _find(os.path.join(out, "kt"), "kernel_stats.csv")
+    if stats:
+        shutil.copy(stats, os.path.join(prof, f"{tag}_kernel_stats.csv"))
+        for row in csv.DictReader(open(stats)):
+            if KERNEL in row["Name"]:
+                res["rocprof_avg_ns"] = float(row["AverageNs"])
+                res["rocprof_calls"] = int(row["Calls"])
+    b = _bench_line(os.path.join(out, "kt.log"))
+    if b:
+        res["bench_under_rocprof"] = b
+        cfg = b["config"]
+        res.update(envs=cfg["envs_per_gpu"], cars=cfg["cars_per_env"], track=cfg["track"])
+        res["bench_kernel_ms_events"] = b["roofline"]["kernel_ms"]
+    f = _find(os.path.join(out, "fetch"), "counter_collection.csv")
+    w = _find(os.path.join(out, "write"), "counter_collection.csv")
+    if f and w:
+        fv, wv = _per_dispatch(f, "FETCH_SIZE"), _per_dispatch(w, "WRITE_SIZE")
+        if fv and wv:
+            fetch_kb, write_kb = sum(fv) / len(fv), sum(wv) / len(wv)
+            res.update(fetch_size_kb=fetch_kb, write_size_kb=write_kb, dispatches=[len(fv), len(wv)],
+                       bytes_per_launch=(2 * fetch_kb + write_kb) * 1024.0,
+                       bytes_per_launch_uncorrected=(fetch_kb + write_kb) * 1024.0)
+            if "envs" in res:
+                res["bytes_per_car_step"] = res["bytes_per_launch"] / (res["envs"] * res["cars"])
+    json.dump(res, open(os.path.join(prof, f"{tag}_pmc_step_kernel.json"), "w"), indent=1)
+    if "bytes_per_launch" in res and "envs" in res:
+        json.dump({k: res[k] for k in ("envs", "cars", "track", "bytes_per_launch", "bytes_per_launch_uncorrected",
+                                       "fetch_size_kb", "write_size_kb", "tag")},
+                  open(os.path.join(prof, "pmc_traffic.json"), "w"), indent=1)
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main()
