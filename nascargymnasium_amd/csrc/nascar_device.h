@@ -16,6 +16,20 @@
 
 #pragma clang fp contract(off)
 
+#define BLOCK 256   // threads per workgroup of the per-car kernels
+
+#ifdef NASCAR_PROFILE
+// profile build only: per-wave s_memtime stamps at phase boundaries of step_kernel
+__device__ unsigned long long* g_prof = nullptr;
+#define PROF(ph) do { unsigned long long _t = __builtin_amdgcn_s_memtime(); \
+    if (g_prof && (threadIdx.x & 63) == 0) g_prof[((size_t)blockIdx.x * (BLOCK / 64) + threadIdx.x / 64) * 16 + (ph)] = _t; } while (0)
+#define PROF_RT(slot) do { unsigned long long _t = __builtin_amdgcn_s_memrealtime(); \
+    if (g_prof && (threadIdx.x & 63) == 0) g_prof[((size_t)blockIdx.x * (BLOCK / 64) + threadIdx.x / 64) * 16 + (slot)] = _t; } while (0)
+#else
+#define PROF(ph) do { } while (0)
+#define PROF_RT(slot) do { } while (0)
+#endif
+
 namespace nascar {
 
 // ---------------------------------------------------------------- settings
@@ -147,6 +161,34 @@ struct LWall {
 __device__ __forceinline__ Xf wall_xf(const LWall& w) { Xf t; t.p = V(w.px, w.py); t.q.s = w.qs; t.q.c = w.qc; return t; }
 __device__ __forceinline__ Aabb wall_fat(const LWall& w) { Aabb a; a.lo = V(w.flx, w.fly); a.hi = V(w.fhx, w.fhy); return a; }
 
+// Uniform grid of wall lists over a track (built on the host, nascar_add_track).
+// Cell (ix, iy) covers [ox + ix*cell, ox + (ix+1)*cell) x [...]; its list holds every
+// wall that can matter to a query centred in the cell:
+//   bp: walls whose fat AABB overlaps the cell grown by `reach` (query half-extent
+//       <= reach - 0.05, else the caller scans all walls); ascending wall index, so the
+//       broadphase pair order (b2BroadPhase::UpdatePairs sorts pairs) is unchanged.
+//   sn: walls whose culling circle comes within 250 m of the cell (distance sensors),
+//       nearest first.
+struct WallGrid {
+  float ox, oy, inv_cell, reach;
+  int nx, ny;
+  const int* start;        // [nx*ny + 1]
+  const uint16_t* idx;
+};
+struct WallSet {
+  const LWall* W; int nw;
+  WallGrid bp, sn;
+};
+// list of the cell containing (x, y), or false when outside the grid
+__device__ __forceinline__ bool grid_list(const WallGrid& g, float x, float y, int& beg, int& end) {
+  if (!g.start) return false;
+  const float fx = (x - g.ox) * g.inv_cell, fy = (y - g.oy) * g.inv_cell;
+  if (!(fx >= 0.0f && fy >= 0.0f && fx < (float)g.nx && fy < (float)g.ny)) return false;
+  const int cell = (int)fy * g.nx + (int)fx;
+  beg = g.start[cell]; end = g.start[cell + 1];
+  return true;
+}
+
 // ------------------------------------------------------------------ per-car register state
 struct Car {
   // b2Body
@@ -226,10 +268,20 @@ __device__ __forceinline__ void sync_fixtures(Car& c) {
 }
 
 // b2BroadPhase::UpdatePairs + b2ContactManager::AddPair (ascending wall proxy id, prepend)
-__device__ inline void find_new_contacts(Car& c, const LWall* W, int nw) {
+__device__ inline void find_new_contacts(Car& c, const WallSet& S) {
   if (!c.moved) return;
   c.moved = 0;
-  for (int j = 0; j < nw; ++j) {
+  const LWall* W = S.W;
+  int beg = 0, end = S.nw;
+  const uint16_t* list = nullptr;
+  {
+    const float hx = 0.5f * (c.fat.hi.x - c.fat.lo.x), hy = 0.5f * (c.fat.hi.y - c.fat.lo.y);
+    const float cx = 0.5f * (c.fat.hi.x + c.fat.lo.x), cy = 0.5f * (c.fat.hi.y + c.fat.lo.y);
+    if (hx <= S.bp.reach - 0.05f && hy <= S.bp.reach - 0.05f && grid_list(S.bp, cx, cy, beg, end)) list = S.bp.idx;
+    else { beg = 0; end = S.nw; }
+  }
+  for (int k = beg; k < end; ++k) {
+    const int j = list ? (int)list[k] : k;
     const LWall& wl = W[j];
     if (!overlap(c.fat, wall_fat(wl))) continue;
     bool exists = false;
@@ -649,7 +701,8 @@ __device__ inline void integrate_positions(BodyState& A, float h) {
 }
 
 // b2World::Solve (single dynamic body island)
-__device__ inline void solve(Car& c, const LWall* W, int nw, float dt, float dtRatio, float friction) {
+__device__ inline void solve(Car& c, const WallSet& S, float dt, float dtRatio, float friction) {
+  const LWall* W = S.W;
   if (!c.awake) return;
   int cidx[MAX_ISLAND]; int n = 0;
   for (int i = 0; i < c.nct; ++i) {
@@ -690,8 +743,9 @@ __device__ inline void solve(Car& c, const LWall* W, int nw, float dt, float dtR
       c.awake = 0; c.sleep = 0.0f; c.v = zero2(); c.w = 0.0f; c.force = zero2(); c.torque = 0.0f;
     }
   }
+  PROF(12);
   sync_fixtures(c);
-  find_new_contacts(c, W, nw);
+  find_new_contacts(c, S);
 }
 
 // ------------------------------------------------------------------ GJK / TOI
@@ -952,7 +1006,8 @@ __device__ inline void island_solve_toi(Car& c, const LWall* W, const int* cidx,
 }
 
 // b2World::SolveTOI
-__device__ inline void solve_toi(Car& c, const LWall* W, int nw, float dt, float friction) {
+__device__ inline void solve_toi(Car& c, const WallSet& S, float dt, float friction) {
+  const LWall* W = S.W;
   Poly pa; make_box(&pa, CAR_HX, CAR_HY);
   c.alpha0 = 0.0f;
   for (int i = 0; i < c.nct; ++i) { c.ct[i].flags &= ~(CT_TOI | CT_ISLAND); c.ct[i].toiCount = 0; c.ct[i].toi = 1.0f; }
@@ -1018,28 +1073,31 @@ __device__ inline void solve_toi(Car& c, const LWall* W, int nw, float dt, float
     island_solve_toi(c, W, cidx, n, subdt, friction);
     sync_fixtures(c);
     for (int i = 0; i < c.nct; ++i) c.ct[i].flags &= ~(CT_TOI | CT_ISLAND);
-    find_new_contacts(c, W, nw);
+    find_new_contacts(c, S);
   }
 }
 
-__device__ inline void b2_step(Car& c, const LWall* W, int nw, float dt, float friction) {
+__device__ inline void b2_step(Car& c, const WallSet& S, float dt, float friction) {
+  const LWall* W = S.W;
   float inv_dt = dt > 0.0f ? fdiv_cr(1.0f, dt) : 0.0f;
   float dtRatio = c.invdt0 * dt;
   collide(c, W);
-  solve(c, W, nw, dt, dtRatio, friction);
-  solve_toi(c, W, nw, dt, friction);
+  PROF(11);
+  solve(c, S, dt, dtRatio, friction);
+  PROF(13);
+  solve_toi(c, S, dt, friction);
   c.invdt0 = inv_dt;
   c.force = zero2(); c.torque = 0.0f;
 }
 
 // b2Body::SetTransform
-__device__ inline void set_transform(Car& c, const LWall* W, int nw, V2 pos, float angle) {
+__device__ inline void set_transform(Car& c, const WallSet& S, V2 pos, float angle) {
   c.xf.q = rot_set(angle);
   c.xf.p = pos;
   c.c = xmul(c.xf, zero2()); c.a = angle;
   c.c0 = c.c; c.a0 = angle;
   move_proxy(c, c.xf, c.xf);
-  find_new_contacts(c, W, nw);
+  find_new_contacts(c, S);
 }
 
 }  // namespace nascar

@@ -14,6 +14,8 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
+#include <cmath>
 #include <string>
 #include <unordered_map>
 #include <vector>
@@ -25,7 +27,6 @@
 
 using namespace nascar;
 
-#define BLOCK 256
 #define MAX_SEG 64
 
 #ifdef NASCAR_DEBUG
@@ -36,6 +37,7 @@ __device__ int g_dbg_car = -1;
 #define DBG(n, slot, val) do { } while (0)
 #endif
 
+
 // ------------------------------------------------------------------ device-side tables
 struct DSeg {   // per segment, float64 (src/track_generator.py TrackSegment)
   double sx, sy, ex, ey, width, banking, la, chord;  // la: banking lateral assist (src/car.py:527-533)
@@ -45,6 +47,7 @@ struct TrackDev {
   DSeg* segs; int nseg;
   double* prefix;      // cumulative chord length before segment k (src/car_env.py:1593-1600)
   double total_length; int startline; int has_banking;
+  WallGrid bp, sn;
 };
 
 struct Params {
@@ -490,41 +493,90 @@ __device__ inline bool lap_update(const TrackDev& T, Car& c, double px, double p
 }
 
 // ------------------------------------------------------------------ distance sensors (src/distance_sensor.py:71-117)
-// 16 rays x walls in LDS; a conservative bounding-circle cull skips walls the exact
-// b2PolygonShape::RayCast test provably rejects or cannot make the minimum.
-__device__ inline void sensor_rays(const LWall* W, int nw, V2 p1, double px, double py, double ang, float out[16]) {
-  V2 p2[16]; float dxf[16], dyf[16], best[16];
+// 16 rays x the walls in LDS.  The reference result per ray is the minimum over walls
+// of the exact b2PolygonShape::RayCast fraction (maxFraction 1, p2 fixed), so any cull
+// that provably keeps every wall that can hit a ray gives the identical minimum.
+// Cull, per wall: (1) range -- the wall's bounding circle (radius R incl. margin) must
+// reach within 250 m; (2) angle -- from the car the circle subtends
+// [phi - asin(R/d), phi + asin(R/d)]; only rays whose direction falls inside (plus a
+// 2e-3 rad guard for the approximate atan2 / f32 ray directions) are tested exactly.
+// A wall at distance d cannot beat the current best of a ray if d - R exceeds it.
+// Per-ray state (best fraction, f32 endpoint) lives in LDS so the ray loop can index
+// it dynamically: rs = [3][16][BLOCK] floats of this workgroup.
+__device__ __forceinline__ float atan2_approx(float y, float x) {   // |err| < 1.2e-5 rad
+  float ax = fabsf(x), ay = fabsf(y);
+  float mx = fmaxf(ax, ay), mn = fminf(ax, ay);
+  float t = mx > 0.0f ? mn * __builtin_amdgcn_rcpf(mx) : 0.0f;
+  float s2 = t * t;
+  float r = ((((0.0208351f * s2 - 0.0851330f) * s2 + 0.1801410f) * s2 - 0.3302995f) * s2 + 0.9998660f) * t;
+  if (ay > ax) r = 1.57079637f - r;
+  if (x < 0.0f) r = 3.14159274f - r;
+  return y < 0.0f ? -r : r;
+}
+
+__device__ inline void sensor_rays(const WallSet& S, V2 p1, double px, double py, double ang, float out[16],
+                                   float* rs) {
+  const LWall* W = S.W;
+  const int tid = threadIdx.x;
+  float* s_best = rs;
+  float* s_p2x = rs + 16 * BLOCK;
+  float* s_p2y = rs + 32 * BLOCK;
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
     double sa = -((double)i * (360.0 / 16) * RAD_PER_DEG) + ang;
     double dx = cos(sa), dy = sin(sa);
-    p2[i] = OV(px + dx * 250.0, py + dy * 250.0);
-    dxf[i] = (float)dx; dyf[i] = (float)dy; best[i] = 2.0f;
+    V2 p2 = OV(px + dx * 250.0, py + dy * 250.0);
+    s_p2x[i * BLOCK + tid] = p2.x; s_p2y[i * BLOCK + tid] = p2.y; s_best[i * BLOCK + tid] = 2.0f;
   }
   const float MARGIN = 0.25f;
-  for (int j = 0; j < nw; ++j) {
-    const LWall wl = W[j];
-    float rx = wl.px - p1.x, ry = wl.py - p1.y;
-    float R = wl.rad + MARGIN;
-    if (rx * rx + ry * ry > (250.0f + R) * (250.0f + R)) continue;
+  const float angf = (float)ang;
+  const float K = 2.54647909f;   // 8 / pi: rays are pi/8 apart, ray i points along ang - i*pi/8
+  int beg = 0, end = S.nw;
+  const uint16_t* list = nullptr;
+  if (grid_list(S.sn, p1.x, p1.y, beg, end)) list = S.sn.idx;
+  else { beg = 0; end = S.nw; }
+  for (int kk = beg; kk < end; ++kk) {
+    const LWall wl = W[list ? (int)list[kk] : kk];
+    const float rx = wl.px - p1.x, ry = wl.py - p1.y;
+    const float R = wl.rad + MARGIN;
+    const float d2 = rx * rx + ry * ry;
+    if (d2 > (250.0f + R) * (250.0f + R)) continue;
+    const float d = __builtin_amdgcn_sqrtf(d2);
+    unsigned mask;
+    if (d <= R * 1.0001f + 0.01f) {
+      mask = 0xFFFFu;
+    } else {
+      const float x = R * __builtin_amdgcn_rcpf(d) * 1.0001f;
+      const float half = fminf(x * (1.0f + 0.5708f * x * x), 1.5708f) + 2e-3f;   // >= asin(R/d) + guard
+      float u = (angf - atan2_approx(ry, rx)) * K;                                  // ray-index coordinate
+      u = u - 16.0f * floorf(u * 0.0625f);
+      const float w = half * K;
+      const int lo = (int)ceilf(u - w), hi = (int)floorf(u + w);
+      const int cnt = hi - lo + 1;
+      if (cnt <= 0) continue;
+      mask = cnt >= 16 ? 0xFFFFu : ((((1u << cnt) - 1u) << (lo & 15)) | (((1u << cnt) - 1u) >> (16 - (lo & 15))));
+      mask &= 0xFFFFu;
+    }
+    const float dlo = (d - R) * (1.0f / 250.0f) - 1e-4f;   // lower bound of any hit fraction on this wall
     Rot q; q.s = wl.qs; q.c = wl.qc;
-    V2 l1 = rmulT(q, V(p1.x - wl.px, p1.y - wl.py));
+    const V2 l1 = rmulT(q, V(p1.x - wl.px, p1.y - wl.py));
     const float hx = wl.hx, hy = wl.hy;
     // numerators of the 4 faces depend only on p1 (b2Dot(normal_i, vertex_i - p1))
     const float n0 = 0.0f * ((-hx) - l1.x) + (-1.0f) * ((-hy) - l1.y);
     const float n1 = 1.0f * (hx - l1.x) + 0.0f * ((-hy) - l1.y);
     const float n2 = 0.0f * (hx - l1.x) + 1.0f * (hy - l1.y);
     const float n3 = (-1.0f) * ((-hx) - l1.x) + 0.0f * (hy - l1.y);
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      float tc = rx * dxf[i] + ry * dyf[i];
-      float perp = fabsf(rx * dyf[i] - ry * dxf[i]);
-      if (perp > R || tc < -R || (tc - R) > 250.0f * best[i]) continue;
-      V2 l2 = rmulT(q, V(p2[i].x - wl.px, p2[i].y - wl.py));
-      V2 d = vsub(l2, l1);
+    while (mask) {
+      const int i = __builtin_ctz(mask);
+      mask &= mask - 1u;
+      const float bi = s_best[i * BLOCK + tid];
+      if (dlo > bi) continue;
+      V2 l2 = rmulT(q, V(s_p2x[i * BLOCK + tid] - wl.px, s_p2y[i * BLOCK + tid] - wl.py));
+      V2 dd = vsub(l2, l1);
       float lower = 0.0f, upper = 1.0f; int index = -1; bool ok = true;
       const float num[4] = {n0, n1, n2, n3};
-      const float den[4] = {0.0f * d.x + (-1.0f) * d.y, 1.0f * d.x + 0.0f * d.y, 0.0f * d.x + 1.0f * d.y, (-1.0f) * d.x + 0.0f * d.y};
+      const float den[4] = {0.0f * dd.x + (-1.0f) * dd.y, 1.0f * dd.x + 0.0f * dd.y, 0.0f * dd.x + 1.0f * dd.y,
+                            (-1.0f) * dd.x + 0.0f * dd.y};
 #pragma unroll
       for (int f = 0; f < 4; ++f) {
         if (!ok) break;
@@ -533,12 +585,13 @@ __device__ inline void sensor_rays(const LWall* W, int nw, V2 p1, double px, dou
         else if (den[f] > 0.0f && num[f] < upper * den[f]) { upper = fdiv_cr(num[f], den[f]); }
         if (upper < lower) ok = false;
       }
-      if (ok && index >= 0 && lower < best[i]) best[i] = lower;
+      if (ok && index >= 0 && lower < bi) s_best[i * BLOCK + tid] = lower;
     }
   }
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
-    double hd = best[i] <= 1.0f ? (double)best[i] * 250.0 : 250.0;
+    const float bi = s_best[i * BLOCK + tid];
+    double hd = bi <= 1.0f ? (double)bi * 250.0 : 250.0;
     float d32 = (float)hd;
     float v = fdiv_cr(d32, 250.0f);
     out[i] = v < 0.0f ? 0.0f : (v > 1.0f ? 1.0f : v);
@@ -546,11 +599,17 @@ __device__ inline void sensor_rays(const LWall* W, int nw, V2 p1, double px, dou
 }
 
 // CarPhysics._check_wall_collision AABB query (src/car_physics.py:470-524)
-__device__ inline bool query_on_wall(const LWall* W, int nw, double px, double py, double radius) {
+__device__ inline bool query_on_wall(const WallSet& S, double px, double py, double radius) {
+  const LWall* W = S.W;
   Aabb q; q.lo = V((float)(px - radius), (float)(py - radius)); q.hi = V((float)(px + radius), (float)(py + radius));
   V2 center = V((float)px, (float)py);
-  for (int j = 0; j < nw; ++j) {
-    const LWall& wl = W[j];
+  int beg = 0, end = S.nw;
+  const uint16_t* list = nullptr;
+  if (radius <= (double)S.bp.reach - 0.1 && grid_list(S.bp, 0.5f * (q.lo.x + q.hi.x), 0.5f * (q.lo.y + q.hi.y), beg, end))
+    list = S.bp.idx;
+  else { beg = 0; end = S.nw; }
+  for (int kk = beg; kk < end; ++kk) {
+    const LWall& wl = W[list ? (int)list[kk] : kk];
     if (!overlap(wall_fat(wl), q)) continue;
     Xf xf = wall_xf(wl);
     Poly p; make_box(&p, wl.hx, wl.hy);
@@ -568,7 +627,7 @@ __device__ inline bool query_on_wall(const LWall* W, int nw, double px, double p
 }
 
 // CarEnv._get_multi_obs for one car (src/car_env.py:891-956)
-__device__ inline void car_obs(const Car& c, const LWall* W, int nw, float* o) {
+__device__ inline void car_obs(const Car& c, const WallSet& S, float* o, float* rs) {
   double px = c.xf.p.x, py = c.xf.p.y, vx = c.v.x, vy = c.v.y, ang = c.a, av = c.w;
   o[0] = (float)npclip(px / 10000.0, -1, 1); o[1] = (float)npclip(py / 10000.0, -1, 1);
   o[2] = (float)npclip(vx / 111.1, -1, 1); o[3] = (float)npclip(vy / 111.1, -1, 1);
@@ -593,11 +652,11 @@ __device__ inline void car_obs(const Car& c, const LWall* W, int nw, float* o) {
   }
   o[19] = (float)npclip(imp / 50000.0, 0, 1); o[20] = (float)npclip(ca / PI_D, -1, 1);
   o[21] = (float)npclip(c.cum_impact / 250000.0, 0, 1);
-  sensor_rays(W, nw, c.xf.p, px, py, ang, o + 22);
+  sensor_rays(S, c.xf.p, px, py, ang, o + 22, rs);
 }
 
 // ------------------------------------------------------------------ reset (src/car_env.py:316-535)
-__device__ inline void car_reset(const Params& P, Car& c, int n, bool fresh, const LWall* W, int nw, const TrackDev& T) {
+__device__ inline void car_reset(const Params& P, Car& c, int n, bool fresh, const WallSet& S, const TrackDev& T) {
   V2 p = OV(P.start_x, P.start_y); float a = P.start_angle;
   if (fresh) {   // Car() + CarPhysics(car, track): new b2World (src/car_physics.py:74-107)
     c.xf.q = rot_set(a); c.xf.p = p;
@@ -609,13 +668,13 @@ __device__ inline void car_reset(const Params& P, Car& c, int n, bool fresh, con
     V2 r = V(AABB_EXT, AABB_EXT);
     c.fat.lo = vsub(ab.lo, r); c.fat.hi = vadd(ab.hi, r);
     c.nct = 0; c.overflow = 0; c.moved = 1;
-    find_new_contacts(c, W, nw);
+    find_new_contacts(c, S);
     c.bank = 0.0;
   } else {       // CarPhysics.reset_car + Car.reset (src/car_physics.py:550-571, src/car.py:1027-1058)
-    set_transform(c, W, nw, p, c.a);
-    set_transform(c, W, nw, c.xf.p, a);
-    set_transform(c, W, nw, p, c.a);
-    set_transform(c, W, nw, c.xf.p, a);
+    set_transform(c, S, p, c.a);
+    set_transform(c, S, c.xf.p, a);
+    set_transform(c, S, p, c.a);
+    set_transform(c, S, c.xf.p, a);
     c.v = zero2(); c.w = 0.0f;
   }
   c.rpm = 1000.0;
@@ -646,21 +705,27 @@ __global__ void __launch_bounds__(BLOCK) step_kernel(Params P, const void* actio
   __shared__ int s_laps_old[BLOCK], s_dis_old[BLOCK], s_laps_new[BLOCK], s_dis_new[BLOCK], s_lapdone[BLOCK];
   __shared__ int s_dis_final[BLOCK], s_below[BLOCK];
   __shared__ int s_envdone[BLOCK / 1];
+  __shared__ float s_rays[48 * BLOCK];
   const int tid = threadIdx.x, C = P.C;
   const int el = tid / C, car = tid - el * C;
   const int slot = blockIdx.x * P.epb + el;
   const int env = (el < P.epb) ? P.blk_env[slot] : -1;
   const int n = env >= 0 ? env * C + car : 0;
+  PROF_RT(14);
+  PROF(0);
   const TrackDev T = P.tracks[P.blk_track[blockIdx.x]];
   stage_track(T, sw);
   __syncthreads();
+  PROF(1);
   const int nw = T.nwall;
+  const WallSet S{sw, nw, T.bp, T.sn};
   Car c;
   bool lapdone = false;
   double sim = 0.0;
   if (env >= 0) {
     car_load(P, n, c);
     sim = P.env_time[env];
+    PROF(2);
     s_laps_old[tid] = c.lt_laps; s_dis_old[tid] = c.disabled;
     // actions (BaseEnv._convert_to_internal_action / _discrete_to_continuous, np.float32)
     float tb, st;
@@ -678,7 +743,9 @@ __global__ void __launch_bounds__(BLOCK) step_kernel(Params P, const void* actio
     c.brk_in = pymax(0.0, pymin(1.0, (double)a1));
     c.str_in = pymax(-1.0, pymin(1.0, (double)a2));
     car_update_physics(P, c, n, T);
-    b2_step(c, sw, nw, P.dt_f, P.friction);
+    PROF(3);
+    b2_step(c, S, P.dt_f, P.friction);
+    PROF(4);
     c.bank = T.has_banking ? banking_at(T, c.xf.p.x, c.xf.p.y) : 0.0;
     if (!c.disabled) {   // _run_single_physics_step (src/car_env.py:582-638)
       double imp = c.imp_present ? c.imp : 0.0;
@@ -692,6 +759,7 @@ __global__ void __launch_bounds__(BLOCK) step_kernel(Params P, const void* actio
     lapdone = lap_update(T, c, c.xf.p.x, c.xf.p.y, sim);
     s_laps_new[tid] = c.lt_laps; s_dis_new[tid] = c.disabled; s_lapdone[tid] = lapdone;
   }
+  PROF(5);
   __syncthreads();
   // env pass 1: lap-reset pending (src/car_env.py:672-676 with _all_active_cars_completed_lap :1640-1669,
   // evaluated in car order with cars > i not yet updated)
@@ -733,7 +801,9 @@ __global__ void __launch_bounds__(BLOCK) step_kernel(Params P, const void* actio
         }
       } else { c.stuck_dur = 0.0; c.has_stuck_start = 0; }
     }
-    car_obs(c, sw, nw, o);
+    PROF(6);
+    car_obs(c, S, o, s_rays);
+    PROF(7);
     // _calculate_multi_rewards (src/car_env.py:980-1113)
     if (c.disabled && !c.just_disabled) rew = 0.0f;
     else {
@@ -769,6 +839,7 @@ __global__ void __launch_bounds__(BLOCK) step_kernel(Params P, const void* actio
     s_dis_final[tid] = c.disabled;
     s_below[tid] = (!c.disabled && c.cum_reward < -250.0f) ? 1 : 0;
   }
+  PROF(8);
   __syncthreads();
   // env pass 2: termination (src/car_env.py:1115-1158, 791-794)
   if (env >= 0 && car == 0) {
@@ -805,13 +876,16 @@ __global__ void __launch_bounds__(BLOCK) step_kernel(Params P, const void* actio
     float* orow = obs + (size_t)n * 38;
     if (reset_now) {
       if (terminal_obs) { float* t = terminal_obs + (size_t)n * 38; for (int i = 0; i < 38; ++i) t[i] = o[i]; }
-      car_reset(P, c, n, false, sw, nw, T);
-      car_obs(c, sw, nw, o);
+      car_reset(P, c, n, false, S, T);
+      car_obs(c, S, o, s_rays);
     } else if (terminal_obs) {
       float* t = terminal_obs + (size_t)n * 38; for (int i = 0; i < 38; ++i) t[i] = o[i];
     }
+    PROF(9);
     for (int i = 0; i < 38; ++i) orow[i] = o[i];
     car_store(P, n, c);
+    PROF(10);
+    PROF_RT(15);
     if (reset_now && car == 0) {
       P.env_time[env] = 0.0;
       P.env_i32[E_PENDING * P.E + env] = 0; P.env_i32[E_REASON * P.E + env] = 0;
@@ -821,6 +895,7 @@ __global__ void __launch_bounds__(BLOCK) step_kernel(Params P, const void* actio
 }
 
 __global__ void __launch_bounds__(BLOCK) reset_kernel(Params P, const uint8_t* mask, float* obs) {
+  __shared__ float s_rays[48 * BLOCK];
   LWall* sw = (LWall*)smem;
   const int tid = threadIdx.x, C = P.C;
   const int el = tid / C, car = tid - el * C;
@@ -830,14 +905,15 @@ __global__ void __launch_bounds__(BLOCK) reset_kernel(Params P, const uint8_t* m
   const TrackDev T = P.tracks[P.blk_track[blockIdx.x]];
   stage_track(T, sw);
   __syncthreads();
+  const WallSet S{sw, T.nwall, T.bp, T.sn};
   if (env >= 0) {
     const int n = env * C + car;
     const bool fresh = P.env_i32[E_CREATED * P.E + env] == 0;
     Car c;
     car_load(P, n, c);
-    car_reset(P, c, n, fresh, sw, T.nwall, T);
+    car_reset(P, c, n, fresh, S, T);
     float o[38];
-    car_obs(c, sw, T.nwall, o);
+    car_obs(c, S, o, s_rays);
     for (int i = 0; i < 38; ++i) obs[(size_t)n * 38 + i] = o[i];
     car_store(P, n, c);
   }
@@ -858,6 +934,7 @@ __global__ void __launch_bounds__(BLOCK) info_kernel(Params P, double* info) {
   const TrackDev T = P.tracks[P.blk_track[blockIdx.x]];
   stage_track(T, sw);
   __syncthreads();
+  const WallSet S{sw, T.nwall, T.bp, T.sn};
   if (env < 0) return;
   const int n = env * C + car;
   Car c;
@@ -869,7 +946,7 @@ __global__ void __launch_bounds__(BLOCK) info_kernel(Params P, double* info) {
   o[INFO_IS_TIMING] = c.lt_timing; o[INFO_CUR_LAP_TIME] = c.lt_cur; o[INFO_LAP_DIST] = c.lt_dist;
   o[INFO_HAS_CROSSED] = c.lt_crossed; o[INFO_DISABLED] = c.disabled; o[INFO_CUM_REWARD] = c.cum_reward_info;
   o[INFO_CUM_IMPACT] = c.cum_impact;
-  o[INFO_ON_TRACK] = query_on_wall(sw, T.nwall, c.xf.p.x, c.xf.p.y, 0.5) ? 0.0 : 1.0;
+  o[INFO_ON_TRACK] = query_on_wall(S, c.xf.p.x, c.xf.p.y, 0.5) ? 0.0 : 1.0;
   o[INFO_RPM] = c.rpm; o[INFO_SIM_TIME] = P.env_time[env]; o[INFO_NCT] = c.nct; o[INFO_ERROR] = c.overflow;
 }
 
@@ -918,11 +995,74 @@ static int fail(const char* fmt, ...) {
 }
 #define HIPCHK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) return fail("%s failed: %s", #x, hipGetErrorString(e_)); } while (0)
 
+struct HostGrid {
+  WallGrid g{};
+  std::vector<int> start; std::vector<uint16_t> idx;
+  int* d_start = nullptr; uint16_t* d_idx = nullptr;
+};
 struct HostTrack {
   std::vector<LWall> walls; std::vector<DSeg> segs; std::vector<double> prefix;
   double total_length; int startline, has_banking;
   LWall* d_walls = nullptr; DSeg* d_segs = nullptr; double* d_prefix = nullptr;
+  HostGrid bp, sn;
 };
+
+// Wall grids (see WallGrid in nascar_device.h).  Conservative by construction: the
+// broadphase list of a cell holds every wall whose fat AABB overlaps the cell grown by
+// reach (+5 cm); the sensor list every wall whose culling circle (rad + 0.25 m) comes
+// within 251 m of the cell, nearest first.
+static const float BP_CELL = 4.0f, BP_REACH = 7.0f, SN_CELL = 16.0f, SN_PAD = 20.0f;
+static void build_grids(HostTrack& t) {
+  double lx = 1e30, ly = 1e30, hx = -1e30, hy = -1e30;
+  for (auto& w : t.walls) { lx = std::min(lx, (double)w.flx); ly = std::min(ly, (double)w.fly);
+                            hx = std::max(hx, (double)w.fhx); hy = std::max(hy, (double)w.fhy); }
+  auto setup = [&](HostGrid& G, float cell, float pad, float reach) {
+    G.g.ox = (float)(lx - pad); G.g.oy = (float)(ly - pad); G.g.inv_cell = 1.0f / cell; G.g.reach = reach;
+    G.g.nx = (int)std::ceil((hx + pad - G.g.ox) / cell) + 1; G.g.ny = (int)std::ceil((hy + pad - G.g.oy) / cell) + 1;
+    G.start.assign((size_t)G.g.nx * G.g.ny + 1, 0);
+  };
+  setup(t.bp, BP_CELL, BP_REACH + 4.0f, BP_REACH);
+  setup(t.sn, SN_CELL, SN_PAD, 0.0f);
+  const int nw = (int)t.walls.size();
+  for (int cy = 0; cy < t.bp.g.ny; ++cy)
+    for (int cx = 0; cx < t.bp.g.nx; ++cx) {
+      const double x0 = t.bp.g.ox + (double)cx * BP_CELL - BP_REACH - 0.05, x1 = t.bp.g.ox + (double)(cx + 1) * BP_CELL + BP_REACH + 0.05;
+      const double y0 = t.bp.g.oy + (double)cy * BP_CELL - BP_REACH - 0.05, y1 = t.bp.g.oy + (double)(cy + 1) * BP_CELL + BP_REACH + 0.05;
+      t.bp.start[(size_t)cy * t.bp.g.nx + cx] = (int)t.bp.idx.size();
+      for (int j = 0; j < nw; ++j) {
+        const LWall& w = t.walls[j];
+        if (w.flx > x1 || w.fhx < x0 || w.fly > y1 || w.fhy < y0) continue;
+        t.bp.idx.push_back((uint16_t)j);
+      }
+    }
+  t.bp.start.back() = (int)t.bp.idx.size();
+  std::vector<std::pair<double, int>> cand;
+  for (int cy = 0; cy < t.sn.g.ny; ++cy)
+    for (int cx = 0; cx < t.sn.g.nx; ++cx) {
+      const double x0 = t.sn.g.ox + (double)cx * SN_CELL, x1 = x0 + SN_CELL;
+      const double y0 = t.sn.g.oy + (double)cy * SN_CELL, y1 = y0 + SN_CELL;
+      const double mx = 0.5 * (x0 + x1), my = 0.5 * (y0 + y1);
+      t.sn.start[(size_t)cy * t.sn.g.nx + cx] = (int)t.sn.idx.size();
+      cand.clear();
+      for (int j = 0; j < nw; ++j) {
+        const LWall& w = t.walls[j];
+        const double dx = std::max(std::max(x0 - w.px, 0.0), w.px - x1), dy = std::max(std::max(y0 - w.py, 0.0), w.py - y1);
+        if (std::sqrt(dx * dx + dy * dy) > 251.0 + w.rad + 0.25) continue;
+        cand.push_back({std::hypot(w.px - mx, w.py - my) - w.rad, j});
+      }
+      std::sort(cand.begin(), cand.end());
+      for (auto& c : cand) t.sn.idx.push_back((uint16_t)c.second);
+    }
+  t.sn.start.back() = (int)t.sn.idx.size();
+}
+static int upload_grid(HostGrid& G) {
+  HIPCHK(hipMalloc(&G.d_start, sizeof(int) * G.start.size()));
+  HIPCHK(hipMemcpy(G.d_start, G.start.data(), sizeof(int) * G.start.size(), hipMemcpyHostToDevice));
+  HIPCHK(hipMalloc(&G.d_idx, sizeof(uint16_t) * std::max<size_t>(G.idx.size(), 1)));
+  if (!G.idx.empty()) HIPCHK(hipMemcpy(G.d_idx, G.idx.data(), sizeof(uint16_t) * G.idx.size(), hipMemcpyHostToDevice));
+  G.g.start = G.d_start; G.g.idx = G.d_idx;
+  return 0;
+}
 
 struct NascarHandle {
   NascarConfig cfg;
@@ -975,7 +1115,10 @@ extern "C" int nascar_create(const NascarConfig* cfg, NascarHandle** out) {
 extern "C" void nascar_destroy(NascarHandle* h) {
   if (!h) return;
   hipFree(h->arena); hipFree(h->d_ctl);
-  for (auto& t : h->tracks) { hipFree(t.d_walls); hipFree(t.d_segs); hipFree(t.d_prefix); }
+  for (auto& t : h->tracks) {
+    hipFree(t.d_walls); hipFree(t.d_segs); hipFree(t.d_prefix);
+    hipFree(t.bp.d_start); hipFree(t.bp.d_idx); hipFree(t.sn.d_start); hipFree(t.sn.d_idx);
+  }
   hipFree(h->d_tracks); hipFree(h->d_blk_track); hipFree(h->d_blk_env);
   delete h;
 }
@@ -1037,6 +1180,9 @@ extern "C" int nascar_add_track(NascarHandle* h, const double* segments, int32_t
   HIPCHK(hipMemcpy(t.d_segs, t.segs.data(), sizeof(DSeg) * t.segs.size(), hipMemcpyHostToDevice));
   HIPCHK(hipMalloc(&t.d_prefix, sizeof(double) * t.prefix.size()));
   HIPCHK(hipMemcpy(t.d_prefix, t.prefix.data(), sizeof(double) * t.prefix.size(), hipMemcpyHostToDevice));
+  if (nwall > 65535) return fail("track has %d walls (grid indices are 16-bit)", nwall);
+  build_grids(t);
+  if (upload_grid(t.bp) < 0 || upload_grid(t.sn) < 0) return -1;
   h->tracks.push_back(t);
   h->max_lds = std::max(h->max_lds, lds);
   h->dirty_tracks = true;
@@ -1061,6 +1207,7 @@ static int prepare(NascarHandle* h) {
     TrackDev d;
     d.walls = t.d_walls; d.nwall = (int)t.walls.size(); d.segs = t.d_segs; d.nseg = (int)t.segs.size();
     d.prefix = t.d_prefix; d.total_length = t.total_length; d.startline = t.startline; d.has_banking = t.has_banking;
+    d.bp = t.bp.g; d.sn = t.sn.g;
     td.push_back(d);
   }
   hipFree(h->d_tracks);
@@ -1163,6 +1310,12 @@ extern "C" int nascar_debug_sincosf(const float* x, float* s, float* c, int32_t 
   return 0;
 }
 
+#ifdef NASCAR_PROFILE
+extern "C" int nascar_debug_profile(unsigned long long* dev_buf) {
+  HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_prof), &dev_buf, sizeof(dev_buf)));
+  return 0;
+}
+#endif
 #ifdef NASCAR_DEBUG
 extern "C" int nascar_debug_tap(double* dev_buf, int32_t car) {
   HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_dbg), &dev_buf, sizeof(dev_buf)));
