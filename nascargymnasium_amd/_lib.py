@@ -9,7 +9,7 @@ import os
 import subprocess
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libnascar.so")
+LIB_PATH = os.environ.get("NASCAR_LIB") or os.path.join(HERE, "libnascar.so")   # NASCAR_LIB: A/B experiments
 CSRC = os.path.join(HERE, "csrc")
 
 INFO_FIELDS = ["x", "y", "vx", "vy", "angle", "omega", "speed", "lap_count", "last_lap_time", "best_lap_time",

@@ -23,10 +23,15 @@
 __device__ unsigned long long* g_prof = nullptr;
 #define PROF(ph) do { unsigned long long _t = __builtin_amdgcn_s_memtime(); \
     if (g_prof && (threadIdx.x & 63) == 0) g_prof[((size_t)blockIdx.x * (BLOCK / 64) + threadIdx.x / 64) * 16 + (ph)] = _t; } while (0)
+#define PROFS(ph) do { unsigned long long _t = __builtin_amdgcn_s_memtime(); \
+    if (g_prof && (threadIdx.x & 63) == 0) g_prof[(65536 + (size_t)blockIdx.x * (BLOCK / 64) + threadIdx.x / 64) * 16 + (ph)] = _t; } while (0)
+#define PCOUNT(slot, v) do { if (g_prof) atomicAdd(&g_prof[2 * 65536 * 16 + (slot)], (unsigned long long)(v)); } while (0)
 #define PROF_RT(slot) do { unsigned long long _t = __builtin_amdgcn_s_memrealtime(); \
     if (g_prof && (threadIdx.x & 63) == 0) g_prof[((size_t)blockIdx.x * (BLOCK / 64) + threadIdx.x / 64) * 16 + (slot)] = _t; } while (0)
 #else
 #define PROF(ph) do { } while (0)
+#define PROFS(ph) do { } while (0)
+#define PCOUNT(slot, v) do { } while (0)
 #define PROF_RT(slot) do { } while (0)
 #endif
 

@@ -48,6 +48,7 @@ struct TrackDev {
   double* prefix;      // cumulative chord length before segment k (src/car_env.py:1593-1600)
   double total_length; int startline; int has_banking;
   WallGrid bp, sn;
+  const float4* groups; int ngroup;   // sensor wall groups: (cx, cy, radius incl. margin, first | count << 16)
 };
 
 struct Params {
@@ -59,6 +60,7 @@ struct Params {
   double* env_time; int* env_i32;
   const int* blk_track; const int* blk_env;
   const TrackDev* tracks;
+  float4* pose;        // [2][N] sensor hand-off: (x, y, angle, mode) -- see sensor_kernel
 };
 
 #define F32P(P, f) ((P).f32 + (size_t)F32_##f * (P).N)
@@ -514,90 +516,6 @@ __device__ __forceinline__ float atan2_approx(float y, float x) {   // |err| < 1
   return y < 0.0f ? -r : r;
 }
 
-__device__ inline void sensor_rays(const WallSet& S, V2 p1, double px, double py, double ang, float out[16],
-                                   float* rs) {
-  const LWall* W = S.W;
-  const int tid = threadIdx.x;
-  float* s_best = rs;
-  float* s_p2x = rs + 16 * BLOCK;
-  float* s_p2y = rs + 32 * BLOCK;
-#pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    double sa = -((double)i * (360.0 / 16) * RAD_PER_DEG) + ang;
-    double dx = cos(sa), dy = sin(sa);
-    V2 p2 = OV(px + dx * 250.0, py + dy * 250.0);
-    s_p2x[i * BLOCK + tid] = p2.x; s_p2y[i * BLOCK + tid] = p2.y; s_best[i * BLOCK + tid] = 2.0f;
-  }
-  const float MARGIN = 0.25f;
-  const float angf = (float)ang;
-  const float K = 2.54647909f;   // 8 / pi: rays are pi/8 apart, ray i points along ang - i*pi/8
-  int beg = 0, end = S.nw;
-  const uint16_t* list = nullptr;
-  if (grid_list(S.sn, p1.x, p1.y, beg, end)) list = S.sn.idx;
-  else { beg = 0; end = S.nw; }
-  for (int kk = beg; kk < end; ++kk) {
-    const LWall wl = W[list ? (int)list[kk] : kk];
-    const float rx = wl.px - p1.x, ry = wl.py - p1.y;
-    const float R = wl.rad + MARGIN;
-    const float d2 = rx * rx + ry * ry;
-    if (d2 > (250.0f + R) * (250.0f + R)) continue;
-    const float d = __builtin_amdgcn_sqrtf(d2);
-    unsigned mask;
-    if (d <= R * 1.0001f + 0.01f) {
-      mask = 0xFFFFu;
-    } else {
-      const float x = R * __builtin_amdgcn_rcpf(d) * 1.0001f;
-      const float half = fminf(x * (1.0f + 0.5708f * x * x), 1.5708f) + 2e-3f;   // >= asin(R/d) + guard
-      float u = (angf - atan2_approx(ry, rx)) * K;                                  // ray-index coordinate
-      u = u - 16.0f * floorf(u * 0.0625f);
-      const float w = half * K;
-      const int lo = (int)ceilf(u - w), hi = (int)floorf(u + w);
-      const int cnt = hi - lo + 1;
-      if (cnt <= 0) continue;
-      mask = cnt >= 16 ? 0xFFFFu : ((((1u << cnt) - 1u) << (lo & 15)) | (((1u << cnt) - 1u) >> (16 - (lo & 15))));
-      mask &= 0xFFFFu;
-    }
-    const float dlo = (d - R) * (1.0f / 250.0f) - 1e-4f;   // lower bound of any hit fraction on this wall
-    Rot q; q.s = wl.qs; q.c = wl.qc;
-    const V2 l1 = rmulT(q, V(p1.x - wl.px, p1.y - wl.py));
-    const float hx = wl.hx, hy = wl.hy;
-    // numerators of the 4 faces depend only on p1 (b2Dot(normal_i, vertex_i - p1))
-    const float n0 = 0.0f * ((-hx) - l1.x) + (-1.0f) * ((-hy) - l1.y);
-    const float n1 = 1.0f * (hx - l1.x) + 0.0f * ((-hy) - l1.y);
-    const float n2 = 0.0f * (hx - l1.x) + 1.0f * (hy - l1.y);
-    const float n3 = (-1.0f) * ((-hx) - l1.x) + 0.0f * (hy - l1.y);
-    while (mask) {
-      const int i = __builtin_ctz(mask);
-      mask &= mask - 1u;
-      const float bi = s_best[i * BLOCK + tid];
-      if (dlo > bi) continue;
-      V2 l2 = rmulT(q, V(s_p2x[i * BLOCK + tid] - wl.px, s_p2y[i * BLOCK + tid] - wl.py));
-      V2 dd = vsub(l2, l1);
-      float lower = 0.0f, upper = 1.0f; int index = -1; bool ok = true;
-      const float num[4] = {n0, n1, n2, n3};
-      const float den[4] = {0.0f * dd.x + (-1.0f) * dd.y, 1.0f * dd.x + 0.0f * dd.y, 0.0f * dd.x + 1.0f * dd.y,
-                            (-1.0f) * dd.x + 0.0f * dd.y};
-#pragma unroll
-      for (int f = 0; f < 4; ++f) {
-        if (!ok) break;
-        if (den[f] == 0.0f) { if (num[f] < 0.0f) ok = false; }
-        else if (den[f] < 0.0f && num[f] < lower * den[f]) { lower = fdiv_cr(num[f], den[f]); index = f; }
-        else if (den[f] > 0.0f && num[f] < upper * den[f]) { upper = fdiv_cr(num[f], den[f]); }
-        if (upper < lower) ok = false;
-      }
-      if (ok && index >= 0 && lower < bi) s_best[i * BLOCK + tid] = lower;
-    }
-  }
-#pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    const float bi = s_best[i * BLOCK + tid];
-    double hd = bi <= 1.0f ? (double)bi * 250.0 : 250.0;
-    float d32 = (float)hd;
-    float v = fdiv_cr(d32, 250.0f);
-    out[i] = v < 0.0f ? 0.0f : (v > 1.0f ? 1.0f : v);
-  }
-}
-
 // CarPhysics._check_wall_collision AABB query (src/car_physics.py:470-524)
 __device__ inline bool query_on_wall(const WallSet& S, double px, double py, double radius) {
   const LWall* W = S.W;
@@ -626,8 +544,9 @@ __device__ inline bool query_on_wall(const WallSet& S, double px, double py, dou
   return false;
 }
 
-// CarEnv._get_multi_obs for one car (src/car_env.py:891-956)
-__device__ inline void car_obs(const Car& c, const WallSet& S, float* o, float* rs) {
+// CarEnv._get_multi_obs for one car (src/car_env.py:891-956): obs[0:22] (the 16 sensor
+// values obs[22:38] are written by sensor_kernel from the pose handed over in P.pose)
+__device__ inline void car_obs(const Car& c, float* o) {
   double px = c.xf.p.x, py = c.xf.p.y, vx = c.v.x, vy = c.v.y, ang = c.a, av = c.w;
   o[0] = (float)npclip(px / 10000.0, -1, 1); o[1] = (float)npclip(py / 10000.0, -1, 1);
   o[2] = (float)npclip(vx / 111.1, -1, 1); o[3] = (float)npclip(vy / 111.1, -1, 1);
@@ -652,7 +571,13 @@ __device__ inline void car_obs(const Car& c, const WallSet& S, float* o, float* 
   }
   o[19] = (float)npclip(imp / 50000.0, 0, 1); o[20] = (float)npclip(ca / PI_D, -1, 1);
   o[21] = (float)npclip(c.cum_impact / 250000.0, 0, 1);
-  sensor_rays(S, c.xf.p, px, py, ang, o + 22, rs);
+}
+// sensor hand-off modes (bits): A -> obs, A -> terminal_obs, B -> obs
+#define PM_A_OBS 1
+#define PM_A_TERM 2
+#define PM_B_OBS 4
+__device__ __forceinline__ float4 car_pose(const Car& c, int mode) {
+  return make_float4(c.xf.p.x, c.xf.p.y, c.a, __int_as_float(mode));
 }
 
 // ------------------------------------------------------------------ reset (src/car_env.py:316-535)
@@ -695,17 +620,202 @@ __device__ inline void car_reset(const Params& P, Car& c, int n, bool fresh, con
 // ------------------------------------------------------------------ the fused step
 extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
 
-__device__ inline void stage_track(const TrackDev& T, LWall* sw) {
-  for (int j = threadIdx.x; j < T.nwall; j += blockDim.x) sw[j] = T.walls[j];
+
+// Sensor kernel: LPC lanes per car, BLOCK / LPC cars of one track per workgroup.
+// The candidate list of the car's cell (WallGrid sn) holds wall GROUPS (runs of adjacent
+// walls with a bounding circle), nearest first; lane r of a car takes groups r, r+LPC, ...
+// Per group: range test, angular ray mask (as for single walls), then the rays whose
+// current best (shared by the car's lanes in LDS, atomicMin) is already closer than the
+// group are dropped; surviving rays are tested per wall with the bounding-circle cull and
+// the exact b2PolygonShape::RayCast.  The result is the minimum over every wall that can
+// hit each ray, i.e. the reference's value, whatever the visiting order.
+#ifndef SENSOR_LPC
+#define SENSOR_LPC 4
+#endif
+__device__ __forceinline__ float sensor_value(float best) {   // DistanceSensor distance -> obs (src/car_env.py:946)
+  double hd = best <= 1.0f ? (double)best * 250.0 : 250.0;
+  float d32 = (float)hd;
+  float v = fdiv_cr(d32, 250.0f);
+  return v < 0.0f ? 0.0f : (v > 1.0f ? 1.0f : v);
+}
+
+// rays (pi/8 apart, ray i along ang - i*pi/8) that can meet a circle (center r from the car, radius R)
+__device__ __forceinline__ unsigned ray_mask(float rx, float ry, float d, float R, float angf) {
+  if (d <= R * 1.0001f + 0.01f) return 0xFFFFu;
+  const float K = 2.54647909f;   // 8 / pi
+  const float x = R * __builtin_amdgcn_rcpf(d) * 1.0001f;
+  const float half = fminf(x * (1.0f + 0.5708f * x * x), 1.5708f) + 2e-3f;   // >= asin(R/d) + guard
+  float u = (angf - atan2_approx(ry, rx)) * K;                                  // ray-index coordinate
+  u = u - 16.0f * floorf(u * 0.0625f);
+  const float w = half * K;
+  const int lo = (int)ceilf(u - w), hi = (int)floorf(u + w);
+  const int cnt = hi - lo + 1;
+  if (cnt <= 0) return 0u;
+  if (cnt >= 16) return 0xFFFFu;
+  const unsigned m = (1u << cnt) - 1u;
+  return ((m << (lo & 15)) | (m >> (16 - (lo & 15)))) & 0xFFFFu;
+}
+
+template <int LPC>
+__global__ void __launch_bounds__(BLOCK) sensor_kernel(Params P, float* obs, float* terminal_obs) {
+  constexpr int CPW = BLOCK / LPC;          // cars per workgroup
+  constexpr int RPL = 16 / LPC;             // rays whose end points / outputs a lane owns
+  PROFS(0);
+  __shared__ float s_p2[CPW * 32];          // [car][ray][x, y]: f32 ray end points (exact test)
+  __shared__ float s_dir[CPW * 32];         // [car][ray][x, y]: unit ray directions (cull only)
+  __shared__ unsigned s_best[CPW * 16];     // [car][ray]: best fraction so far (float bits, >= 0)
+  float4* swa = (float4*)smem;
+  const int b = blockIdx.x / LPC, sub = blockIdx.x - b * LPC;
+  const int t = threadIdx.x, lc = t / LPC, r = t - lc * LPC;
+  const int C = P.C;
+  const int slot = sub * CPW + lc;          // car slot within the step kernel's workgroup b
+  const int el = slot / C, car = slot - el * C;
+  const int env = (el < P.epb) ? P.blk_env[b * P.epb + el] : -1;
+  const TrackDev T = P.tracks[P.blk_track[b]];
+  const int nw = T.nwall, ng = T.ngroup;
+  float4* swb = swa + nw;
+  float4* sgr = swb + nw;
+  for (int j = t; j < nw; j += BLOCK) {
+    const LWall w = T.walls[j];
+    swa[j] = make_float4(w.px, w.py, w.rad + 0.25f, w.hx);
+    swb[j] = make_float4(w.qs, w.qc, w.hy, 0.0f);
+  }
+  for (int g = t; g < ng; g += BLOCK) sgr[g] = T.groups[g];
+  const int n = env >= 0 ? env * C + car : 0;
+  float4 pa = make_float4(0.f, 0.f, 0.f, 0.f), pb = pa;
+  int mode = 0;
+  if (env >= 0) {
+    pa = P.pose[n];
+    mode = __float_as_int(pa.w);
+    if (mode & PM_B_OBS) pb = P.pose[P.N + n];
+  }
+  PROFS(1);
+  unsigned* best = s_best + lc * 16;
+  const float* p2s = s_p2 + lc * 32;
+  const float* dirs = s_dir + lc * 32;
+  for (int pass = 0; pass < 2; ++pass) {
+    const bool active = env >= 0 && (pass == 0 ? (mode & (PM_A_OBS | PM_A_TERM)) != 0 : (mode & PM_B_OBS) != 0);
+    const float4 ps = pass == 0 ? pa : pb;
+    const V2 p1 = V(ps.x, ps.y);
+    const double px = ps.x, py = ps.y, ang = ps.z;
+#pragma unroll
+    for (int q = 0; q < RPL; ++q) {
+      const int i = r * RPL + q;
+      if (active) {
+        double sa = -((double)i * (360.0 / 16) * RAD_PER_DEG) + ang;
+        double dx = cos(sa), dy = sin(sa);
+        V2 p2 = OV(px + dx * 250.0, py + dy * 250.0);
+        s_p2[(lc * 16 + i) * 2] = p2.x; s_p2[(lc * 16 + i) * 2 + 1] = p2.y;
+        s_dir[(lc * 16 + i) * 2] = (float)dx; s_dir[(lc * 16 + i) * 2 + 1] = (float)dy;
+      }
+      s_best[lc * 16 + i] = __float_as_uint(2.0f);
+    }
+    if (pass == 0) PROFS(2);
+    __syncthreads();   // also publishes the staged walls / groups on pass 0
+    if (pass == 0) PROFS(3);
+    if (active) {
+      int beg = 0, end = ng;
+      const uint16_t* list = nullptr;
+      if (grid_list(T.sn, p1.x, p1.y, beg, end)) list = T.sn.idx;
+      else { beg = 0; end = ng; }
+      const float angf = ps.z;
+#ifdef NASCAR_PROFILE
+      int c_vis = 0, c_rng = 0, c_open = 0, c_wr = 0, c_ex = 0, c_walls = 0;
+#define CNT(x) (x)++
+#else
+#define CNT(x) do { } while (0)
+#endif
+      for (int kk = beg + r; kk < end; kk += LPC) {
+        CNT(c_vis);
+        const float4 G = sgr[list ? (int)list[kk] : kk];
+        const float grx = G.x - p1.x, gry = G.y - p1.y;
+        const float d2 = grx * grx + gry * gry;
+        if (d2 > (250.0f + G.z) * (250.0f + G.z)) continue;
+        const float d = __builtin_amdgcn_sqrtf(d2);
+        CNT(c_rng);
+        unsigned mask = ray_mask(grx, gry, d, G.z, angf);
+        const float dlo = (d - G.z) * (1.0f / 250.0f) - 1e-4f;   // lower bound of any hit fraction in the group
+        unsigned open = 0u;
+        while (mask) {
+          const int i = __builtin_ctz(mask);
+          mask &= mask - 1u;
+          if (!(dlo > __uint_as_float(best[i]))) open |= 1u << i;
+        }
+        if (!open) continue;
+        CNT(c_open);
+        const int first = __float_as_int(G.w) & 0xFFFF, cnt = __float_as_int(G.w) >> 16;
+        for (int j = first; j < first + cnt; ++j) {
+          const float4 wa = swa[j];
+          const float rx = wa.x - p1.x, ry = wa.y - p1.y;
+          const float R = wa.z;
+          const float4 wb = swb[j];
+          Rot q; q.s = wb.x; q.c = wb.y;
+          const V2 l1 = rmulT(q, V(p1.x - wa.x, p1.y - wa.y));
+          const float hx = wa.w, hy = wb.z;
+          // numerators of the 4 faces depend only on p1 (b2Dot(normal_i, vertex_i - p1))
+          const float n0 = 0.0f * ((-hx) - l1.x) + (-1.0f) * ((-hy) - l1.y);
+          const float n1 = 1.0f * (hx - l1.x) + 0.0f * ((-hy) - l1.y);
+          const float n2 = 0.0f * (hx - l1.x) + 1.0f * (hy - l1.y);
+          const float n3 = (-1.0f) * ((-hx) - l1.x) + 0.0f * (hy - l1.y);
+          unsigned m = open;
+          CNT(c_walls);
+          while (m) {
+            const int i = __builtin_ctz(m);
+            m &= m - 1u;
+            const float bi = __uint_as_float(best[i]);
+            CNT(c_wr);
+            const float dx = dirs[2 * i], dy = dirs[2 * i + 1];
+            const float tc = rx * dx + ry * dy, perp = fabsf(rx * dy - ry * dx);
+            if (perp > R || tc < -R || (tc - R) > 250.0f * bi) continue;
+            CNT(c_ex);
+            const V2 l2 = rmulT(q, V(p2s[2 * i] - wa.x, p2s[2 * i + 1] - wa.y));
+            const V2 dd = vsub(l2, l1);
+            float lower = 0.0f, upper = 1.0f; int index = -1; bool ok = true;
+            const float num[4] = {n0, n1, n2, n3};
+            const float den[4] = {0.0f * dd.x + (-1.0f) * dd.y, 1.0f * dd.x + 0.0f * dd.y, 0.0f * dd.x + 1.0f * dd.y,
+                                  (-1.0f) * dd.x + 0.0f * dd.y};
+#pragma unroll
+            for (int f = 0; f < 4; ++f) {
+              if (!ok) break;
+              if (den[f] == 0.0f) { if (num[f] < 0.0f) ok = false; }
+              else if (den[f] < 0.0f && num[f] < lower * den[f]) { lower = fdiv_cr(num[f], den[f]); index = f; }
+              else if (den[f] > 0.0f && num[f] < upper * den[f]) { upper = fdiv_cr(num[f], den[f]); }
+              if (upper < lower) ok = false;
+            }
+            if (ok && index >= 0 && lower < bi) atomicMin(&best[i], __float_as_uint(lower));
+          }
+        }
+      }
+#ifdef NASCAR_PROFILE
+      if (pass == 0) { PCOUNT(0, c_vis); PCOUNT(1, c_rng); PCOUNT(2, c_open); PCOUNT(3, c_walls); PCOUNT(4, c_wr); PCOUNT(5, c_ex); PCOUNT(6, 1); }
+#endif
+    }
+    if (pass == 0) PROFS(4);
+    __syncthreads();   // all lanes of the car are done with best[]
+    if (pass == 0) PROFS(5);
+    if (active) {
+#pragma unroll
+      for (int q = 0; q < RPL; ++q) {
+        const int i = r * RPL + q;
+        const float val = sensor_value(__uint_as_float(best[i]));
+        if (pass == 0) {
+          if (mode & PM_A_OBS) obs[(size_t)n * 38 + 22 + i] = val;
+          if (mode & PM_A_TERM) terminal_obs[(size_t)n * 38 + 22 + i] = val;
+        } else {
+          obs[(size_t)n * 38 + 22 + i] = val;
+        }
+      }
+    }
+    if (pass == 0) PROFS(6);
+    if (!__syncthreads_or(mode & PM_B_OBS)) break;   // barrier: best / p2 are reused by pass 1
+  }
 }
 
 __global__ void __launch_bounds__(BLOCK) step_kernel(Params P, const void* actions, int discrete, float* obs, float* reward,
                                                      uint8_t* car_flags, uint8_t* env_flags, int auto_reset, float* terminal_obs) {
-  LWall* sw = (LWall*)smem;
   __shared__ int s_laps_old[BLOCK], s_dis_old[BLOCK], s_laps_new[BLOCK], s_dis_new[BLOCK], s_lapdone[BLOCK];
   __shared__ int s_dis_final[BLOCK], s_below[BLOCK];
   __shared__ int s_envdone[BLOCK / 1];
-  __shared__ float s_rays[48 * BLOCK];
   const int tid = threadIdx.x, C = P.C;
   const int el = tid / C, car = tid - el * C;
   const int slot = blockIdx.x * P.epb + el;
@@ -714,11 +824,9 @@ __global__ void __launch_bounds__(BLOCK) step_kernel(Params P, const void* actio
   PROF_RT(14);
   PROF(0);
   const TrackDev T = P.tracks[P.blk_track[blockIdx.x]];
-  stage_track(T, sw);
-  __syncthreads();
   PROF(1);
   const int nw = T.nwall;
-  const WallSet S{sw, nw, T.bp, T.sn};
+  const WallSet S{T.walls, nw, T.bp, T.sn};
   Car c;
   bool lapdone = false;
   double sim = 0.0;
@@ -782,7 +890,7 @@ __global__ void __launch_bounds__(BLOCK) step_kernel(Params P, const void* actio
     }
     P.env_i32[E_PENDING * P.E + env] = pend;
   }
-  float o[38];
+  float o[22];
   float rew = 0.0f;
   if (env >= 0) {
     // _check_and_disable_cars (src/car_env.py:805-888)
@@ -802,7 +910,7 @@ __global__ void __launch_bounds__(BLOCK) step_kernel(Params P, const void* actio
       } else { c.stuck_dur = 0.0; c.has_stuck_start = 0; }
     }
     PROF(6);
-    car_obs(c, S, o, s_rays);
+    car_obs(c, o);
     PROF(7);
     // _calculate_multi_rewards (src/car_env.py:980-1113)
     if (c.disabled && !c.just_disabled) rew = 0.0f;
@@ -874,15 +982,17 @@ __global__ void __launch_bounds__(BLOCK) step_kernel(Params P, const void* actio
     if (car_flags) car_flags[n] = flags;
     const bool reset_now = auto_reset && s_envdone[el];
     float* orow = obs + (size_t)n * 38;
-    if (reset_now) {
-      if (terminal_obs) { float* t = terminal_obs + (size_t)n * 38; for (int i = 0; i < 38; ++i) t[i] = o[i]; }
-      car_reset(P, c, n, false, S, T);
-      car_obs(c, S, o, s_rays);
-    } else if (terminal_obs) {
-      float* t = terminal_obs + (size_t)n * 38; for (int i = 0; i < 38; ++i) t[i] = o[i];
-    }
     PROF(9);
-    for (int i = 0; i < 38; ++i) orow[i] = o[i];
+    if (terminal_obs) { float* t = terminal_obs + (size_t)n * 38; for (int i = 0; i < 22; ++i) t[i] = o[i]; }
+    if (reset_now) {
+      P.pose[n] = car_pose(c, terminal_obs ? (PM_A_TERM | PM_B_OBS) : PM_B_OBS);
+      car_reset(P, c, n, false, S, T);
+      car_obs(c, o);
+      P.pose[P.N + n] = car_pose(c, 0);
+    } else {
+      P.pose[n] = car_pose(c, terminal_obs ? (PM_A_OBS | PM_A_TERM) : PM_A_OBS);
+    }
+    for (int i = 0; i < 22; ++i) orow[i] = o[i];
     car_store(P, n, c);
     PROF(10);
     PROF_RT(15);
@@ -895,26 +1005,23 @@ __global__ void __launch_bounds__(BLOCK) step_kernel(Params P, const void* actio
 }
 
 __global__ void __launch_bounds__(BLOCK) reset_kernel(Params P, const uint8_t* mask, float* obs) {
-  __shared__ float s_rays[48 * BLOCK];
-  LWall* sw = (LWall*)smem;
   const int tid = threadIdx.x, C = P.C;
   const int el = tid / C, car = tid - el * C;
   const int slot = blockIdx.x * P.epb + el;
   int env = (el < P.epb) ? P.blk_env[slot] : -1;
-  if (env >= 0 && mask && !mask[env]) env = -1;
+  if (env >= 0 && mask && !mask[env]) { P.pose[env * C + car] = make_float4(0.f, 0.f, 0.f, __int_as_float(0)); env = -1; }
   const TrackDev T = P.tracks[P.blk_track[blockIdx.x]];
-  stage_track(T, sw);
-  __syncthreads();
-  const WallSet S{sw, T.nwall, T.bp, T.sn};
+  const WallSet S{T.walls, T.nwall, T.bp, T.sn};
   if (env >= 0) {
     const int n = env * C + car;
     const bool fresh = P.env_i32[E_CREATED * P.E + env] == 0;
     Car c;
     car_load(P, n, c);
     car_reset(P, c, n, fresh, S, T);
-    float o[38];
-    car_obs(c, S, o, s_rays);
-    for (int i = 0; i < 38; ++i) obs[(size_t)n * 38 + i] = o[i];
+    float o[22];
+    car_obs(c, o);
+    for (int i = 0; i < 22; ++i) obs[(size_t)n * 38 + i] = o[i];
+    P.pose[n] = car_pose(c, PM_A_OBS);
     car_store(P, n, c);
   }
   __syncthreads();   // every lane of an env has read E_CREATED before its car 0 writes it
@@ -926,15 +1033,12 @@ __global__ void __launch_bounds__(BLOCK) reset_kernel(Params P, const uint8_t* m
 }
 
 __global__ void __launch_bounds__(BLOCK) info_kernel(Params P, double* info) {
-  LWall* sw = (LWall*)smem;
   const int tid = threadIdx.x, C = P.C;
   const int el = tid / C, car = tid - el * C;
   const int slot = blockIdx.x * P.epb + el;
   const int env = (el < P.epb) ? P.blk_env[slot] : -1;
   const TrackDev T = P.tracks[P.blk_track[blockIdx.x]];
-  stage_track(T, sw);
-  __syncthreads();
-  const WallSet S{sw, T.nwall, T.bp, T.sn};
+  const WallSet S{T.walls, T.nwall, T.bp, T.sn};
   if (env < 0) return;
   const int n = env * C + car;
   Car c;
@@ -1005,6 +1109,7 @@ struct HostTrack {
   double total_length; int startline, has_banking;
   LWall* d_walls = nullptr; DSeg* d_segs = nullptr; double* d_prefix = nullptr;
   HostGrid bp, sn;
+  std::vector<float4> groups; float4* d_groups = nullptr;
 };
 
 // Wall grids (see WallGrid in nascar_device.h).  Conservative by construction: the
@@ -1012,6 +1117,7 @@ struct HostTrack {
 // reach (+5 cm); the sensor list every wall whose culling circle (rad + 0.25 m) comes
 // within 251 m of the cell, nearest first.
 static const float BP_CELL = 4.0f, BP_REACH = 7.0f, SN_CELL = 16.0f, SN_PAD = 20.0f;
+static const double SN_GROUP_R = 12.0; static const int SN_GROUP_N = 8;
 static void build_grids(HostTrack& t) {
   double lx = 1e30, ly = 1e30, hx = -1e30, hy = -1e30;
   for (auto& w : t.walls) { lx = std::min(lx, (double)w.flx); ly = std::min(ly, (double)w.fly);
@@ -1036,7 +1142,46 @@ static void build_grids(HostTrack& t) {
       }
     }
   t.bp.start.back() = (int)t.bp.idx.size();
+  // sensor wall groups: runs of consecutive walls (index order follows each boundary through
+  // the curves) whose corners fit in a circle of radius <= SN_GROUP_R, at most SN_GROUP_N walls
+  {
+    auto corners = [&](int j, double* xs, double* ys) {
+      const LWall& w = t.walls[j];
+      const float vx[4] = {-w.hx, w.hx, w.hx, -w.hx}, vy[4] = {-w.hy, -w.hy, w.hy, w.hy};
+      for (int i = 0; i < 4; ++i) { xs[i] = (w.qc * vx[i] - w.qs * vy[i]) + w.px; ys[i] = (w.qs * vx[i] + w.qc * vy[i]) + w.py; }
+    };
+    auto circle = [&](int first, int count, double& cx, double& cy) {
+      double lx = 1e30, ly = 1e30, ux = -1e30, uy = -1e30, xs[4], ys[4];
+      for (int j = first; j < first + count; ++j) {
+        corners(j, xs, ys);
+        for (int i = 0; i < 4; ++i) { lx = std::min(lx, xs[i]); ux = std::max(ux, xs[i]); ly = std::min(ly, ys[i]); uy = std::max(uy, ys[i]); }
+      }
+      cx = 0.5 * (lx + ux); cy = 0.5 * (ly + uy);
+      double r = 0.0;
+      for (int j = first; j < first + count; ++j) {
+        corners(j, xs, ys);
+        for (int i = 0; i < 4; ++i) r = std::max(r, std::hypot(xs[i] - cx, ys[i] - cy));
+      }
+      return r;
+    };
+    t.groups.clear();
+    int first = 0;
+    while (first < nw) {
+      int count = 1;
+      while (first + count < nw && count < SN_GROUP_N) {
+        double cx, cy;
+        if (circle(first, count + 1, cx, cy) > SN_GROUP_R) break;
+        ++count;
+      }
+      double cx, cy, r = circle(first, count, cx, cy);
+      const int packed = first | (count << 16);
+      float pf; memcpy(&pf, &packed, sizeof pf);
+      t.groups.push_back(make_float4((float)cx, (float)cy, (float)(r + 0.3), pf));
+      first += count;
+    }
+  }
   std::vector<std::pair<double, int>> cand;
+  const int ng = (int)t.groups.size();
   for (int cy = 0; cy < t.sn.g.ny; ++cy)
     for (int cx = 0; cx < t.sn.g.nx; ++cx) {
       const double x0 = t.sn.g.ox + (double)cx * SN_CELL, x1 = x0 + SN_CELL;
@@ -1044,11 +1189,11 @@ static void build_grids(HostTrack& t) {
       const double mx = 0.5 * (x0 + x1), my = 0.5 * (y0 + y1);
       t.sn.start[(size_t)cy * t.sn.g.nx + cx] = (int)t.sn.idx.size();
       cand.clear();
-      for (int j = 0; j < nw; ++j) {
-        const LWall& w = t.walls[j];
-        const double dx = std::max(std::max(x0 - w.px, 0.0), w.px - x1), dy = std::max(std::max(y0 - w.py, 0.0), w.py - y1);
-        if (std::sqrt(dx * dx + dy * dy) > 251.0 + w.rad + 0.25) continue;
-        cand.push_back({std::hypot(w.px - mx, w.py - my) - w.rad, j});
+      for (int g = 0; g < ng; ++g) {
+        const float4 G = t.groups[g];
+        const double dx = std::max(std::max(x0 - G.x, 0.0), G.x - x1), dy = std::max(std::max(y0 - G.y, 0.0), G.y - y1);
+        if (std::sqrt(dx * dx + dy * dy) > 251.0 + G.z) continue;
+        cand.push_back({std::hypot(G.x - mx, G.y - my) - G.z, g});
       }
       std::sort(cand.begin(), cand.end());
       for (auto& c : cand) t.sn.idx.push_back((uint16_t)c.second);
@@ -1074,7 +1219,8 @@ struct NascarHandle {
   int* d_blk_track = nullptr; int* d_blk_env = nullptr; int nblocks = 0;
   std::vector<int> env_track;
   float* d_ctl = nullptr;    // rule-driver state for nascar_policy_actions
-  size_t max_lds = 0;
+  float4* d_pose = nullptr;  // [2][N] step/reset -> sensor_kernel hand-off
+  size_t max_lds = 0, max_sensor_lds = 0;
   bool dirty_tracks = true;
 };
 
@@ -1106,6 +1252,8 @@ extern "C" int nascar_create(const NascarConfig* cfg, NascarHandle** out) {
   if (e != hipSuccess) { delete h; return fail("hipMalloc(%zu) failed: %s", o, hipGetErrorString(e)); }
   hipMemset(h->arena, 0, o);
   hipMalloc(&h->d_ctl, sizeof(float) * 4 * N);
+  if (hipMalloc(&h->d_pose, sizeof(float4) * 2 * N) != hipSuccess) { hipFree(h->arena); hipFree(h->d_ctl); delete h; return fail("hipMalloc(pose) failed"); }
+  hipMemset(h->d_pose, 0, sizeof(float4) * 2 * N);
   hipMemset(h->d_ctl, 0, sizeof(float) * 4 * N);
   h->env_track.assign(E, 0);
   *out = h;
@@ -1114,10 +1262,10 @@ extern "C" int nascar_create(const NascarConfig* cfg, NascarHandle** out) {
 
 extern "C" void nascar_destroy(NascarHandle* h) {
   if (!h) return;
-  hipFree(h->arena); hipFree(h->d_ctl);
+  hipFree(h->arena); hipFree(h->d_ctl); hipFree(h->d_pose);
   for (auto& t : h->tracks) {
     hipFree(t.d_walls); hipFree(t.d_segs); hipFree(t.d_prefix);
-    hipFree(t.bp.d_start); hipFree(t.bp.d_idx); hipFree(t.sn.d_start); hipFree(t.sn.d_idx);
+    hipFree(t.bp.d_start); hipFree(t.bp.d_idx); hipFree(t.sn.d_start); hipFree(t.sn.d_idx); hipFree(t.d_groups);
   }
   hipFree(h->d_tracks); hipFree(h->d_blk_track); hipFree(h->d_blk_env);
   delete h;
@@ -1183,6 +1331,9 @@ extern "C" int nascar_add_track(NascarHandle* h, const double* segments, int32_t
   if (nwall > 65535) return fail("track has %d walls (grid indices are 16-bit)", nwall);
   build_grids(t);
   if (upload_grid(t.bp) < 0 || upload_grid(t.sn) < 0) return -1;
+  HIPCHK(hipMalloc(&t.d_groups, sizeof(float4) * t.groups.size()));
+  HIPCHK(hipMemcpy(t.d_groups, t.groups.data(), sizeof(float4) * t.groups.size(), hipMemcpyHostToDevice));
+  h->max_sensor_lds = std::max(h->max_sensor_lds, 2 * sizeof(float4) * t.walls.size() + sizeof(float4) * t.groups.size());
   h->tracks.push_back(t);
   h->max_lds = std::max(h->max_lds, lds);
   h->dirty_tracks = true;
@@ -1207,7 +1358,7 @@ static int prepare(NascarHandle* h) {
     TrackDev d;
     d.walls = t.d_walls; d.nwall = (int)t.walls.size(); d.segs = t.d_segs; d.nseg = (int)t.segs.size();
     d.prefix = t.d_prefix; d.total_length = t.total_length; d.startline = t.startline; d.has_banking = t.has_banking;
-    d.bp = t.bp.g; d.sn = t.sn.g;
+    d.bp = t.bp.g; d.sn = t.sn.g; d.groups = t.d_groups; d.ngroup = (int)t.groups.size();
     td.push_back(d);
   }
   hipFree(h->d_tracks);
@@ -1244,14 +1395,23 @@ static Params make_params(NascarHandle* h) {
   P.acc = (double*)(a + h->off_acc); P.ct = (DContact*)(a + h->off_ct); P.act_key = (int*)(a + h->off_key);
   P.act_n = (float*)(a + h->off_n); P.env_time = (double*)(a + h->off_time); P.env_i32 = (int*)(a + h->off_ei32);
   P.blk_track = h->d_blk_track; P.blk_env = h->d_blk_env; P.tracks = h->d_tracks;
+  P.pose = h->d_pose;
   return P;
+}
+
+static void launch_sensors(NascarHandle* h, const Params& P, float* obs, float* terminal_obs, void* stream) {
+  const size_t lds = h->max_sensor_lds;
+  hipLaunchKernelGGL(sensor_kernel<SENSOR_LPC>, dim3(h->nblocks * SENSOR_LPC), dim3(BLOCK), lds, (hipStream_t)stream,
+                     P, obs, terminal_obs);
 }
 
 extern "C" int nascar_reset(NascarHandle* h, const uint8_t* env_mask, float* obs, void* stream) {
   if (!h || !obs) return fail("null argument");
   if (prepare(h)) return -1;
   Params P = make_params(h);
-  hipLaunchKernelGGL(reset_kernel, dim3(h->nblocks), dim3(BLOCK), h->max_lds, (hipStream_t)stream, P, env_mask, obs);
+  hipLaunchKernelGGL(reset_kernel, dim3(h->nblocks), dim3(BLOCK), 0, (hipStream_t)stream, P, env_mask, obs);
+  HIPCHK(hipGetLastError());
+  launch_sensors(h, P, obs, nullptr, stream);
   HIPCHK(hipGetLastError());
   return 0;
 }
@@ -1261,8 +1421,10 @@ extern "C" int nascar_step(NascarHandle* h, const void* actions, int32_t discret
   if (!h || !actions || !obs || !reward) return fail("null argument");
   if (prepare(h)) return -1;
   Params P = make_params(h);
-  hipLaunchKernelGGL(step_kernel, dim3(h->nblocks), dim3(BLOCK), h->max_lds, (hipStream_t)stream, P, actions, discrete,
+  hipLaunchKernelGGL(step_kernel, dim3(h->nblocks), dim3(BLOCK), 0, (hipStream_t)stream, P, actions, discrete,
                      obs, reward, car_flags, env_flags, auto_reset, terminal_obs);
+  HIPCHK(hipGetLastError());
+  launch_sensors(h, P, obs, terminal_obs, stream);
   HIPCHK(hipGetLastError());
   return 0;
 }
@@ -1271,7 +1433,7 @@ extern "C" int nascar_get_info(NascarHandle* h, double* info, void* stream) {
   if (!h || !info) return fail("null argument");
   if (prepare(h)) return -1;
   Params P = make_params(h);
-  hipLaunchKernelGGL(info_kernel, dim3(h->nblocks), dim3(BLOCK), h->max_lds, (hipStream_t)stream, P, info);
+  hipLaunchKernelGGL(info_kernel, dim3(h->nblocks), dim3(BLOCK), 0, (hipStream_t)stream, P, info);
   HIPCHK(hipGetLastError());
   return 0;
 }

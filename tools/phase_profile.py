@@ -46,7 +46,7 @@ def main():
     for _ in range(a.warmup):
         env.step(torch.rand((a.envs, a.cars, 2), generator=g, device="cuda:0") * 2 - 1, auto_reset=True)
     nwaves = 65536
-    buf = torch.zeros(nwaves * 16, dtype=torch.int64, device="cuda:0")
+    buf = torch.zeros(2 * nwaves * 16 + 16, dtype=torch.int64, device="cuda:0")
     L.nascar_debug_profile(ctypes.c_void_p(buf.data_ptr()))
     acc = []
     for _ in range(a.steps):
@@ -55,8 +55,18 @@ def main():
         torch.cuda.synchronize()
         env.launch_step(acts, auto_reset=True)
         torch.cuda.synchronize()
-        acc.append(buf.view(nwaves, 16).cpu().numpy().copy())
+        acc.append(buf[:2 * nwaves * 16].view(2 * nwaves, 16).cpu().numpy().copy())
+        cnt = buf[2 * nwaves * 16:].cpu().numpy()
+        if cnt[6]:
+            print("sensor lanes %d: per lane groups visited %.1f in-range %.1f open %.1f | walls %.1f wall-ray culls %.1f exact %.1f"
+                  % (cnt[6], *(cnt[:6] / cnt[6])))
     L.nascar_debug_profile(ctypes.c_void_p(0))
+    sens = []
+    for b in acc:
+        sb = b[nwaves:]
+        sb = sb[(sb[:, 0] != 0) & (sb[:, 6] != 0)].astype(np.float64)
+        sens.append(np.diff(sb[:, :7], axis=1))
+    acc = [b[:nwaves] for b in acc]
     res = []
     for b in acc:
         b = b[b[:, 10] != 0]
@@ -76,6 +86,12 @@ def main():
     if len(sub):
         for k, name in enumerate(["collide", "solve", "sync_fixtures+find_new_contacts", "solve_toi"]):
             print(f"    b2_step/{name:30s} mean {sub[:, k].mean():10.0f}  max {sub[:, k].max():10.0f}")
+    sd = np.concatenate(sens)
+    if len(sd):
+        print(f"sensor_kernel: waves/launch {len(sens[0])}, mean wave cycles {sd.sum(1).mean():.0f}")
+        for k, name in enumerate(["setup (walls/groups/pose)", "ray end points (f64 cos/sin)", "barrier", "group/wall cull",
+                                  "barrier", "write obs"]):
+            print(f"  {name:30s} mean {sd[:, k].mean():10.0f}  max {sd[:, k].max():10.0f}")
     for _, st, en in res[:3]:
         t0 = st.min()
         print(f"  realtime (us): first start 0, last start {(st.max() - t0) / 100:.1f}, "
