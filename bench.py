@@ -43,6 +43,23 @@ def cpu_baseline(track, cars, budget_s=12.0):
                       f"{steps} steps on {os.path.basename(track)}, uniform actions, 1 host thread"}
 
 
+def reduce_max(values, device):
+    """MAX over ranks of per-rank timings (no-op at world size 1).  Ranks own disjoint env shards and
+    never exchange simulation data: this is the only collective in the benchmark."""
+    import torch
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return [float(v) for v in values]
+    t = torch.tensor([float(v) for v in values], device=device, dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return [float(x) for x in t.tolist()]
+
+
+def throughput(world, envs, cars, steps, elapsed_max):
+    """whole-job car-steps/s under weak scaling: every rank steps its own envs x cars."""
+    return world * envs * cars * steps / elapsed_max
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -106,12 +123,8 @@ def main():
     elapsed = time.perf_counter() - t0
     kern_ms = sum(s.elapsed_time(e) for s, e in ev) / K
     errs = int(((env.car_flags & 128) != 0).sum().item())
-    if world > 1:
-        t = torch.tensor([elapsed, kern_ms], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, kern_ms = float(t[0]), float(t[1])
-    total_car_steps = world * E * C * K
-    value = total_car_steps / elapsed
+    elapsed, kern_ms = reduce_max([elapsed, kern_ms], dev)
+    value = throughput(world, E, C, K, elapsed)
     achieved = E * C * ALGO_BYTES_PER_CAR_STEP / (kern_ms * 1e-3) / 1e9
     traffic = None
     tfile = os.path.join(ROOT, "profiles", "pmc_traffic.json")

@@ -48,8 +48,7 @@ class BatchedCarEnv:
         if len(files) != self.E:
             raise ValueError("need one track per env")
         uniq = sorted(set(track_path(f) for f in files))
-        self.tracks = [load_track(p) for p in uniq]
-        first = self.tracks[uniq.index(track_path(files[0]))]
+        first = load_track(track_path(files[0]))
         sx, sy = start_position if start_position is not None else first.start_position
         cfg = _lib.NascarConfig(self.E, self.C, int(reset_on_lap), self.device.index, float(sx), float(sy),
                                 float(start_angle))
@@ -57,15 +56,10 @@ class BatchedCarEnv:
         with torch.cuda.device(self.device):
             _lib.check(self.L.nascar_create(ctypes.byref(cfg), ctypes.byref(h)))
         self.h = h
-        for t in self.tracks:
-            seg = np.ascontiguousarray(t.segment_table())
-            walls = np.ascontiguousarray(build_walls(t)[:, :4])
-            dp = ctypes.POINTER(ctypes.c_double)
-            _lib.check(self.L.nascar_add_track(self.h, seg.ctypes.data_as(dp), seg.shape[0], float(t.total_length),
-                                               walls.ctypes.data_as(dp), walls.shape[0]))
-        env_track = np.array([uniq.index(track_path(f)) for f in files], np.int32)
-        _lib.check(self.L.nascar_set_env_tracks(self.h, env_track.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))))
-        self.env_track = env_track
+        self.tracks, self._track_id = [], {}
+        for p in uniq:
+            self._add_track(p)
+        self.set_env_tracks(files)
         dev = self.device
         self.obs = torch.zeros(self.E, self.C, _lib.OBS_DIM, dtype=torch.float32, device=dev)
         self.reward = torch.zeros(self.E, self.C, dtype=torch.float32, device=dev)
@@ -74,6 +68,33 @@ class BatchedCarEnv:
         self.terminal_obs = torch.zeros_like(self.obs)
         self._info = torch.zeros(self.E, self.C, _lib.N_INFO, dtype=torch.float64, device=dev)
         self._actions = torch.zeros(self.E, self.C, 2, dtype=torch.float32, device=dev)
+
+    def _add_track(self, path: str) -> int:
+        """Load a .track file into the handle (TrackLoader + _create_track_walls tables); returns its id."""
+        path = track_path(path)
+        if path in self._track_id:
+            return self._track_id[path]
+        t = load_track(path)
+        seg = np.ascontiguousarray(t.segment_table())
+        walls = np.ascontiguousarray(build_walls(t)[:, :4])
+        dp = ctypes.POINTER(ctypes.c_double)
+        tid = _lib.check(self.L.nascar_add_track(self.h, seg.ctypes.data_as(dp), seg.shape[0], float(t.total_length),
+                                                 walls.ctypes.data_as(dp), walls.shape[0]))
+        self.tracks.append(t)
+        self._track_id[path] = tid
+        return tid
+
+    def set_env_tracks(self, files: Sequence[str]):
+        """Per-env track (name or path) for the next reset of each env; new tracks are loaded on demand.
+        The start pose is the handle's (every bundled track starts its GRID at (0, 0), heading 0)."""
+        if isinstance(files, str):
+            files = [files] * self.E
+        if len(files) != self.E:
+            raise ValueError("need one track per env")
+        env_track = np.array([self._add_track(f) for f in files], np.int32)
+        _lib.check(self.L.nascar_set_env_tracks(self.h, env_track.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))))
+        self.env_track = env_track
+        self.track_files = [track_path(f) for f in files]
 
     # ------------------------------------------------------------------ core API
     def reset(self, env_mask: Optional[torch.Tensor] = None) -> torch.Tensor:

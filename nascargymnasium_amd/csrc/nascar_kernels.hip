@@ -1342,8 +1342,13 @@ extern "C" int nascar_add_track(NascarHandle* h, const double* segments, int32_t
 
 extern "C" int nascar_set_env_tracks(NascarHandle* h, const int32_t* env_track) {
   if (!h || !env_track) return fail("null argument");
-  for (int e = 0; e < h->E; ++e) {
+  for (int e = 0; e < h->E; ++e)
     if (env_track[e] < 0 || env_track[e] >= (int)h->tracks.size()) return fail("env %d: bad track id %d", e, env_track[e]);
+  // an env whose track changes gets fresh physics worlds at its next reset
+  // (CarEnv.reset recreates CarPhysics on a track change, src/car_env.py:375-394)
+  char* created = (char*)h->arena + h->off_ei32 + sizeof(int) * (size_t)E_CREATED * h->E;
+  for (int e = 0; e < h->E; ++e) {
+    if (h->env_track[e] != env_track[e]) HIPCHK(hipMemset(created + sizeof(int) * e, 0, sizeof(int)));
     h->env_track[e] = env_track[e];
   }
   h->dirty_tracks = true;

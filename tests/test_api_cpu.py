@@ -1,0 +1,72 @@
+"""Host-side API semantics on CPU (no GPU needed): the restated gymnasium 0.29.1 spaces,
+BaseEnv action conversions (src/base_env.py:201-252) and CarEnv constructor errors
+(src/car_env.py:103-129, src/track_generator.py:318-319)."""
+import numpy as np
+import pytest
+
+from nascargymnasium_amd.car_env import BaseEnv, CarEnv, _format_time
+from nascargymnasium_amd.spaces import Box, Discrete, MultiDiscrete
+
+
+def test_box_contains_semantics():
+    sp = BaseEnv(num_cars=1).action_space
+    assert isinstance(sp, Box) and sp.shape == (2,)
+    assert sp.contains(np.array([0.5, -1.0], np.float32))
+    assert sp.contains([0.5, -1.0])                              # list -> asarray(float32)
+    assert not sp.contains(np.array([0.5, -1.0], np.float64))    # np.can_cast(float64, float32) is False
+    assert not sp.contains(np.array([1.5, 0.0], np.float32))     # out of bounds
+    assert not sp.contains(np.array([[0.5, 0.0]], np.float32))   # shape must match exactly
+    assert not sp.contains("abc")
+    multi = BaseEnv(num_cars=3).action_space
+    assert multi.shape == (3, 2) and multi.contains(np.zeros((3, 2), np.float32))
+    assert not multi.contains(np.zeros((2,), np.float32))
+    obs = BaseEnv(num_cars=1).observation_space
+    assert obs.shape == (38,) and obs.low[4] == 0.0 and obs.low[5] == -1.0 and obs.low[20] == -1.0
+
+
+def test_discrete_contains_semantics():
+    sp = BaseEnv(discrete_action_space=True, num_cars=1).action_space
+    assert isinstance(sp, Discrete)
+    assert sp.contains(0) and sp.contains(4) and sp.contains(np.int64(3)) and sp.contains(np.array(2))
+    assert not sp.contains(5) and not sp.contains(-1) and not sp.contains(1.0) and not sp.contains(np.array([1]))
+    md = BaseEnv(discrete_action_space=True, num_cars=4).action_space
+    assert isinstance(md, MultiDiscrete)
+    assert md.contains([0, 1, 2, 4]) and md.contains(np.array([4, 4, 4, 4]))
+    assert not md.contains([0, 1, 2, 5]) and not md.contains([0, 1, 2])
+
+
+def test_action_conversions():
+    conv = BaseEnv._convert_to_internal_action
+    assert conv([0.7, -0.2]) == [0.7, 0.0, -0.2]
+    assert conv([-0.4, 0.3]) == [0.0, 0.4, 0.3]
+    d2c = BaseEnv._discrete_to_continuous
+    assert [d2c(a) for a in range(5)] == [[0.0, 0.0], [1.0, 0.0], [-1.0, 0.0], [0.0, -1.0], [0.0, 1.0]]
+    with pytest.raises(ValueError):
+        d2c(7)
+
+
+def test_carenv_constructor_errors():
+    with pytest.raises(ValueError):
+        CarEnv(track_file="daytona", num_cars=0)
+    with pytest.raises(ValueError):
+        CarEnv(track_file="daytona", num_cars=11)
+    with pytest.raises(ValueError):
+        CarEnv(track_file="daytona", num_cars=2, car_names=["a"])
+    with pytest.raises(FileNotFoundError):
+        CarEnv(track_file="/nonexistent/track.track")
+    with pytest.raises(NotImplementedError):
+        CarEnv(track_file="daytona", render_mode="human")
+
+
+def test_carenv_needs_device():
+    """The product path fails loudly without a HIP device (no CPU fallback)."""
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        CarEnv(track_file="daytona")
+
+
+def test_format_time():
+    assert _format_time(None) == "--:--.---" and _format_time(-1.0) == "--:--.---"
+    assert _format_time(83.4567) == " 1:23.457"

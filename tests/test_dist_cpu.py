@@ -1,0 +1,53 @@
+"""bench.py's multi-rank path on CPU: world_size 2 over gloo (127.0.0.1).  Ranks hold
+disjoint env shards; the only collective is the MAX-reduction of the timings."""
+import os
+import socket
+import sys
+
+import pytest
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    import torch
+    import torch.distributed as dist
+    sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import bench
+    elapsed, kern = bench.reduce_max([1.0 + rank, 0.5 - 0.1 * rank], torch.device("cpu"))
+    value = bench.throughput(dist.get_world_size(), 8192, 10, 200, elapsed)
+    # per-rank synthetic action streams differ (seed 1234 + rank), as in bench.main
+    g = torch.Generator().manual_seed(1234 + rank)
+    a = torch.rand(4, generator=g)
+    gathered = [torch.zeros(4) for _ in range(world)]
+    dist.all_gather(gathered, a)
+    q.put((rank, elapsed, kern, value, not torch.equal(gathered[0], gathered[1])))
+    dist.destroy_process_group()
+
+
+def test_bench_reduction_world2():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, elapsed, kern, value, distinct in res:
+        assert elapsed == 2.0 and kern == pytest.approx(0.5)
+        assert value == pytest.approx(2 * 8192 * 10 * 200 / 2.0)
+        assert distinct

@@ -1,0 +1,117 @@
+"""The Gymnasium CarEnv / SB3-style VecCarEnv host API over the HIP engine, checked
+against the reference's golden traces (tests/golden) and the engine itself."""
+import os
+
+import numpy as np
+import pytest
+
+from golden_replay import TRACKS, load
+
+pytestmark = pytest.mark.gpu
+
+
+def _replay_carenv(name, steps=None):
+    from nascargymnasium_amd import CarEnv
+    d = load(name)
+    C = int(d["C"])
+    env = CarEnv(track_file=os.path.join(TRACKS, str(d["track"])), num_cars=C, reset_on_lap=bool(d["reset_on_lap"]))
+    obs, info = env.reset(seed=0)
+    want0 = d["obs0"][0] if C == 1 else d["obs0"]
+    assert obs.shape == ((38,) if C == 1 else (C, 38)) and obs.dtype == np.float32
+    assert np.array_equal(obs, want0)
+    assert info["simulation_time"] == 0.0 and len(info["cars"]) == C
+    keep = set(d["obs_steps"].tolist()) if "obs_steps" in d else None
+    n = len(d["actions"]) if steps is None else steps
+    j = 0
+    for k in range(n):
+        if d["reset"][k]:
+            obs, info = env.reset()
+            if keep is None or k in keep:
+                j += 1
+            continue
+        a = d["actions"][k]
+        obs, rew, term, trunc, info = env.step(a[0] if C == 1 else a)
+        if C == 1:
+            assert isinstance(rew, np.float32) and obs.shape == (38,)
+        assert bool(term) == bool(d["terminated"][k]) and bool(trunc) == bool(d["truncated"][k]), k
+        assert np.array_equal(np.atleast_1d(rew), d["rewards"][k]), k
+        if keep is None or k in keep:
+            assert np.array_equal(obs.reshape(C, 38), d["obs"][j]), k
+            j += 1
+        lap = [c["lap_timing"]["lap_count"] for c in info["cars"]]
+        assert lap == d["info"][k, :, 0].astype(int).tolist(), k
+        assert [c["disabled"] for c in info["cars"]] == (d["info"][k, :, 8] != 0).tolist(), k
+        assert env.disabled_cars == {i for i in range(C) if d["info"][k, i, 8] != 0}
+    env.close()
+
+
+@pytest.mark.parametrize("name", ["daytona_mixed", "daytona_crash", "martinsville_lap", "nascar2_seam"])
+def test_carenv_golden(name):
+    _replay_carenv(name)
+
+
+def test_carenv_errors_and_discrete():
+    from nascargymnasium_amd import CarEnv
+    env = CarEnv(track_file="daytona", discrete_action_space=True, num_cars=2)
+    with pytest.raises(RuntimeError):
+        env.step(np.array([1, 1]))
+    env.reset()
+    with pytest.raises(AssertionError):
+        env.step(np.array([1, 7]))
+    for k in range(30):
+        obs, rew, term, trunc, info = env.step(np.array([1, 4]))
+    assert obs.shape == (2, 38) and rew.shape == (2,)
+    assert info["cars"][0]["car_speed_ms"] > 0
+    env.close()
+    env = CarEnv(track_file="daytona")
+    env.reset()
+    with pytest.raises(AssertionError):
+        env.step(np.array([0.5, 0.5], np.float64))     # gymnasium Box: float64 is not castable to float32
+    env.close()
+
+
+def test_random_track_mode_recreates_worlds():
+    from nascargymnasium_amd import CarEnv
+    from nascargymnasium_amd.batched import BatchedCarEnv
+    env = CarEnv(track_file=None, num_cars=1)
+    seen = set()
+    for s in range(4):
+        obs, info = env.reset(seed=s)
+        seen.add(os.path.basename(env.track_file))
+        fresh = BatchedCarEnv(1, 1, env.track_file, device="cuda:0")
+        fo = fresh.reset()[0, 0].cpu().numpy()
+        assert np.array_equal(obs, fo), env.track_file      # reset after a track change == a fresh env
+        for k in range(40):
+            o, r, t, tr, _ = env.step(np.array([0.8, 0.1], np.float32))
+            fo = fresh.step(__import__("torch").tensor([[[0.8, 0.1]]], device="cuda:0"))[0][0, 0].cpu().numpy()
+            assert np.array_equal(o, fo)
+        fresh.close()
+    assert len(seen) >= 2
+    env.close()
+
+
+def test_vec_env_auto_reset_matches_engine():
+    import torch
+    from nascargymnasium_amd import VecCarEnv
+    from nascargymnasium_amd.batched import BatchedCarEnv
+    E = 16
+    venv = VecCarEnv(E, "martinsville", num_cars=1)
+    ref = BatchedCarEnv(E, 1, "martinsville", device="cuda:0")
+    o = venv.reset()
+    assert o.shape == (E, 38) and np.array_equal(o, ref.reset()[:, 0].cpu().numpy())
+    rng = np.random.default_rng(3)
+    episodes = 0
+    for k in range(800):
+        a = rng.uniform(-1, 1, (E, 2)).astype(np.float32)
+        a[:, 0] = np.where(np.arange(E) % 2 == 0, 0.0, a[:, 0])     # idle half -> stuck -> episode ends
+        obs, rew, done, infos = venv.step(a)
+        robs, rrew, rterm, rtrunc = ref.step(torch.from_numpy(a).view(E, 1, 2).cuda(), auto_reset=True, terminal_obs=True)
+        assert np.array_equal(obs, robs[:, 0].cpu().numpy()) and np.array_equal(rew, rrew[:, 0].cpu().numpy())
+        rdone = (rterm | rtrunc).cpu().numpy()
+        assert np.array_equal(done, rdone)
+        for e in np.nonzero(done)[0]:
+            episodes += 1
+            assert np.array_equal(infos[e]["terminal_observation"], ref.terminal_obs[e, 0].cpu().numpy())
+            assert infos[e]["episode"]["l"] > 0
+    assert episodes > 0
+    venv.close(); ref.close()
