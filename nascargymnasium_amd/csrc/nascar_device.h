@@ -26,11 +26,20 @@ __device__ unsigned long long* g_prof = nullptr;
 #define PROFS(ph) do { unsigned long long _t = __builtin_amdgcn_s_memtime(); \
     if (g_prof && (threadIdx.x & 63) == 0) g_prof[(65536 + (size_t)blockIdx.x * (BLOCK / 64) + threadIdx.x / 64) * 16 + (ph)] = _t; } while (0)
 #define PCOUNT(slot, v) do { if (g_prof) atomicAdd(&g_prof[2 * 65536 * 16 + (slot)], (unsigned long long)(v)); } while (0)
+#ifdef NASCAR_PROFILE_UP   // sub-phases of update_physics in slots 11-13 instead of b2_step's
+#define PROFB(ph) do { } while (0)
+#define PROFU(ph) PROF(ph)
+#else
+#define PROFB(ph) PROF(ph)
+#define PROFU(ph) do { } while (0)
+#endif
 #define PROF_RT(slot) do { unsigned long long _t = __builtin_amdgcn_s_memrealtime(); \
     if (g_prof && (threadIdx.x & 63) == 0) g_prof[((size_t)blockIdx.x * (BLOCK / 64) + threadIdx.x / 64) * 16 + (slot)] = _t; } while (0)
 #else
 #define PROF(ph) do { } while (0)
 #define PROFS(ph) do { } while (0)
+#define PROFB(ph) do { } while (0)
+#define PROFU(ph) do { } while (0)
 #define PCOUNT(slot, v) do { } while (0)
 #define PROF_RT(slot) do { } while (0)
 #endif
@@ -748,7 +757,7 @@ __device__ inline void solve(Car& c, const WallSet& S, float dt, float dtRatio, 
       c.awake = 0; c.sleep = 0.0f; c.v = zero2(); c.w = 0.0f; c.force = zero2(); c.torque = 0.0f;
     }
   }
-  PROF(12);
+  PROFB(12);
   sync_fixtures(c);
   find_new_contacts(c, S);
 }
@@ -1087,9 +1096,9 @@ __device__ inline void b2_step(Car& c, const WallSet& S, float dt, float frictio
   float inv_dt = dt > 0.0f ? fdiv_cr(1.0f, dt) : 0.0f;
   float dtRatio = c.invdt0 * dt;
   collide(c, W);
-  PROF(11);
+  PROFB(11);
   solve(c, S, dt, dtRatio, friction);
-  PROF(13);
+  PROFB(13);
   solve_toi(c, S, dt, friction);
   c.invdt0 = inv_dt;
   c.force = zero2(); c.torque = 0.0f;

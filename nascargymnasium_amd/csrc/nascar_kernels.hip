@@ -301,6 +301,7 @@ __device__ inline void car_update_physics(const Params& P, Car& c, int n, const 
     V2 pt = V((c.xf.q.c * lx - c.xf.q.s * ly) + c.xf.p.x, (c.xf.q.s * lx + c.xf.q.c * ly) + c.xf.p.y);
     apply_force(c, OV(Fx, Fy), pt);
   }
+  PROFU(11);
   if (c.brk > 0.01) {  // _apply_brake_force (:451-469)
     double sfac = 1.0 - pymin(0.3, fabs(c.steer) * 1.5);
     double mbf = CAR_MASS * 14.0 * sfac;
@@ -336,22 +337,34 @@ __device__ inline void car_update_physics(const Params& P, Car& c, int n, const 
     double lon = ax * fwd.x + ay * fwd.y, lat = ax * rtx + ay * rty;
     lon = pymax(-12.0, pymin(12.0, lon));
     lat = pymax(-12.0, pymin(12.0, lat));
+    // history kept oldest-first in HBM (acc_head stays 0): load the 10 slots (independent loads,
+    // issued together), shift/append in registers, sum oldest -> newest like Python's sum(), store back
     double* acc = P.acc;
     const size_t N = P.N;
-    int slot;
-    if (c.acc_len == 10) { slot = c.acc_head; c.acc_head = (c.acc_head + 1) % 10; }
-    else { slot = (c.acc_head + c.acc_len) % 10; c.acc_len++; }
-    acc[(size_t)(2 * slot) * N + n] = lon; acc[(size_t)(2 * slot + 1) * N + n] = lat;
-    double s0 = 0.0, s1 = 0.0;
-    for (int k = 0; k < c.acc_len; ++k) {
-      int idx = (c.acc_head + k) % 10;
-      s0 += acc[(size_t)(2 * idx) * N + n]; s1 += acc[(size_t)(2 * idx + 1) * N + n];
+    double hl[10], ht[10];
+#pragma unroll
+    for (int q = 0; q < 10; ++q) { hl[q] = acc[(size_t)(2 * q) * N + n]; ht[q] = acc[(size_t)(2 * q + 1) * N + n]; }
+    if (c.acc_len == 10) {
+#pragma unroll
+      for (int q = 0; q < 9; ++q) { hl[q] = hl[q + 1]; ht[q] = ht[q + 1]; }
+      hl[9] = lon; ht[9] = lat;
+    } else {
+#pragma unroll
+      for (int q = 0; q < 10; ++q) if (q == c.acc_len) { hl[q] = lon; ht[q] = lat; }
+      c.acc_len++;
     }
+    c.acc_head = 0;
+    double s0 = 0.0, s1 = 0.0;
+#pragma unroll
+    for (int q = 0; q < 10; ++q) if (q < c.acc_len) { s0 += hl[q]; s1 += ht[q]; }
+#pragma unroll
+    for (int q = 0; q < 10; ++q) { acc[(size_t)(2 * q) * N + n] = hl[q]; acc[(size_t)(2 * q + 1) * N + n] = ht[q]; }
     alon = s0 / c.acc_len; alat = s1 / c.acc_len;
     DBG(n, 6, alon); DBG(n, 7, alat);
 
     c.pvx = cvx; c.pvy = cvy;
   }
+  PROFU(12);
   {  // TyreManager.update (src/tyre_manager.py:78-97)
     double speed = (double)vlen(c.v);
     double loads[4];
@@ -364,6 +377,7 @@ __device__ inline void car_update_physics(const Params& P, Car& c, int n, const 
 #pragma unroll
     for (int i = 0; i < 4; ++i) tyre_update(c, i, dt, loads[i], fr[i], speed, alat, c.slip);
   }
+  PROFU(13);
   {  // _apply_lateral_tire_forces (:635-700)
     double speed = (double)vlen(c.v);
     if (speed > 0.05) {
@@ -823,7 +837,14 @@ __global__ void __launch_bounds__(BLOCK) step_kernel(Params P, const void* actio
   const int n = env >= 0 ? env * C + car : 0;
   PROF_RT(14);
   PROF(0);
-  const TrackDev T = P.tracks[P.blk_track[blockIdx.x]];
+  __shared__ DSeg s_segs[MAX_SEG];
+  __shared__ double s_prefix[MAX_SEG];
+  __shared__ float s_obs[BLOCK * 22];
+  __shared__ int s_rowbase[BLOCK];
+  TrackDev T = P.tracks[P.blk_track[blockIdx.x]];
+  if (tid < T.nseg) { s_segs[tid] = T.segs[tid]; s_prefix[tid] = T.prefix[tid]; }
+  __syncthreads();
+  T.segs = s_segs; T.prefix = s_prefix;
   PROF(1);
   const int nw = T.nwall;
   const WallSet S{T.walls, nw, T.bp, T.sn};
@@ -981,7 +1002,6 @@ __global__ void __launch_bounds__(BLOCK) step_kernel(Params P, const void* actio
     reward[n] = rew;
     if (car_flags) car_flags[n] = flags;
     const bool reset_now = auto_reset && s_envdone[el];
-    float* orow = obs + (size_t)n * 38;
     PROF(9);
     if (terminal_obs) { float* t = terminal_obs + (size_t)n * 38; for (int i = 0; i < 22; ++i) t[i] = o[i]; }
     if (reset_now) {
@@ -992,16 +1012,24 @@ __global__ void __launch_bounds__(BLOCK) step_kernel(Params P, const void* actio
     } else {
       P.pose[n] = car_pose(c, terminal_obs ? (PM_A_OBS | PM_A_TERM) : PM_A_OBS);
     }
-    for (int i = 0; i < 22; ++i) orow[i] = o[i];
+    for (int i = 0; i < 22; ++i) s_obs[tid * 22 + i] = o[i];
     car_store(P, n, c);
     PROF(10);
-    PROF_RT(15);
     if (reset_now && car == 0) {
       P.env_time[env] = 0.0;
       P.env_i32[E_PENDING * P.E + env] = 0; P.env_i32[E_REASON * P.E + env] = 0;
       P.env_i32[E_TERMINATED * P.E + env] = 0; P.env_i32[E_TRUNCATED * P.E + env] = 0;
     }
   }
+  s_rowbase[tid] = env >= 0 ? n * 38 : -1;
+  __syncthreads();
+  // obs[:, 0:22] rows of this workgroup, written 22 consecutive floats per row by consecutive lanes
+  for (int i = tid; i < BLOCK * 22; i += BLOCK) {
+    const int row = i / 22, col = i - row * 22;
+    const int base = s_rowbase[row];
+    if (base >= 0) obs[(size_t)base + col] = s_obs[i];
+  }
+  PROF_RT(15);
 }
 
 __global__ void __launch_bounds__(BLOCK) reset_kernel(Params P, const uint8_t* mask, float* obs) {

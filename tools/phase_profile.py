@@ -29,8 +29,10 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=100)
     ap.add_argument("--no-build", action="store_true")
+    ap.add_argument("--lib", default="libnascar_prof.so")
+    ap.add_argument("--up", action="store_true", help="library built with -DNASCAR_PROFILE_UP")
     a = ap.parse_args()
-    so = os.path.join(ROOT, "tools", "libnascar_prof.so")
+    so = os.path.join(ROOT, "tools", a.lib)
     if not a.no_build:
         subprocess.run(["hipcc"] + _lib.HIPCC_FLAGS + ["-DNASCAR_PROFILE", "-o", so,
                         os.path.join(_lib.CSRC, "nascar_kernels.hip")], check=True)
@@ -84,8 +86,17 @@ def main():
     for k, name in enumerate(PHASES):
         print(f"  {name:28s} mean {d[:, k].mean():10.0f}  max {d[:, k].max():10.0f}  {100 * d[:, k].mean() / tot.mean():5.1f}%")
     if len(sub):
-        for k, name in enumerate(["collide", "solve", "sync_fixtures+find_new_contacts", "solve_toi"]):
-            print(f"    b2_step/{name:30s} mean {sub[:, k].mean():10.0f}  max {sub[:, k].max():10.0f}")
+        names = (["engine force", "brake/drag/rolling + acc history", "weight transfer + tyres", "lateral..end"]
+                 if a.up else ["collide", "solve", "sync_fixtures+find_new_contacts", "solve_toi"])
+        pre = "update_physics" if a.up else "b2_step"
+        if a.up:   # slots: 2 -> 11 -> 12 -> 13 -> 3
+            sub = []
+            for b in acc:
+                b = b[(b[:, 10] != 0) & (b[:, 11] != 0) & (b[:, 12] != 0) & (b[:, 13] != 0)].astype(np.float64)
+                sub.append(np.stack([b[:, 11] - b[:, 2], b[:, 12] - b[:, 11], b[:, 13] - b[:, 12], b[:, 3] - b[:, 13]], 1))
+            sub = np.concatenate(sub)
+        for k, name in enumerate(names):
+            print(f"    {pre}/{name:34s} mean {sub[:, k].mean():10.0f}  max {sub[:, k].max():10.0f}")
     sd = np.concatenate(sens)
     if len(sd):
         print(f"sensor_kernel: waves/launch {len(sens[0])}, mean wave cycles {sd.sum(1).mean():.0f}")
