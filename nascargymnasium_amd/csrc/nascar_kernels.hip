@@ -670,6 +670,35 @@ __device__ __forceinline__ unsigned ray_mask(float rx, float ry, float d, float 
   return ((m << (lo & 15)) | (m >> (16 - (lo & 15)))) & 0xFFFFu;
 }
 
+// Rays that can meet a long thin wall: the box lies inside the capsule of its centre line
+// (end points A, B) with radius rr; seen from p1 the capsule spans the arc between the
+// directions to A and B (< pi when p1 is off the segment) widened by asin(rr / dist).
+// dseg returns the point-to-segment distance (occlusion bound).
+__device__ __forceinline__ unsigned seg_ray_mask(float ax, float ay, float bx, float by, float rr, float angf, float& dseg) {
+  const float sx = bx - ax, sy = by - ay;
+  const float ll = sx * sx + sy * sy;
+  float tt = ll > 0.0f ? -(ax * sx + ay * sy) * __builtin_amdgcn_rcpf(ll) : 0.0f;
+  tt = fminf(1.0f, fmaxf(0.0f, tt));
+  const float qx = ax + tt * sx, qy = ay + tt * sy;
+  dseg = __builtin_amdgcn_sqrtf(qx * qx + qy * qy);
+  if (dseg <= rr * 1.0001f + 0.05f) return 0xFFFFu;
+  const float K = 2.54647909f;   // 8 / pi
+  const float x = rr * __builtin_amdgcn_rcpf(dseg) * 1.0001f;
+  const float half = fminf(x * (1.0f + 0.5708f * x * x), 1.5708f) + 2e-3f;   // >= asin(rr / dseg) + guard
+  float ua = (angf - atan2_approx(ay, ax)) * K, ub = (angf - atan2_approx(by, bx)) * K;
+  ua = ua - 16.0f * floorf(ua * 0.0625f);
+  ub = ub - 16.0f * floorf(ub * 0.0625f);
+  if (ub < ua) { const float tmp = ua; ua = ub; ub = tmp; }
+  if (ub - ua > 8.0f) { const float tmp = ua + 16.0f; ua = ub; ub = tmp; }   // take the short arc
+  const float w = half * K;
+  const int lo = (int)ceilf(ua - w), hi = (int)floorf(ub + w);
+  const int cnt = hi - lo + 1;
+  if (cnt <= 0) return 0u;
+  if (cnt >= 16) return 0xFFFFu;
+  const unsigned m = (1u << cnt) - 1u;
+  return ((m << (lo & 15)) | (m >> (16 - (lo & 15)))) & 0xFFFFu;
+}
+
 template <int LPC>
 __global__ void __launch_bounds__(BLOCK) sensor_kernel(Params P, float* obs, float* terminal_obs) {
   constexpr int CPW = BLOCK / LPC;          // cars per workgroup
@@ -717,7 +746,8 @@ __global__ void __launch_bounds__(BLOCK) sensor_kernel(Params P, float* obs, flo
       const int i = r * RPL + q;
       if (active) {
         double sa = -((double)i * (360.0 / 16) * RAD_PER_DEG) + ang;
-        double dx = cos(sa), dy = sin(sa);
+        double dy, dx;
+        sincos(sa, &dy, &dx);
         V2 p2 = OV(px + dx * 250.0, py + dy * 250.0);
         s_p2[(lc * 16 + i) * 2] = p2.x; s_p2[(lc * 16 + i) * 2 + 1] = p2.y;
         s_dir[(lc * 16 + i) * 2] = (float)dx; s_dir[(lc * 16 + i) * 2 + 1] = (float)dy;
@@ -747,8 +777,20 @@ __global__ void __launch_bounds__(BLOCK) sensor_kernel(Params P, float* obs, flo
         if (d2 > (250.0f + G.z) * (250.0f + G.z)) continue;
         const float d = __builtin_amdgcn_sqrtf(d2);
         CNT(c_rng);
-        unsigned mask = ray_mask(grx, gry, d, G.z, angf);
-        const float dlo = (d - G.z) * (1.0f / 250.0f) - 1e-4f;   // lower bound of any hit fraction in the group
+        unsigned mask;
+        float dlo;   // lower bound of any hit fraction in the group
+        if (G.z > 24.0f) {   // a single long (straight) wall: mask from its end points
+          const int j = __float_as_int(G.w) & 0xFFFF;
+          const float4 wa = swa[j], wb = swb[j];
+          const float ex = wa.w * wb.y, ey = wa.w * wb.x;   // hx * (qc, qs)
+          const float cx = wa.x - p1.x, cy = wa.y - p1.y;
+          float dseg;
+          mask = seg_ray_mask(cx - ex, cy - ey, cx + ex, cy + ey, wb.z * 1.4143f + 0.3f, angf, dseg);
+          dlo = (dseg - (wb.z * 1.4143f + 0.3f)) * (1.0f / 250.0f) - 1e-4f;
+        } else {
+          mask = ray_mask(grx, gry, d, G.z, angf);
+          dlo = (d - G.z) * (1.0f / 250.0f) - 1e-4f;
+        }
         unsigned open = 0u;
         while (mask) {
           const int i = __builtin_ctz(mask);

@@ -60,8 +60,8 @@ def main():
         acc.append(buf[:2 * nwaves * 16].view(2 * nwaves, 16).cpu().numpy().copy())
         cnt = buf[2 * nwaves * 16:].cpu().numpy()
         if cnt[6]:
-            print("sensor lanes %d: per lane groups visited %.1f in-range %.1f open %.1f | walls %.1f wall-ray culls %.1f exact %.1f"
-                  % (cnt[6], *(cnt[:6] / cnt[6])))
+            print("sensor workgroups %d: per WG items %.1f q1 %.1f q2 %.1f | rays with a hit (any lane) %.1f | active cars %.1f"
+                  % (cnt[6], cnt[0] / cnt[6], cnt[1] / cnt[6], cnt[2] / cnt[6], cnt[3] / cnt[6], cnt[5] / cnt[6]))
     L.nascar_debug_profile(ctypes.c_void_p(0))
     sens = []
     for b in acc:
