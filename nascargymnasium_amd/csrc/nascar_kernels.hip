@@ -823,6 +823,8 @@ __global__ void __launch_bounds__(BLOCK) sensor_kernel(Params P, float* obs, flo
             const float dx = dirs[2 * i], dy = dirs[2 * i + 1];
             const float tc = rx * dx + ry * dy, perp = fabsf(rx * dy - ry * dx);
             if (perp > R || tc < -R || (tc - R) > 250.0f * bi) continue;
+            // separating axis along the ray normal: the box must straddle the ray line (+2 cm guard)
+            if (perp > hx * fabsf(q.c * dy - q.s * dx) + hy * fabsf(q.s * dy + q.c * dx) + 0.02f) continue;
             CNT(c_ex);
             const V2 l2 = rmulT(q, V(p2s[2 * i] - wa.x, p2s[2 * i + 1] - wa.y));
             const V2 dd = vsub(l2, l1);
