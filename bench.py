@@ -132,7 +132,7 @@ def main():
         try:
             tj = json.load(open(tfile))
             if tj.get("envs") == E and tj.get("cars") == C and tj.get("track") == os.path.basename(tpath):
-                traffic = tj.get("bytes_per_launch")
+                traffic = tj.get("bytes_per_step")
         except Exception:
             traffic = None
     out = {
@@ -145,7 +145,7 @@ def main():
                    "envs_per_gpu": E, "cars_per_env": C, "track": os.path.basename(tpath), "parallelism": f"dp{world} (env shards, no collective)"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": "step_kernel", "kernel_ms": kern_ms,
+                     "kernel": "step_kernel + sensor_kernel (one env step)", "kernel_ms": kern_ms,
                      "algo_bytes_per_car_step": ALGO_BYTES_PER_CAR_STEP},
         "engine_errors": errs,
     }

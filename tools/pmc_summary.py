@@ -3,11 +3,12 @@
     python tools/pmc_summary.py <out_dir> <tag>
 
 Reads the rocprofv3 CSVs under <out_dir>/{kt,fetch,write}, and writes
-  profiles/<tag>_kernel_stats.csv     (rocprofv3 --stats summary, copied verbatim)
-  profiles/<tag>_pmc_step_kernel.json (per-launch FETCH_SIZE / WRITE_SIZE of step_kernel)
-  profiles/pmc_traffic.json           (read by bench.py for roofline.traffic)
-HBM bytes per launch = (2 * FETCH_SIZE + WRITE_SIZE) * 1024: FETCH_SIZE/WRITE_SIZE are in KiB and
-gfx950 FETCH_SIZE tallies half the bytes of a wide coalesced read (MI355X_MICROARCH.md "HBM").
+  profiles/<tag>_kernel_stats.csv  (rocprofv3 --stats summary, copied verbatim)
+  profiles/<tag>_pmc_step.json     (per-dispatch FETCH_SIZE / WRITE_SIZE of the two kernels of a step)
+  profiles/pmc_traffic.json        (read by bench.py for roofline.traffic)
+One env step = one step_kernel + one sensor_kernel launch.  HBM bytes = (2 * FETCH_SIZE + WRITE_SIZE)
+* 1024: FETCH_SIZE/WRITE_SIZE are in KiB and gfx950 FETCH_SIZE tallies half the bytes of a wide
+coalesced read (MI355X_MICROARCH.md "HBM").
 """
 import csv
 import glob
@@ -18,7 +19,7 @@ import sys
 from collections import defaultdict
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNEL = "step_kernel"
+KERNELS = ("step_kernel", "sensor_kernel")
 
 
 def _find(d, suffix):
@@ -34,10 +35,10 @@ def _bench_line(log):
     return None
 
 
-def _per_dispatch(path, counter):
+def _per_dispatch(path, counter, kernel):
     vals = defaultdict(float)
     for row in csv.DictReader(open(path)):
-        if KERNEL not in row.get("Kernel_Name", "") or row.get("Counter_Name") != counter:
+        if kernel not in row.get("Kernel_Name", "") or row.get("Counter_Name") != counter:
             continue
         vals[row["Dispatch_Id"]] += float(row["Counter_Value"])
     return list(vals.values())
@@ -52,30 +53,41 @@ def main():
     if stats:
         shutil.copy(stats, os.path.join(prof, f"{tag}_kernel_stats.csv"))
         for row in csv.DictReader(open(stats)):
-            if KERNEL in row["Name"]:
-                res["rocprof_avg_ns"] = float(row["AverageNs"])
-                res["rocprof_calls"] = int(row["Calls"])
+            for kn in KERNELS:
+                if row["Name"].startswith(kn) or ("void " + kn) in row["Name"]:
+                    res[f"{kn}_rocprof_avg_ns"] = float(row["AverageNs"])
+                    res[f"{kn}_rocprof_calls"] = int(row["Calls"])
+        res["step_rocprof_avg_ns"] = sum(res.get(f"{kn}_rocprof_avg_ns", 0.0) for kn in KERNELS)
     b = _bench_line(os.path.join(out, "kt.log"))
     if b:
         res["bench_under_rocprof"] = b
         cfg = b["config"]
         res.update(envs=cfg["envs_per_gpu"], cars=cfg["cars_per_env"], track=cfg["track"])
-        res["bench_kernel_ms_events"] = b["roofline"]["kernel_ms"]
+        res["bench_step_ms_events"] = b["roofline"]["kernel_ms"]
     f = _find(os.path.join(out, "fetch"), "counter_collection.csv")
     w = _find(os.path.join(out, "write"), "counter_collection.csv")
     if f and w:
-        fv, wv = _per_dispatch(f, "FETCH_SIZE"), _per_dispatch(w, "WRITE_SIZE")
-        if fv and wv:
-            fetch_kb, write_kb = sum(fv) / len(fv), sum(wv) / len(wv)
-            res.update(fetch_size_kb=fetch_kb, write_size_kb=write_kb, dispatches=[len(fv), len(wv)],
-                       bytes_per_launch=(2 * fetch_kb + write_kb) * 1024.0,
-                       bytes_per_launch_uncorrected=(fetch_kb + write_kb) * 1024.0)
+        tot_f = tot_w = 0.0
+        ok = True
+        for kn in KERNELS:
+            fv, wv = _per_dispatch(f, "FETCH_SIZE", kn), _per_dispatch(w, "WRITE_SIZE", kn)
+            if not (fv and wv):
+                ok = False
+                continue
+            fk, wk = sum(fv) / len(fv), sum(wv) / len(wv)
+            res[f"{kn}_fetch_size_kb"], res[f"{kn}_write_size_kb"] = fk, wk
+            res[f"{kn}_bytes"] = (2 * fk + wk) * 1024.0
+            tot_f += fk
+            tot_w += wk
+        if ok:
+            res.update(fetch_size_kb=tot_f, write_size_kb=tot_w, bytes_per_step=(2 * tot_f + tot_w) * 1024.0,
+                       bytes_per_step_uncorrected=(tot_f + tot_w) * 1024.0)
             if "envs" in res:
-                res["bytes_per_car_step"] = res["bytes_per_launch"] / (res["envs"] * res["cars"])
-    json.dump(res, open(os.path.join(prof, f"{tag}_pmc_step_kernel.json"), "w"), indent=1)
-    if "bytes_per_launch" in res and "envs" in res:
-        json.dump({k: res[k] for k in ("envs", "cars", "track", "bytes_per_launch", "bytes_per_launch_uncorrected",
-                                       "fetch_size_kb", "write_size_kb", "tag")},
+                res["bytes_per_car_step"] = res["bytes_per_step"] / (res["envs"] * res["cars"])
+    json.dump(res, open(os.path.join(prof, f"{tag}_pmc_step.json"), "w"), indent=1)
+    if "bytes_per_step" in res and "envs" in res:
+        json.dump({k: res[k] for k in ("envs", "cars", "track", "bytes_per_step", "bytes_per_step_uncorrected",
+                                       "bytes_per_car_step", "fetch_size_kb", "write_size_kb", "tag")},
                   open(os.path.join(prof, "pmc_traffic.json"), "w"), indent=1)
     print(json.dumps(res, indent=1))
 

@@ -17,4 +17,4 @@ timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv 
     python3 "$ROOT/bench.py" --steps 10 --warmup 2 --no-cpu-baseline $BENCH_ARGS > "$OUT/fetch.log" 2>&1 || exit $?
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$OUT/write" -o run -- \
     python3 "$ROOT/bench.py" --steps 10 --warmup 2 --no-cpu-baseline $BENCH_ARGS > "$OUT/write.log" 2>&1 || exit $?
-python3 "$ROOT/tools/pmc_summary.py" "$OUT" "$TAG" $BENCH_ARGS
+echo "profile-ok: run python tools/pmc_summary.py gpurun_out/prof $TAG locally"
