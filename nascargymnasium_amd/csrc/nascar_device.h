@@ -16,7 +16,10 @@
 
 #pragma clang fp contract(off)
 
-#define BLOCK 256   // threads per workgroup of the per-car kernels
+#define BLOCK 256   // threads per workgroup of the sensor kernel
+#ifndef SBLOCK
+#define SBLOCK 128  // threads per workgroup of the one-lane-per-car kernels (whole envs)
+#endif
 
 #ifdef NASCAR_PROFILE
 // profile build only: per-wave s_memtime stamps at phase boundaries of step_kernel

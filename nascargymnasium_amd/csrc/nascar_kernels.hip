@@ -708,7 +708,8 @@ __global__ void __launch_bounds__(BLOCK) sensor_kernel(Params P, float* obs, flo
   __shared__ float s_dir[CPW * 32];         // [car][ray][x, y]: unit ray directions (cull only)
   __shared__ unsigned s_best[CPW * 16];     // [car][ray]: best fraction so far (float bits, >= 0)
   float4* swa = (float4*)smem;
-  const int b = blockIdx.x / LPC, sub = blockIdx.x - b * LPC;
+  constexpr int SUB = (SBLOCK + CPW - 1) / CPW;   // sensor workgroups per step-kernel workgroup
+  const int b = blockIdx.x / SUB, sub = blockIdx.x - b * SUB;
   const int t = threadIdx.x, lc = t / LPC, r = t - lc * LPC;
   const int C = P.C;
   const int slot = sub * CPW + lc;          // car slot within the step kernel's workgroup b
@@ -869,11 +870,11 @@ __global__ void __launch_bounds__(BLOCK) sensor_kernel(Params P, float* obs, flo
   }
 }
 
-__global__ void __launch_bounds__(BLOCK) step_kernel(Params P, const void* actions, int discrete, float* obs, float* reward,
+__global__ void __launch_bounds__(SBLOCK) step_kernel(Params P, const void* actions, int discrete, float* obs, float* reward,
                                                      uint8_t* car_flags, uint8_t* env_flags, int auto_reset, float* terminal_obs) {
-  __shared__ int s_laps_old[BLOCK], s_dis_old[BLOCK], s_laps_new[BLOCK], s_dis_new[BLOCK], s_lapdone[BLOCK];
-  __shared__ int s_dis_final[BLOCK], s_below[BLOCK];
-  __shared__ int s_envdone[BLOCK / 1];
+  __shared__ int s_laps_old[SBLOCK], s_dis_old[SBLOCK], s_laps_new[SBLOCK], s_dis_new[SBLOCK], s_lapdone[SBLOCK];
+  __shared__ int s_dis_final[SBLOCK], s_below[SBLOCK];
+  __shared__ int s_envdone[SBLOCK];
   const int tid = threadIdx.x, C = P.C;
   const int el = tid / C, car = tid - el * C;
   const int slot = blockIdx.x * P.epb + el;
@@ -883,8 +884,8 @@ __global__ void __launch_bounds__(BLOCK) step_kernel(Params P, const void* actio
   PROF(0);
   __shared__ DSeg s_segs[MAX_SEG];
   __shared__ double s_prefix[MAX_SEG];
-  __shared__ float s_obs[BLOCK * 22];
-  __shared__ int s_rowbase[BLOCK];
+  __shared__ float s_obs[SBLOCK * 22];
+  __shared__ int s_rowbase[SBLOCK];
   TrackDev T = P.tracks[P.blk_track[blockIdx.x]];
   if (tid < T.nseg) { s_segs[tid] = T.segs[tid]; s_prefix[tid] = T.prefix[tid]; }
   __syncthreads();
@@ -1068,7 +1069,7 @@ __global__ void __launch_bounds__(BLOCK) step_kernel(Params P, const void* actio
   s_rowbase[tid] = env >= 0 ? n * 38 : -1;
   __syncthreads();
   // obs[:, 0:22] rows of this workgroup, written 22 consecutive floats per row by consecutive lanes
-  for (int i = tid; i < BLOCK * 22; i += BLOCK) {
+  for (int i = tid; i < SBLOCK * 22; i += SBLOCK) {
     const int row = i / 22, col = i - row * 22;
     const int base = s_rowbase[row];
     if (base >= 0) obs[(size_t)base + col] = s_obs[i];
@@ -1076,7 +1077,7 @@ __global__ void __launch_bounds__(BLOCK) step_kernel(Params P, const void* actio
   PROF_RT(15);
 }
 
-__global__ void __launch_bounds__(BLOCK) reset_kernel(Params P, const uint8_t* mask, float* obs) {
+__global__ void __launch_bounds__(SBLOCK) reset_kernel(Params P, const uint8_t* mask, float* obs) {
   const int tid = threadIdx.x, C = P.C;
   const int el = tid / C, car = tid - el * C;
   const int slot = blockIdx.x * P.epb + el;
@@ -1104,7 +1105,7 @@ __global__ void __launch_bounds__(BLOCK) reset_kernel(Params P, const uint8_t* m
   }
 }
 
-__global__ void __launch_bounds__(BLOCK) info_kernel(Params P, double* info) {
+__global__ void __launch_bounds__(SBLOCK) info_kernel(Params P, double* info) {
   const int tid = threadIdx.x, C = P.C;
   const int el = tid / C, car = tid - el * C;
   const int slot = blockIdx.x * P.epb + el;
@@ -1308,7 +1309,7 @@ extern "C" int nascar_create(const NascarConfig* cfg, NascarHandle** out) {
   NascarHandle* h = new NascarHandle();
   h->cfg = *cfg;
   h->E = cfg->num_envs; h->C = cfg->num_cars; h->N = h->E * h->C;
-  h->epb = BLOCK / h->C;
+  h->epb = SBLOCK / h->C;
   size_t N = h->N, E = h->E, o = 0;
   h->off_f32 = o; o = align256(o + sizeof(float) * N_F32 * N);
   h->off_f64 = o; o = align256(o + sizeof(double) * N_F64 * N);
@@ -1478,7 +1479,8 @@ static Params make_params(NascarHandle* h) {
 
 static void launch_sensors(NascarHandle* h, const Params& P, float* obs, float* terminal_obs, void* stream) {
   const size_t lds = h->max_sensor_lds;
-  hipLaunchKernelGGL(sensor_kernel<SENSOR_LPC>, dim3(h->nblocks * SENSOR_LPC), dim3(BLOCK), lds, (hipStream_t)stream,
+  const int sub = (SBLOCK + BLOCK / SENSOR_LPC - 1) / (BLOCK / SENSOR_LPC);
+  hipLaunchKernelGGL(sensor_kernel<SENSOR_LPC>, dim3(h->nblocks * sub), dim3(BLOCK), lds, (hipStream_t)stream,
                      P, obs, terminal_obs);
 }
 
@@ -1486,7 +1488,7 @@ extern "C" int nascar_reset(NascarHandle* h, const uint8_t* env_mask, float* obs
   if (!h || !obs) return fail("null argument");
   if (prepare(h)) return -1;
   Params P = make_params(h);
-  hipLaunchKernelGGL(reset_kernel, dim3(h->nblocks), dim3(BLOCK), 0, (hipStream_t)stream, P, env_mask, obs);
+  hipLaunchKernelGGL(reset_kernel, dim3(h->nblocks), dim3(SBLOCK), 0, (hipStream_t)stream, P, env_mask, obs);
   HIPCHK(hipGetLastError());
   launch_sensors(h, P, obs, nullptr, stream);
   HIPCHK(hipGetLastError());
@@ -1498,7 +1500,7 @@ extern "C" int nascar_step(NascarHandle* h, const void* actions, int32_t discret
   if (!h || !actions || !obs || !reward) return fail("null argument");
   if (prepare(h)) return -1;
   Params P = make_params(h);
-  hipLaunchKernelGGL(step_kernel, dim3(h->nblocks), dim3(BLOCK), 0, (hipStream_t)stream, P, actions, discrete,
+  hipLaunchKernelGGL(step_kernel, dim3(h->nblocks), dim3(SBLOCK), 0, (hipStream_t)stream, P, actions, discrete,
                      obs, reward, car_flags, env_flags, auto_reset, terminal_obs);
   HIPCHK(hipGetLastError());
   launch_sensors(h, P, obs, terminal_obs, stream);
@@ -1510,7 +1512,7 @@ extern "C" int nascar_get_info(NascarHandle* h, double* info, void* stream) {
   if (!h || !info) return fail("null argument");
   if (prepare(h)) return -1;
   Params P = make_params(h);
-  hipLaunchKernelGGL(info_kernel, dim3(h->nblocks), dim3(BLOCK), 0, (hipStream_t)stream, P, info);
+  hipLaunchKernelGGL(info_kernel, dim3(h->nblocks), dim3(SBLOCK), 0, (hipStream_t)stream, P, info);
   HIPCHK(hipGetLastError());
   return 0;
 }
