@@ -1135,7 +1135,7 @@ __device__ __forceinline__ uint32_t mix32(uint64_t x) {   // splitmix64 finalise
   x ^= x >> 31;
   return (uint32_t)(x >> 32);
 }
-__global__ void policy_kernel(int N, int policy, uint64_t seed, int64_t step, const float* obs, float* act, float* ctl) {
+__global__ void policy_kernel(int N, int policy, uint64_t seed, int64_t step, const float* obs, float* act, double* ctl) {
   const int n = blockIdx.x * blockDim.x + threadIdx.x;
   if (n >= N) return;
   if (policy == 0) {
@@ -1144,22 +1144,27 @@ __global__ void policy_kernel(int N, int policy, uint64_t seed, int64_t step, co
     act[2 * n + 1] = (float)(mix32(key ^ 0xABCDEF12345ull) >> 8) * (2.0f / 16777216.0f) - 1.0f;
     return;
   }
-  // BaseController._fallback_control (game/control/base_controller.py:39-103); state per car in ctl[4*n..]
+  // BaseController._fallback_control (game/control/base_controller.py:39-103); state per car in ctl[4*n..]:
+  // throttle_brake is a Python float (float64 += 0.1, *= 0.5, clamps); steering, speed_limit and
+  // last_forward hold numpy float32 values (NEP 50: float32 op python scalar stays float32).
   const float* o = obs + (size_t)n * 38;
-  float* s = ctl + 4 * (size_t)n;   // throttle_brake, steering, last_forward, speed_limit
-  float fwd = o[22], spd = o[4];
-  if (s[2] >= fwd) s[3] = fwd;
-  if (s[2] < fwd) s[3] = 1.0f;
-  if (spd < s[3] * 0.95f) s[0] += 0.1f;
-  if (spd > s[3] * 1.05f) s[0] -= 0.1f;
-  float r = o[22 + 15], l = o[22 + 1];
-  if (r > l) s[1] = 1.0f - (l / r);
-  else if (l > r) s[1] = (1.0f - (r / l)) * -1.0f;
-  else s[1] *= 0.9f;
-  if (fabsf(s[1]) > 0.25f) s[0] *= 0.5f;
-  s[0] = fmaxf(fminf(s[0], 1.0f), -1.0f); s[1] = fmaxf(fminf(s[1], 1.0f), -1.0f);
-  s[2] = fwd;
-  act[2 * n] = s[0]; act[2 * n + 1] = s[1];
+  double* s = ctl + 4 * (size_t)n;   // throttle_brake, steering, last_forward, speed_limit
+  const float fwd = o[22], spd = o[4];
+  float steer = (float)s[1], last = (float)s[2], lim = (float)s[3];
+  double tb = s[0];
+  if (last >= fwd) lim = fwd;
+  if (last < fwd) lim = 1.0f;
+  if (spd < lim * 0.95f) tb += 0.1;
+  if (spd > lim * 1.05f) tb -= 0.1;
+  const float r = o[22 + 15], l = o[22 + 1];
+  if (r > l) steer = 1.0f - (l / r);
+  else if (l > r) steer = (1.0f - (r / l)) * -1.0f;
+  else steer *= 0.9f;
+  if (fabsf(steer) > 0.25f) tb *= 0.5;
+  tb = tb > 1.0 ? 1.0 : tb;  tb = tb < -1.0 ? -1.0 : tb;            // max(min(tb, 1), -1)
+  steer = steer > 1.0f ? 1.0f : steer;  steer = steer < -1.0f ? -1.0f : steer;
+  s[0] = tb; s[1] = steer; s[2] = fwd; s[3] = lim;
+  act[2 * n] = (float)tb; act[2 * n + 1] = steer;
 }
 
 // =================================================================== host side / C ABI
@@ -1291,7 +1296,7 @@ struct NascarHandle {
   TrackDev* d_tracks = nullptr;
   int* d_blk_track = nullptr; int* d_blk_env = nullptr; int nblocks = 0;
   std::vector<int> env_track;
-  float* d_ctl = nullptr;    // rule-driver state for nascar_policy_actions
+  double* d_ctl = nullptr;   // rule-driver state for nascar_policy_actions
   float4* d_pose = nullptr;  // [2][N] step/reset -> sensor_kernel hand-off
   size_t max_lds = 0, max_sensor_lds = 0;
   bool dirty_tracks = true;
@@ -1324,10 +1329,10 @@ extern "C" int nascar_create(const NascarConfig* cfg, NascarHandle** out) {
   hipError_t e = hipMalloc(&h->arena, o);
   if (e != hipSuccess) { delete h; return fail("hipMalloc(%zu) failed: %s", o, hipGetErrorString(e)); }
   hipMemset(h->arena, 0, o);
-  hipMalloc(&h->d_ctl, sizeof(float) * 4 * N);
+  hipMalloc(&h->d_ctl, sizeof(double) * 4 * N);
   if (hipMalloc(&h->d_pose, sizeof(float4) * 2 * N) != hipSuccess) { hipFree(h->arena); hipFree(h->d_ctl); delete h; return fail("hipMalloc(pose) failed"); }
   hipMemset(h->d_pose, 0, sizeof(float4) * 2 * N);
-  hipMemset(h->d_ctl, 0, sizeof(float) * 4 * N);
+  hipMemset(h->d_ctl, 0, sizeof(double) * 4 * N);
   h->env_track.assign(E, 0);
   *out = h;
   return 0;

@@ -186,3 +186,24 @@ def test_mixed_tracks_one_launch():
         assert np.array_equal(so.cpu().numpy(), mo[envs]), t
         single.close()
     mixed.close()
+
+
+@pytest.mark.parametrize("name,car", [("daytona_long", 0), ("martinsville_lap", 0), ("michigan_banked", 0),
+                                      ("daytona_mixed", 0)])
+def test_device_rule_driver_matches_reference_controller(name, car):
+    """policy_kernel(1) is BaseController._fallback_control (game/control/base_controller.py:39-103):
+    closed loop on the GPU, its actions equal the reference controller's recorded in the golden trace
+    (the driver runs every step, including reset steps, as in oracle/gen_golden.py)."""
+    d = load(name)
+    C = int(d["C"])
+    env = _env(str(d["track"]), 1, C, bool(d["reset_on_lap"]))
+    env.reset()
+    acts = d["actions"]
+    for k in range(len(acts)):
+        a = env.policy_actions(1).clone()[0, car].cpu().numpy()
+        if d["reset"][k]:
+            env.reset()
+            continue
+        assert np.array_equal(a, acts[k][car]), f"step {k}: device {a} reference {acts[k][car]}"
+        env.step(torch.from_numpy(acts[k].reshape(1, C, 2).copy()).cuda())
+    env.close()
