@@ -140,16 +140,22 @@ __device__ __forceinline__ Rot rot_set(float a) { Rot q; q.s = dev_sinf(a); q.c 
 __device__ __forceinline__ V2 zero2() { return V(0.0f, 0.0f); }
 
 // ------------------------------------------------------------------ polygons
+// b2PolygonShape::SetAsBox(hx, hy).  The vertices/normals are kept in arrays: generating
+// them with selects on the vertex index (to save registers) was miscompiled by ROCm 7.2
+// hipcc -O3 inside find_incident_edge (wrong second incident vertex; standalone harness vs a
+// host reference: 50% of cases wrong, the array form 0%), so that is not done.
 struct Poly { V2 v[4]; V2 n[4]; float radius; };
 __device__ __forceinline__ void make_box(Poly* p, float hx, float hy) {
   p->radius = POLY_RADIUS;
   p->v[0] = V(-hx, -hy); p->v[1] = V(hx, -hy); p->v[2] = V(hx, hy); p->v[3] = V(-hx, hy);
   p->n[0] = V(0.0f, -1.0f); p->n[1] = V(1.0f, 0.0f); p->n[2] = V(0.0f, 1.0f); p->n[3] = V(-1.0f, 0.0f);
 }
+__device__ __forceinline__ V2 pv(const Poly* p, int i) { return p->v[i]; }
+__device__ __forceinline__ V2 pn(const Poly* p, int i) { return p->n[i]; }
 __device__ __forceinline__ Aabb poly_aabb(const Poly* p, Xf xf) {
-  V2 lower = xmul(xf, p->v[0]), upper = lower;
+  V2 lower = xmul(xf, pv(p, 0)), upper = lower;
 #pragma unroll
-  for (int i = 1; i < 4; ++i) { V2 v = xmul(xf, p->v[i]); lower = vmin(lower, v); upper = vmax(upper, v); }
+  for (int i = 1; i < 4; ++i) { V2 v = xmul(xf, pv(p, i)); lower = vmin(lower, v); upper = vmax(upper, v); }
   V2 r = V(p->radius, p->radius);
   Aabb a; a.lo = vsub(lower, r); a.hi = vadd(upper, r);
   return a;
@@ -330,22 +336,22 @@ __device__ inline float find_max_separation(int* edgeIndex, const Poly* p1, Xf x
   Xf xf = xmulT_xx(xf2, xf1);
   int best = 0; float maxSep = -FLT_BIG;
   for (int i = 0; i < 4; ++i) {
-    V2 n = rmul(xf.q, p1->n[i]);
-    V2 v1 = xmul(xf, p1->v[i]);
+    V2 n = rmul(xf.q, pn(p1, i));
+    V2 v1 = xmul(xf, pv(p1, i));
     float si = FLT_BIG;
-    for (int j = 0; j < 4; ++j) { float sij = vdot(n, vsub(p2->v[j], v1)); if (sij < si) si = sij; }
+    for (int j = 0; j < 4; ++j) { float sij = vdot(n, vsub(pv(p2, j), v1)); if (sij < si) si = sij; }
     if (si > maxSep) { maxSep = si; best = i; }
   }
   *edgeIndex = best;
   return maxSep;
 }
 __device__ inline void find_incident_edge(Clip c[2], const Poly* p1, Xf xf1, int edge1, const Poly* p2, Xf xf2) {
-  V2 normal1 = rmulT(xf2.q, rmul(xf1.q, p1->n[edge1]));
+  V2 normal1 = rmulT(xf2.q, rmul(xf1.q, pn(p1, edge1)));
   int index = 0; float minDot = FLT_BIG;
-  for (int i = 0; i < 4; ++i) { float d = vdot(normal1, p2->n[i]); if (d < minDot) { minDot = d; index = i; } }
+  for (int i = 0; i < 4; ++i) { float d = vdot(normal1, pn(p2, i)); if (d < minDot) { minDot = d; index = i; } }
   int i1 = index, i2 = i1 + 1 < 4 ? i1 + 1 : 0;
-  c[0].v = xmul(xf2, p2->v[i1]); c[0].id = cf_key(edge1, i1, 1, 0);
-  c[1].v = xmul(xf2, p2->v[i2]); c[1].id = cf_key(edge1, i2, 1, 0);
+  c[0].v = xmul(xf2, pv(p2, i1)); c[0].id = cf_key(edge1, i1, 1, 0);
+  c[1].v = xmul(xf2, pv(p2, i2)); c[1].id = cf_key(edge1, i2, 1, 0);
 }
 __device__ inline int clip_segment(Clip vOut[2], const Clip vIn[2], V2 normal, float offset, int vertexIndexA) {
   int numOut = 0;
@@ -376,7 +382,7 @@ __device__ inline void collide_polygons(DContact& m, const Poly* pA, Xf xfA, con
   Clip incident[2];
   find_incident_edge(incident, poly1, xf1, edge1, poly2, xf2);
   int iv1 = edge1, iv2 = edge1 + 1 < 4 ? edge1 + 1 : 0;
-  V2 v11 = poly1->v[iv1], v12 = poly1->v[iv2];
+  V2 v11 = pv(poly1, iv1), v12 = pv(poly1, iv2);
   V2 localTangent = vsub(v12, v11);
   vnormalize(&localTangent);
   V2 localNormal = vcross_vs(localTangent, 1.0f);
@@ -771,8 +777,8 @@ struct Simplex { SV v[3]; int count; };
 struct SCache { float metric; int count; int iA[3], iB[3]; };
 
 __device__ __forceinline__ int support(const Poly* p, V2 d) {
-  int best = 0; float bestValue = vdot(p->v[0], d);
-  for (int i = 1; i < 4; ++i) { float value = vdot(p->v[i], d); if (value > bestValue) { best = i; bestValue = value; } }
+  int best = 0; float bestValue = vdot(pv(p, 0), d);
+  for (int i = 1; i < 4; ++i) { float value = vdot(pv(p, i), d); if (value > bestValue) { best = i; bestValue = value; } }
   return best;
 }
 __device__ inline float simplex_metric(const Simplex& s) {
@@ -787,7 +793,7 @@ __device__ inline float gjk_distance(SCache& cache, const Poly* pA, Xf tA, const
   for (int i = 0; i < s.count; ++i) {
     SV& v = s.v[i];
     v.iA = cache.iA[i]; v.iB = cache.iB[i];
-    v.wA = xmul(tA, pA->v[v.iA]); v.wB = xmul(tB, pB->v[v.iB]);
+    v.wA = xmul(tA, pv(pA, v.iA)); v.wB = xmul(tB, pv(pB, v.iB));
     v.w = vsub(v.wB, v.wA); v.a = 0.0f;
   }
   if (s.count > 1) {
@@ -797,7 +803,7 @@ __device__ inline float gjk_distance(SCache& cache, const Poly* pA, Xf tA, const
   if (s.count == 0) {
     SV& v = s.v[0];
     v.iA = 0; v.iB = 0;
-    v.wA = xmul(tA, pA->v[0]); v.wB = xmul(tB, pB->v[0]);
+    v.wA = xmul(tA, pv(pA, 0)); v.wB = xmul(tB, pv(pB, 0));
     v.w = vsub(v.wB, v.wA); v.a = 1.0f;
     s.count = 1;
   }
@@ -849,9 +855,9 @@ __device__ inline float gjk_distance(SCache& cache, const Poly* pA, Xf tA, const
     if (vdot(d, d) < FLT_EPS * FLT_EPS) break;
     SV& vx = s.v[s.count];
     vx.iA = support(pA, rmulT(tA.q, vneg(d)));
-    vx.wA = xmul(tA, pA->v[vx.iA]);
+    vx.wA = xmul(tA, pv(pA, vx.iA));
     vx.iB = support(pB, rmulT(tB.q, d));
-    vx.wB = xmul(tB, pB->v[vx.iB]);
+    vx.wB = xmul(tB, pv(pB, vx.iB));
     vx.w = vsub(vx.wB, vx.wA);
     ++iter;
     bool dup = false;
@@ -896,28 +902,28 @@ __device__ inline void sep_init(SepFn& f, const SCache& cache, const Poly* pA, c
   Xf xfA = sweep_xf(f.sA, t1), xfB = sweep_xf(f.sB, t1);
   if (cache.count == 1) {
     f.type = SF_POINTS;
-    V2 pointA = xmul(xfA, pA->v[cache.iA[0]]), pointB = xmul(xfB, pB->v[cache.iB[0]]);
+    V2 pointA = xmul(xfA, pv(pA, cache.iA[0])), pointB = xmul(xfB, pv(pB, cache.iB[0]));
     f.axis = vsub(pointB, pointA);
     vnormalize(&f.axis);
     f.lp = zero2();
   } else if (cache.iA[0] == cache.iA[1]) {
     f.type = SF_FACEB;
-    V2 lB1 = pB->v[cache.iB[0]], lB2 = pB->v[cache.iB[1]];
+    V2 lB1 = pv(pB, cache.iB[0]), lB2 = pv(pB, cache.iB[1]);
     f.axis = vcross_vs(vsub(lB2, lB1), 1.0f);
     vnormalize(&f.axis);
     V2 normal = rmul(xfB.q, f.axis);
     f.lp = vmul(0.5f, vadd(lB1, lB2));
-    V2 pointB = xmul(xfB, f.lp), pointA = xmul(xfA, pA->v[cache.iA[0]]);
+    V2 pointB = xmul(xfB, f.lp), pointA = xmul(xfA, pv(pA, cache.iA[0]));
     float s = vdot(vsub(pointA, pointB), normal);
     if (s < 0.0f) f.axis = vneg(f.axis);
   } else {
     f.type = SF_FACEA;
-    V2 lA1 = pA->v[cache.iA[0]], lA2 = pA->v[cache.iA[1]];
+    V2 lA1 = pv(pA, cache.iA[0]), lA2 = pv(pA, cache.iA[1]);
     f.axis = vcross_vs(vsub(lA2, lA1), 1.0f);
     vnormalize(&f.axis);
     V2 normal = rmul(xfA.q, f.axis);
     f.lp = vmul(0.5f, vadd(lA1, lA2));
-    V2 pointA = xmul(xfA, f.lp), pointB = xmul(xfB, pB->v[cache.iB[0]]);
+    V2 pointA = xmul(xfA, f.lp), pointB = xmul(xfB, pv(pB, cache.iB[0]));
     float s = vdot(vsub(pointB, pointA), normal);
     if (s < 0.0f) f.axis = vneg(f.axis);
   }
@@ -927,32 +933,32 @@ __device__ inline float sep_find_min(const SepFn& f, const Poly* pA, const Poly*
   if (f.type == SF_POINTS) {
     V2 axisA = rmulT(xfA.q, f.axis), axisB = rmulT(xfB.q, vneg(f.axis));
     *iA = support(pA, axisA); *iB = support(pB, axisB);
-    V2 pointA = xmul(xfA, pA->v[*iA]), pointB = xmul(xfB, pB->v[*iB]);
+    V2 pointA = xmul(xfA, pv(pA, *iA)), pointB = xmul(xfB, pv(pB, *iB));
     return vdot(vsub(pointB, pointA), f.axis);
   } else if (f.type == SF_FACEA) {
     V2 normal = rmul(xfA.q, f.axis), pointA = xmul(xfA, f.lp);
     V2 axisB = rmulT(xfB.q, vneg(normal));
     *iA = -1; *iB = support(pB, axisB);
-    V2 pointB = xmul(xfB, pB->v[*iB]);
+    V2 pointB = xmul(xfB, pv(pB, *iB));
     return vdot(vsub(pointB, pointA), normal);
   } else {
     V2 normal = rmul(xfB.q, f.axis), pointB = xmul(xfB, f.lp);
     V2 axisA = rmulT(xfA.q, vneg(normal));
     *iB = -1; *iA = support(pA, axisA);
-    V2 pointA = xmul(xfA, pA->v[*iA]);
+    V2 pointA = xmul(xfA, pv(pA, *iA));
     return vdot(vsub(pointA, pointB), normal);
   }
 }
 __device__ inline float sep_eval(const SepFn& f, const Poly* pA, const Poly* pB, int iA, int iB, float t) {
   Xf xfA = sweep_xf(f.sA, t), xfB = sweep_xf(f.sB, t);
   if (f.type == SF_POINTS) {
-    V2 pointA = xmul(xfA, pA->v[iA]), pointB = xmul(xfB, pB->v[iB]);
+    V2 pointA = xmul(xfA, pv(pA, iA)), pointB = xmul(xfB, pv(pB, iB));
     return vdot(vsub(pointB, pointA), f.axis);
   } else if (f.type == SF_FACEA) {
-    V2 normal = rmul(xfA.q, f.axis), pointA = xmul(xfA, f.lp), pointB = xmul(xfB, pB->v[iB]);
+    V2 normal = rmul(xfA.q, f.axis), pointA = xmul(xfA, f.lp), pointB = xmul(xfB, pv(pB, iB));
     return vdot(vsub(pointB, pointA), normal);
   } else {
-    V2 normal = rmul(xfB.q, f.axis), pointB = xmul(xfB, f.lp), pointA = xmul(xfA, pA->v[iA]);
+    V2 normal = rmul(xfB.q, f.axis), pointB = xmul(xfB, f.lp), pointA = xmul(xfA, pv(pA, iA));
     return vdot(vsub(pointA, pointB), normal);
   }
 }

@@ -129,6 +129,82 @@ __device__ inline void car_store(const Params& P, int n, const Car& c) {
   I32P(P, first_step)[n] = c.first_step; I32P(P, prev_laps)[n] = c.prev_laps;
 }
 
+// Staged load/store for step_kernel: only the body, vehicle-model and listener fields are
+// live through update_physics + the Box2D step; the model fields are written back right
+// after update_physics (a compiler memory barrier stops the reload being forwarded) and the
+// lap-timer / bookkeeping fields are loaded after the Box2D step.  Register pressure, not
+// traffic, is what this buys (the re-read hits L2).
+__device__ inline void car_load_phys(const Params& P, int n, Car& c) {
+  c.c = V(F32P(P, cx)[n], F32P(P, cy)[n]); c.a = F32P(P, a)[n];
+  c.v = V(F32P(P, vx)[n], F32P(P, vy)[n]); c.w = F32P(P, w)[n];
+  c.xf.q.s = F32P(P, qs)[n]; c.xf.q.c = F32P(P, qc)[n]; c.xf.p = V(F32P(P, xpx)[n], F32P(P, xpy)[n]);
+  c.sleep = F32P(P, sleep)[n]; c.invdt0 = F32P(P, invdt0)[n];
+  c.fat.lo = V(F32P(P, flox)[n], F32P(P, floy)[n]); c.fat.hi = V(F32P(P, fhix)[n], F32P(P, fhiy)[n]);
+  c.rpm = F64P(P, rpm)[n]; c.pvx = F64P(P, pvx)[n]; c.pvy = F64P(P, pvy)[n];
+  c.lfm = F64P(P, lfm)[n]; c.slip = F64P(P, slip)[n]; c.bank = F64P(P, bank)[n];
+  c.load[0] = F64P(P, load0)[n]; c.load[1] = F64P(P, load1)[n]; c.load[2] = F64P(P, load2)[n]; c.load[3] = F64P(P, load3)[n];
+  c.temp[0] = F64P(P, temp0)[n]; c.temp[1] = F64P(P, temp1)[n]; c.temp[2] = F64P(P, temp2)[n]; c.temp[3] = F64P(P, temp3)[n];
+  c.wear[0] = F64P(P, wear0)[n]; c.wear[1] = F64P(P, wear1)[n]; c.wear[2] = F64P(P, wear2)[n]; c.wear[3] = F64P(P, wear3)[n];
+  c.imp = F64P(P, imp)[n];
+  c.awake = I32P(P, awake)[n]; c.nct = I32P(P, nct)[n]; c.overflow = I32P(P, overflow)[n];
+  c.acc_len = I32P(P, acc_len)[n]; c.acc_head = I32P(P, acc_head)[n];
+  c.imp_present = I32P(P, imp_present)[n]; c.nact = I32P(P, nact)[n];
+  c.disabled = I32P(P, disabled)[n];
+  c.just_disabled = 0;
+  c.force = zero2(); c.torque = 0.0f; c.c0 = c.c; c.a0 = c.a; c.alpha0 = 0.0f; c.moved = 0;
+  c.ct = P.ct + (size_t)n * MAXC; c.act_key = P.act_key + (size_t)n * MAXC; c.act_n = P.act_n + (size_t)n * MAXC * 2;
+  c.acc = nullptr;
+}
+__device__ inline void car_store_model(const Params& P, int n, const Car& c) {
+  F64P(P, rpm)[n] = c.rpm; F64P(P, pvx)[n] = c.pvx; F64P(P, pvy)[n] = c.pvy;
+  F64P(P, lfm)[n] = c.lfm; F64P(P, slip)[n] = c.slip;
+  F64P(P, load0)[n] = c.load[0]; F64P(P, load1)[n] = c.load[1]; F64P(P, load2)[n] = c.load[2]; F64P(P, load3)[n] = c.load[3];
+  F64P(P, temp0)[n] = c.temp[0]; F64P(P, temp1)[n] = c.temp[1]; F64P(P, temp2)[n] = c.temp[2]; F64P(P, temp3)[n] = c.temp[3];
+  F64P(P, wear0)[n] = c.wear[0]; F64P(P, wear1)[n] = c.wear[1]; F64P(P, wear2)[n] = c.wear[2]; F64P(P, wear3)[n] = c.wear[3];
+  I32P(P, acc_len)[n] = c.acc_len; I32P(P, acc_head)[n] = c.acc_head;
+}
+__device__ inline void car_reload_tyres(const Params& P, int n, Car& c) {
+  c.load[0] = F64P(P, load0)[n]; c.load[1] = F64P(P, load1)[n]; c.load[2] = F64P(P, load2)[n]; c.load[3] = F64P(P, load3)[n];
+  c.temp[0] = F64P(P, temp0)[n]; c.temp[1] = F64P(P, temp1)[n]; c.temp[2] = F64P(P, temp2)[n]; c.temp[3] = F64P(P, temp3)[n];
+  c.wear[0] = F64P(P, wear0)[n]; c.wear[1] = F64P(P, wear1)[n]; c.wear[2] = F64P(P, wear2)[n]; c.wear[3] = F64P(P, wear3)[n];
+}
+__device__ inline void car_load_logic(const Params& P, int n, Car& c) {
+  c.cum_reward = F32P(P, cum_reward)[n]; c.cum_reward_info = F32P(P, cum_reward_info)[n];
+  c.lt_start = F64P(P, lt_start)[n]; c.lt_cur = F64P(P, lt_cur)[n]; c.lt_last = F64P(P, lt_last)[n];
+  c.lt_best = F64P(P, lt_best)[n]; c.lt_px = F64P(P, lt_px)[n]; c.lt_py = F64P(P, lt_py)[n]; c.lt_dist = F64P(P, lt_dist)[n];
+  c.cum_impact = F64P(P, cum_impact)[n]; c.stuck_dur = F64P(P, stuck_dur)[n];
+  c.stuck_sx = F64P(P, stuck_sx)[n]; c.stuck_sy = F64P(P, stuck_sy)[n];
+  c.prev_px = F64P(P, prev_px)[n]; c.prev_py = F64P(P, prev_py)[n];
+  c.prog_hist = F64P(P, prog_hist)[n]; c.back = F64P(P, back)[n]; c.prev_back = F64P(P, prev_back)[n];
+  c.imp_at_obs = F64P(P, imp_at_obs)[n];
+  c.lt_timing = I32P(P, lt_timing)[n]; c.lt_has_last = I32P(P, lt_has_last)[n]; c.lt_has_best = I32P(P, lt_has_best)[n];
+  c.lt_crossed = I32P(P, lt_crossed)[n]; c.lt_has_pos = I32P(P, lt_has_pos)[n]; c.lt_laps = I32P(P, lt_laps)[n];
+  c.has_stuck_start = I32P(P, has_stuck_start)[n];
+  c.first_step = I32P(P, first_step)[n]; c.prev_laps = I32P(P, prev_laps)[n];
+}
+__device__ inline void car_store_late(const Params& P, int n, const Car& c) {   // everything but car_store_model's
+  F32P(P, cx)[n] = c.c.x; F32P(P, cy)[n] = c.c.y; F32P(P, a)[n] = c.a;
+  F32P(P, vx)[n] = c.v.x; F32P(P, vy)[n] = c.v.y; F32P(P, w)[n] = c.w;
+  F32P(P, qs)[n] = c.xf.q.s; F32P(P, qc)[n] = c.xf.q.c; F32P(P, xpx)[n] = c.xf.p.x; F32P(P, xpy)[n] = c.xf.p.y;
+  F32P(P, sleep)[n] = c.sleep; F32P(P, invdt0)[n] = c.invdt0;
+  F32P(P, flox)[n] = c.fat.lo.x; F32P(P, floy)[n] = c.fat.lo.y; F32P(P, fhix)[n] = c.fat.hi.x; F32P(P, fhiy)[n] = c.fat.hi.y;
+  F32P(P, cum_reward)[n] = c.cum_reward; F32P(P, cum_reward_info)[n] = c.cum_reward_info;
+  F64P(P, bank)[n] = c.bank; F64P(P, imp)[n] = c.imp;
+  F64P(P, lt_start)[n] = c.lt_start; F64P(P, lt_cur)[n] = c.lt_cur; F64P(P, lt_last)[n] = c.lt_last;
+  F64P(P, lt_best)[n] = c.lt_best; F64P(P, lt_px)[n] = c.lt_px; F64P(P, lt_py)[n] = c.lt_py; F64P(P, lt_dist)[n] = c.lt_dist;
+  F64P(P, cum_impact)[n] = c.cum_impact; F64P(P, stuck_dur)[n] = c.stuck_dur;
+  F64P(P, stuck_sx)[n] = c.stuck_sx; F64P(P, stuck_sy)[n] = c.stuck_sy;
+  F64P(P, prev_px)[n] = c.prev_px; F64P(P, prev_py)[n] = c.prev_py;
+  F64P(P, prog_hist)[n] = c.prog_hist; F64P(P, back)[n] = c.back; F64P(P, prev_back)[n] = c.prev_back;
+  F64P(P, imp_at_obs)[n] = c.imp_at_obs;
+  I32P(P, awake)[n] = c.awake; I32P(P, nct)[n] = c.nct; I32P(P, overflow)[n] = c.overflow;
+  I32P(P, imp_present)[n] = c.imp_present; I32P(P, nact)[n] = c.nact;
+  I32P(P, lt_timing)[n] = c.lt_timing; I32P(P, lt_has_last)[n] = c.lt_has_last; I32P(P, lt_has_best)[n] = c.lt_has_best;
+  I32P(P, lt_crossed)[n] = c.lt_crossed; I32P(P, lt_has_pos)[n] = c.lt_has_pos; I32P(P, lt_laps)[n] = c.lt_laps;
+  I32P(P, disabled)[n] = c.disabled; I32P(P, has_stuck_start)[n] = c.has_stuck_start;
+  I32P(P, first_step)[n] = c.first_step; I32P(P, prev_laps)[n] = c.prev_laps;
+}
+
 // ------------------------------------------------------------------ tyres (src/tyre.py, src/tyre_manager.py)
 __device__ inline double tyre_grip(double T, double wear) {
   double tg;
@@ -547,10 +623,10 @@ __device__ inline bool query_on_wall(const WallSet& S, double px, double py, dou
     Poly p; make_box(&p, wl.hx, wl.hy);
     V2 pl = rmulT(xf.q, vsub(center, xf.p));
     bool inside = true;
-    for (int i = 0; i < 4; ++i) { if (vdot(p.n[i], vsub(pl, p.v[i])) > 0.0f) { inside = false; break; } }
+    for (int i = 0; i < 4; ++i) { if (vdot(pn(&p, i), vsub(pl, pv(&p, i))) > 0.0f) { inside = false; break; } }
     if (inside) return true;
     for (int i = 0; i < 4; ++i) {
-      V2 v = xmul(xf, p.v[i]);
+      V2 v = xmul(xf, pv(&p, i));
       double dx = px - (double)v.x, dy = py - (double)v.y;
       if (PH(dx * dx + dy * dy) < radius) return true;
     }
@@ -897,10 +973,10 @@ __global__ void __launch_bounds__(SBLOCK) step_kernel(Params P, const void* acti
   bool lapdone = false;
   double sim = 0.0;
   if (env >= 0) {
-    car_load(P, n, c);
+    car_load_phys(P, n, c);
     sim = P.env_time[env];
     PROF(2);
-    s_laps_old[tid] = c.lt_laps; s_dis_old[tid] = c.disabled;
+    s_dis_old[tid] = c.disabled;
     // actions (BaseEnv._convert_to_internal_action / _discrete_to_continuous, np.float32)
     float tb, st;
     if (discrete) {
@@ -917,9 +993,13 @@ __global__ void __launch_bounds__(SBLOCK) step_kernel(Params P, const void* acti
     c.brk_in = pymax(0.0, pymin(1.0, (double)a1));
     c.str_in = pymax(-1.0, pymin(1.0, (double)a2));
     car_update_physics(P, c, n, T);
+    car_store_model(P, n, c);
+    asm volatile("" ::: "memory");   // the tyre state is re-read from memory for the observation
     PROF(3);
     b2_step(c, S, P.dt_f, P.friction);
     PROF(4);
+    car_load_logic(P, n, c);
+    s_laps_old[tid] = c.lt_laps;   // the lap count does not change before lap_update
     c.bank = T.has_banking ? banking_at(T, c.xf.p.x, c.xf.p.y) : 0.0;
     if (!c.disabled) {   // _run_single_physics_step (src/car_env.py:582-638)
       double imp = c.imp_present ? c.imp : 0.0;
@@ -976,6 +1056,7 @@ __global__ void __launch_bounds__(SBLOCK) step_kernel(Params P, const void* acti
       } else { c.stuck_dur = 0.0; c.has_stuck_start = 0; }
     }
     PROF(6);
+    car_reload_tyres(P, n, c);
     car_obs(c, o);
     PROF(7);
     // _calculate_multi_rewards (src/car_env.py:980-1113)
@@ -1058,7 +1139,8 @@ __global__ void __launch_bounds__(SBLOCK) step_kernel(Params P, const void* acti
       P.pose[n] = car_pose(c, terminal_obs ? (PM_A_OBS | PM_A_TERM) : PM_A_OBS);
     }
     for (int i = 0; i < 22; ++i) s_obs[tid * 22 + i] = o[i];
-    car_store(P, n, c);
+    if (reset_now) car_store(P, n, c);    // car_reset rewrote every field
+    else car_store_late(P, n, c);
     PROF(10);
     if (reset_now && car == 0) {
       P.env_time[env] = 0.0;
