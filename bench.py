@@ -68,7 +68,9 @@ def main():
     ap.add_argument("--envs", type=int, default=8192)
     ap.add_argument("--cars", type=int, default=10)
     ap.add_argument("--track", default="daytona")
-    ap.add_argument("--policy", default="uniform", choices=["uniform", "driver"])
+    ap.add_argument("--policy", default="uniform", choices=["uniform", "driver", "sac"],
+                    help="uniform: U[-1,1]^2 resident in HBM; driver: device rule driver; sac: fused SAC actor "
+                         "(random-init weights of the reference architecture) on the previous observation")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     args = ap.parse_args()
@@ -88,6 +90,9 @@ def main():
     E, C, K, W = args.envs, args.cars, args.steps, args.warmup
     tpath = track_path(args.track)
     env = BatchedCarEnv(E, C, tpath, device=dev)
+    if args.policy == "sac":
+        from nascargymnasium_amd.policy import random_actor
+        env.set_actor(random_actor(rank))
     env.reset()
     gen = torch.Generator(device=dev)
     gen.manual_seed(1234 + rank)
@@ -95,8 +100,10 @@ def main():
         acts = torch.rand((W + K, E, C, 2), generator=gen, device=dev) * 2 - 1     # resident before timing
     torch.cuda.synchronize()
 
+    pol = {"driver": 1, "sac": 2}.get(args.policy)
+
     def one_step(i):
-        a = acts[i] if args.policy == "uniform" else env.policy_actions(1, seed=rank, step=i)
+        a = acts[i] if args.policy == "uniform" else env.policy_actions(pol, seed=rank, step=i)
         env.step(a, auto_reset=True)
 
     for i in range(W):
@@ -113,7 +120,7 @@ def main():
             env.launch_step(acts[W + i], auto_reset=True)
             ev[i][1].record()
         else:
-            a = env.policy_actions(1, seed=rank, step=W + i)
+            a = env.policy_actions(pol, seed=rank, step=W + i)
             ev[i][0].record()
             env.launch_step(a, auto_reset=True)
             ev[i][1].record()
@@ -141,7 +148,7 @@ def main():
         "ms_per_step": elapsed / K * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
         "dtype": "f32+f64", "data": "synthetic",
         "config": {"workload": f"{os.path.basename(tpath)[:-6]} {C}-car: {E} envs x {C} cars per GPU, "
-                               f"{'uniform U[-1,1]^2 actions resident in HBM' if args.policy == 'uniform' else 'on-device rule driver'}, auto-reset",
+                               f"{ {'uniform': 'uniform U[-1,1]^2 actions resident in HBM', 'driver': 'on-device rule driver', 'sac': 'fused SAC actor (random-init) closed loop'}[args.policy]}, auto-reset",
                    "envs_per_gpu": E, "cars_per_env": C, "track": os.path.basename(tpath), "parallelism": f"dp{world} (env shards, no collective)"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,

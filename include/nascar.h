@@ -76,11 +76,22 @@ int64_t nascar_state_bytes(NascarHandle* h);
 int nascar_get_state(NascarHandle* h, void* dst_device, void* stream);
 int nascar_set_state(NascarHandle* h, const void* src_device, void* stream);
 
-/* Synthetic action sources for benchmarks, generated on the device:
+/* Device action sources:
  *   policy 0: counter-based uniform U[-1,1]^2 (key = seed, car, step)
- *   policy 1: BaseController._fallback_control (game/control/base_controller.py:39-103) from obs */
+ *   policy 1: BaseController._fallback_control (game/control/base_controller.py:39-103) from obs
+ *   policy 2: the SAC actor loaded with nascar_set_actor, deterministic (SACController.control,
+ *             game/control/sac_control_class.py:80-115) from obs */
 int nascar_policy_actions(NascarHandle* h, int32_t policy, uint64_t seed, int64_t step, const float* obs,
                           float* actions, void* stream);
+
+/* SB3 SAC MlpPolicy actor weights (PyTorch layouts, host float32): w1 [256][38], b1 [256],
+ * w2 [256][256], b2 [256], w3 = mu.weight [2][256], b3 = mu.bias [2]  (obs_dim 38, hidden 256,
+ * act_dim 2; other shapes are rejected).  Replaces SAC.load + policy.predict
+ * (game/control/sac_control_class.py:48-115) with one fused bf16-MFMA kernel. */
+int nascar_set_actor(NascarHandle* h, const float* w1, const float* b1, const float* w2, const float* b2,
+                     const float* w3, const float* b3, int32_t obs_dim, int32_t hidden, int32_t act_dim);
+/* The loaded actor on any device batch: obs [n][38] float32 -> actions [n][2] float32 (both 8-byte aligned). */
+int nascar_actor_forward(NascarHandle* h, const float* obs, int32_t n, float* actions, void* stream);
 
 /* Test hook: the device re-implementation of glibc sinf/cosf used for b2Rot::Set
  * (device pointers, n floats).  Parity tests compare it with the host libm. */

@@ -83,6 +83,11 @@ def lib():
     L.nascar_set_state.restype = ctypes.c_int
     L.nascar_policy_actions.argtypes = [vp, i32, u64, i64, vp, vp, vp]
     L.nascar_policy_actions.restype = ctypes.c_int
+    fp = ctypes.POINTER(ctypes.c_float)
+    L.nascar_set_actor.argtypes = [vp, fp, fp, fp, fp, fp, fp, i32, i32, i32]
+    L.nascar_set_actor.restype = ctypes.c_int
+    L.nascar_actor_forward.argtypes = [vp, vp, i32, vp, vp]
+    L.nascar_actor_forward.restype = ctypes.c_int
     L.nascar_debug_sincosf.argtypes = [vp, vp, vp, i32, vp]
     L.nascar_debug_sincosf.restype = ctypes.c_int
     _lib = L
@@ -91,7 +96,8 @@ def lib():
 
 EXPORTED = ["nascar_create", "nascar_destroy", "nascar_last_error", "nascar_add_track", "nascar_set_env_tracks",
             "nascar_reset", "nascar_step", "nascar_get_info", "nascar_state_bytes", "nascar_get_state",
-            "nascar_set_state", "nascar_policy_actions", "nascar_debug_sincosf"]
+            "nascar_set_state", "nascar_policy_actions", "nascar_set_actor", "nascar_actor_forward",
+            "nascar_debug_sincosf"]
 
 
 def check(rc):

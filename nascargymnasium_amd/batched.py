@@ -132,8 +132,25 @@ class BatchedCarEnv:
     def termination_reason(self) -> torch.Tensor:
         return (self.env_flags >> 4) & 7
 
+    def set_actor(self, weights):
+        """Load an SB3 SAC MlpPolicy actor: a dict from nascargymnasium_amd.policy.load_sb3_actor / random_actor."""
+        from .policy import actor_arrays
+        arrs = actor_arrays(weights)
+        fp = ctypes.POINTER(ctypes.c_float)
+        _lib.check(self.L.nascar_set_actor(self.h, *[a.ctypes.data_as(fp) for a in arrs], 38, 256, 2))
+        self._actor_arrays = arrs
+
+    def actor_forward(self, obs: torch.Tensor) -> torch.Tensor:
+        """The loaded actor on a device batch of observations [..., 38] -> actions [..., 2]."""
+        o = obs.to(self.device, torch.float32).contiguous()
+        n = o.numel() // 38
+        out = torch.empty(o.shape[:-1] + (2,), dtype=torch.float32, device=self.device)
+        with torch.cuda.device(self.device):
+            _lib.check(self.L.nascar_actor_forward(self.h, _ptr(o), n, _ptr(out), _stream()))
+        return out
+
     def policy_actions(self, policy: int, seed: int = 0, step: int = 0, obs: Optional[torch.Tensor] = None):
-        """device-generated synthetic actions: 0 uniform U[-1,1]^2, 1 BaseController fallback driver."""
+        """device-generated actions: 0 uniform U[-1,1]^2, 1 BaseController fallback driver, 2 the SAC actor."""
         o = self.obs if obs is None else obs
         with torch.cuda.device(self.device):
             _lib.check(self.L.nascar_policy_actions(self.h, int(policy), int(seed), int(step), _ptr(o),

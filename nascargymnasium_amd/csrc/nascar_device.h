@@ -38,6 +38,12 @@ __device__ unsigned long long* g_prof = nullptr;
 #endif
 #define PROF_RT(slot) do { unsigned long long _t = __builtin_amdgcn_s_memrealtime(); \
     if (g_prof && (threadIdx.x & 63) == 0) g_prof[((size_t)blockIdx.x * (BLOCK / 64) + threadIdx.x / 64) * 16 + (slot)] = _t; } while (0)
+// actor_kernel stamps: region after the counters, 16 slots per wave (64-thread waves, any block size)
+#define APROF_BASE (2 * 65536 * 16 + 64)
+#define APROF(ph) do { unsigned long long _t = __builtin_amdgcn_s_memtime(); \
+    if (g_prof && (threadIdx.x & 63) == 0) g_prof[APROF_BASE + ((size_t)blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64) * 16 + (ph)] = _t; } while (0)
+#define APROF_RT(ph) do { unsigned long long _t = __builtin_amdgcn_s_memrealtime(); \
+    if (g_prof && (threadIdx.x & 63) == 0) g_prof[APROF_BASE + ((size_t)blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64) * 16 + (ph)] = _t; } while (0)
 #else
 #define PROF(ph) do { } while (0)
 #define PROFS(ph) do { } while (0)
@@ -45,6 +51,8 @@ __device__ unsigned long long* g_prof = nullptr;
 #define PROFU(ph) do { } while (0)
 #define PCOUNT(slot, v) do { } while (0)
 #define PROF_RT(slot) do { } while (0)
+#define APROF(ph) do { } while (0)
+#define APROF_RT(ph) do { } while (0)
 #endif
 
 namespace nascar {

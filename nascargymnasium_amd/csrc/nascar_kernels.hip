@@ -22,6 +22,7 @@
 
 #include "../../include/nascar.h"
 #include "nascar_device.h"
+#include "nascar_actor.h"
 
 #pragma clang fp contract(off)
 
@@ -1259,6 +1260,15 @@ static int fail(const char* fmt, ...) {
 }
 #define HIPCHK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) return fail("%s failed: %s", #x, hipGetErrorString(e_)); } while (0)
 
+// persistent actor grid: one workgroup per CU (W2 fills the LDS), never more than the tiles
+static int actor_grid(int n) {
+  static int cus = 0;
+  if (!cus) { int dev = 0; hipGetDevice(&dev); hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev); if (cus <= 0) cus = 256; }
+  const int tiles = (n + 32 * ACT_WAVES - 1) / (32 * ACT_WAVES);   // >= one tile per wave
+  return std::max(1, std::min(tiles, cus));
+}
+
+
 struct HostGrid {
   WallGrid g{};
   std::vector<int> start; std::vector<uint16_t> idx;
@@ -1380,6 +1390,8 @@ struct NascarHandle {
   std::vector<int> env_track;
   double* d_ctl = nullptr;   // rule-driver state for nascar_policy_actions
   float4* d_pose = nullptr;  // [2][N] step/reset -> sensor_kernel hand-off
+  void* d_actor = nullptr;   // SAC actor weights (nascar_set_actor), one allocation
+  ActorDev actor{};
   size_t max_lds = 0, max_sensor_lds = 0;
   bool dirty_tracks = true;
 };
@@ -1422,7 +1434,7 @@ extern "C" int nascar_create(const NascarConfig* cfg, NascarHandle** out) {
 
 extern "C" void nascar_destroy(NascarHandle* h) {
   if (!h) return;
-  hipFree(h->arena); hipFree(h->d_ctl); hipFree(h->d_pose);
+  hipFree(h->arena); hipFree(h->d_ctl); hipFree(h->d_pose); hipFree(h->d_actor);
   for (auto& t : h->tracks) {
     hipFree(t.d_walls); hipFree(t.d_segs); hipFree(t.d_prefix);
     hipFree(t.bp.d_start); hipFree(t.bp.d_idx); hipFree(t.sn.d_start); hipFree(t.sn.d_idx); hipFree(t.d_groups);
@@ -1619,7 +1631,14 @@ extern "C" int nascar_set_state(NascarHandle* h, const void* src, void* stream) 
 extern "C" int nascar_policy_actions(NascarHandle* h, int32_t policy, uint64_t seed, int64_t step, const float* obs,
                                      float* actions, void* stream) {
   if (!h || !actions) return fail("null argument");
-  if (policy == 1 && !obs) return fail("policy 1 needs obs");
+  if (policy >= 1 && !obs) return fail("policy %d needs obs", policy);
+  if (policy == 2) {
+    if (!h->d_actor) return fail("policy 2 needs an actor (nascar_set_actor)");
+    if (((uintptr_t)obs | (uintptr_t)actions) & 7) return fail("actor obs/actions must be 8-byte aligned");
+    hipLaunchKernelGGL(actor_kernel, dim3(actor_grid(h->N)), dim3(64 * ACT_WAVES), 0, (hipStream_t)stream, h->N, obs, actions, h->actor);
+    HIPCHK(hipGetLastError());
+    return 0;
+  }
   int nb = (h->N + 255) / 256;
   hipLaunchKernelGGL(policy_kernel, dim3(nb), dim3(256), 0, (hipStream_t)stream, h->N, policy, seed, step, obs, actions, h->d_ctl);
   HIPCHK(hipGetLastError());
@@ -1631,6 +1650,80 @@ __global__ void sincos_kernel(const float* x, float* s, float* c, int n) {
   int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) { s[i] = dev_sinf(x[i]); c[i] = dev_cosf(x[i]); }
 }
+static uint16_t f32_to_bf16_rne(float f) {
+  uint32_t u; memcpy(&u, &f, 4);
+  if ((u & 0x7F800000u) == 0x7F800000u && (u & 0x007FFFFFu)) return (uint16_t)((u >> 16) | 0x40);   // quiet NaN
+  u += 0x7FFFu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+
+// SB3 SAC MlpPolicy actor (game/control/sac_control_class.py:80-115), PyTorch layouts:
+// w1 [256][38], b1 [256], w2 [256][256], b2 [256], w3 (mu) [2][256], b3 [2]; host float32.
+extern "C" int nascar_set_actor(NascarHandle* h, const float* w1, const float* b1, const float* w2, const float* b2,
+                                const float* w3, const float* b3, int32_t obs_dim, int32_t hidden, int32_t act_dim) {
+  if (!h || !w1 || !b1 || !w2 || !b2 || !w3 || !b3) return fail("null argument");
+  if (obs_dim != ACT_OBS || hidden != ACT_H || act_dim != ACT_OUT)
+    return fail("actor shape %dx%dx%d unsupported (need 38x256x2: SB3 MlpPolicy net_arch [256, 256])", obs_dim, hidden, act_dim);
+  std::vector<uint16_t> w1p((size_t)ACT_H * ACT_K, 0), w2p((size_t)ACT_H * ACT_H);
+  for (int o = 0; o < ACT_H; ++o) {
+    for (int i = 0; i < ACT_OBS; ++i) w1p[(size_t)o * ACT_K + i] = f32_to_bf16_rne(w1[(size_t)o * ACT_OBS + i]);
+    // b1 rides in the two extra K columns (the observation tile holds 1.0 there): hi + lo bf16 halves
+    const uint16_t hi = f32_to_bf16_rne(b1[o]);
+    const uint32_t hb = (uint32_t)hi << 16;
+    float hf; memcpy(&hf, &hb, 4);
+    w1p[(size_t)o * ACT_K + ACT_OBS] = hi;
+    w1p[(size_t)o * ACT_K + ACT_OBS + 1] = f32_to_bf16_rne(b1[o] - hf);
+  }
+  // layer-2 A fragments in the k order of the layer-1 accumulator registers (nascar_actor.h)
+  for (int o = 0; o < 8; ++o)
+    for (int q = 0; q < 8; ++q)
+      for (int s = 0; s < 2; ++s)
+        for (int r = 0; r < 32; ++r)
+          for (int hh = 0; hh < 2; ++hh)
+            for (int j = 0; j < 8; ++j) {
+              const int row = 32 * o + r, col = 32 * q + 16 * s + 8 * (j >> 2) + 4 * hh + (j & 3);
+              w2p[((((size_t)(o * 8 + q) * 2 + s) * 2 + hh) * 32 + r) * 8 + j] = f32_to_bf16_rne(w2[(size_t)row * ACT_H + col]);
+            }
+  // layer-3 A fragments: W3' rows 0-3 = hi(w3[0]), hi(w3[1]), lo(w3[0]), lo(w3[1]) in the k order of the
+  // layer-2 accumulator registers (rows 4-31 are zero and not stored)
+  std::vector<uint16_t> w3p((size_t)8 * 2 * 2 * 4 * 8);
+  for (int o = 0; o < 8; ++o)
+    for (int s = 0; s < 2; ++s)
+      for (int hh = 0; hh < 2; ++hh)
+        for (int r = 0; r < 4; ++r)
+          for (int j = 0; j < 8; ++j) {
+            const int col = 32 * o + 16 * s + 8 * (j >> 2) + 4 * hh + (j & 3);
+            const float w = w3[(size_t)(r & 1) * ACT_H + col];
+            const uint16_t hi = f32_to_bf16_rne(w);
+            const uint32_t hb = (uint32_t)hi << 16;
+            float hf; memcpy(&hf, &hb, 4);
+            w3p[((((size_t)o * 2 + s) * 2 + hh) * 4 + r) * 8 + j] = r < 2 ? hi : f32_to_bf16_rne(w - hf);
+          }
+  const size_t o_w1 = 0, o_w2 = o_w1 + w1p.size() * 2, o_b2 = o_w2 + w2p.size() * 2,
+               o_w3 = o_b2 + ACT_H * 4, o_b3 = o_w3 + w3p.size() * 2, total = o_b3 + 64;
+  if (!h->d_actor) HIPCHK(hipMalloc(&h->d_actor, total));
+  char* d = (char*)h->d_actor;
+  HIPCHK(hipMemcpy(d + o_w1, w1p.data(), w1p.size() * 2, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(d + o_w2, w2p.data(), w2p.size() * 2, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(d + o_b2, b2, ACT_H * 4, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(d + o_w3, w3p.data(), w3p.size() * 2, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(d + o_b3, b3, ACT_OUT * 4, hipMemcpyHostToDevice));
+  h->actor.w1p = (const bf16x8*)(d + o_w1); h->actor.w2p = (const bf16x8*)(d + o_w2);
+  h->actor.b2 = (const float*)(d + o_b2); h->actor.w3p = (const bf16x8*)(d + o_w3); h->actor.b3 = (const float*)(d + o_b3);
+  return 0;
+}
+
+// Actor forward on an arbitrary device batch: obs [n][38] float32 -> actions [n][2] float32.
+extern "C" int nascar_actor_forward(NascarHandle* h, const float* obs, int32_t n, float* actions, void* stream) {
+  if (!h || !obs || !actions || n < 0) return fail("bad argument");
+  if (!h->d_actor) return fail("no actor loaded (nascar_set_actor)");
+  if (((uintptr_t)obs | (uintptr_t)actions) & 7) return fail("actor obs/actions must be 8-byte aligned");
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(actor_kernel, dim3(actor_grid(n)), dim3(64 * ACT_WAVES), 0, (hipStream_t)stream, n, obs, actions, h->actor);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
 extern "C" int nascar_debug_sincosf(const float* x, float* s, float* c, int32_t n, void* stream) {
   if (!x || !s || !c || n < 0) return fail("bad argument");
   hipLaunchKernelGGL(sincos_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, x, s, c, n);

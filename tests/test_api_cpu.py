@@ -70,3 +70,29 @@ def test_carenv_needs_device():
 def test_format_time():
     assert _format_time(None) == "--:--.---" and _format_time(-1.0) == "--:--.---"
     assert _format_time(83.4567) == " 1:23.457"
+
+
+def test_sb3_actor_loader(tmp_path):
+    """policy.load_sb3_actor reads an SB3 zip with zipfile + torch.load(weights_only=True)."""
+    import io
+    import zipfile
+    import torch
+    from nascargymnasium_amd.policy import ACTOR_KEYS, load_sb3_actor, random_actor
+    w = random_actor(3)
+    sd = {k: torch.from_numpy(v) for k, v in w.items()}
+    sd["critic.qf0.0.weight"] = torch.zeros(4, 4)
+    buf = io.BytesIO()
+    torch.save(sd, buf)
+    p = tmp_path / "sac.zip"
+    with zipfile.ZipFile(p, "w") as z:
+        z.writestr("policy.pth", buf.getvalue())
+        z.writestr("data", "{}")
+    got = load_sb3_actor(str(p))
+    assert set(got) == set(ACTOR_KEYS)
+    for k in ACTOR_KEYS:
+        assert np.array_equal(got[k], w[k])
+    bad = tmp_path / "bad.zip"
+    with zipfile.ZipFile(bad, "w") as z:
+        buf2 = io.BytesIO(); torch.save({"x": torch.zeros(1)}, buf2); z.writestr("policy.pth", buf2.getvalue())
+    with pytest.raises(ValueError):
+        load_sb3_actor(str(bad))
