@@ -152,7 +152,7 @@ def main():
                    "envs_per_gpu": E, "cars_per_env": C, "track": os.path.basename(tpath), "parallelism": f"dp{world} (env shards, no collective)"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": "step_kernel + sensor_kernel (one env step)", "kernel_ms": kern_ms,
+                     "kernel": "model_kernel + logic_kernel + sensor_kernel (one env step)", "kernel_ms": kern_ms,
                      "algo_bytes_per_car_step": ALGO_BYTES_PER_CAR_STEP},
         "engine_errors": errs,
     }

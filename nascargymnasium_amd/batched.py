@@ -112,7 +112,7 @@ class BatchedCarEnv:
         return self.obs, self.reward, terminated, truncated
 
     def launch_step(self, actions: torch.Tensor, auto_reset: bool = False, terminal_obs: bool = False):
-        """Enqueue exactly one step_kernel launch on the current stream (no other device work when
+        """Enqueue exactly one env step (model, logic and sensor kernels) on the current stream (no other device work when
         `actions` is already a contiguous float32/int32 tensor on this device)."""
         discrete = not actions.is_floating_point()
         a = actions.to(self.device, torch.int32 if discrete else torch.float32).contiguous()

@@ -130,7 +130,7 @@ __device__ inline void car_store(const Params& P, int n, const Car& c) {
   I32P(P, first_step)[n] = c.first_step; I32P(P, prev_laps)[n] = c.prev_laps;
 }
 
-// Staged load/store for step_kernel: only the body, vehicle-model and listener fields are
+// Staged load/store for model_kernel: only the body, vehicle-model and listener fields are
 // live through update_physics + the Box2D step; the model fields are written back right
 // after update_physics (a compiler memory barrier stops the reload being forwarded) and the
 // lap-timer / bookkeeping fields are loaded after the Box2D step.  Register pressure, not
@@ -183,12 +183,36 @@ __device__ inline void car_load_logic(const Params& P, int n, Car& c) {
   c.has_stuck_start = I32P(P, has_stuck_start)[n];
   c.first_step = I32P(P, first_step)[n]; c.prev_laps = I32P(P, prev_laps)[n];
 }
-__device__ inline void car_store_late(const Params& P, int n, const Car& c) {   // everything but car_store_model's
+
+// model_kernel -> logic_kernel hand-off: the body / listener fields the Box2D step produced
+__device__ inline void car_store_body(const Params& P, int n, const Car& c) {
   F32P(P, cx)[n] = c.c.x; F32P(P, cy)[n] = c.c.y; F32P(P, a)[n] = c.a;
   F32P(P, vx)[n] = c.v.x; F32P(P, vy)[n] = c.v.y; F32P(P, w)[n] = c.w;
   F32P(P, qs)[n] = c.xf.q.s; F32P(P, qc)[n] = c.xf.q.c; F32P(P, xpx)[n] = c.xf.p.x; F32P(P, xpy)[n] = c.xf.p.y;
   F32P(P, sleep)[n] = c.sleep; F32P(P, invdt0)[n] = c.invdt0;
   F32P(P, flox)[n] = c.fat.lo.x; F32P(P, floy)[n] = c.fat.lo.y; F32P(P, fhix)[n] = c.fat.hi.x; F32P(P, fhiy)[n] = c.fat.hi.y;
+  F64P(P, imp)[n] = c.imp;
+  I32P(P, awake)[n] = c.awake; I32P(P, nct)[n] = c.nct; I32P(P, overflow)[n] = c.overflow;
+  I32P(P, imp_present)[n] = c.imp_present; I32P(P, nact)[n] = c.nact;
+}
+__device__ inline void car_load_body(const Params& P, int n, Car& c) {
+  c.c = V(F32P(P, cx)[n], F32P(P, cy)[n]); c.a = F32P(P, a)[n];
+  c.v = V(F32P(P, vx)[n], F32P(P, vy)[n]); c.w = F32P(P, w)[n];
+  c.xf.q.s = F32P(P, qs)[n]; c.xf.q.c = F32P(P, qc)[n]; c.xf.p = V(F32P(P, xpx)[n], F32P(P, xpy)[n]);
+  c.sleep = F32P(P, sleep)[n]; c.invdt0 = F32P(P, invdt0)[n];
+  c.fat.lo = V(F32P(P, flox)[n], F32P(P, floy)[n]); c.fat.hi = V(F32P(P, fhix)[n], F32P(P, fhiy)[n]);
+  c.imp = F64P(P, imp)[n];
+  c.awake = I32P(P, awake)[n]; c.nct = I32P(P, nct)[n]; c.overflow = I32P(P, overflow)[n];
+  c.imp_present = I32P(P, imp_present)[n]; c.nact = I32P(P, nact)[n];
+  c.disabled = I32P(P, disabled)[n];
+  c.just_disabled = 0;
+  c.force = zero2(); c.torque = 0.0f; c.c0 = c.c; c.a0 = c.a; c.alpha0 = 0.0f; c.moved = 0;
+  c.ct = P.ct + (size_t)n * MAXC; c.act_key = P.act_key + (size_t)n * MAXC; c.act_n = P.act_n + (size_t)n * MAXC * 2;
+  c.acc = nullptr;
+}
+// logic_kernel's write-back: every field but the vehicle-model ones (car_store_model) and the body
+// ones only the model kernel changes
+__device__ inline void car_store_logic(const Params& P, int n, const Car& c) {
   F32P(P, cum_reward)[n] = c.cum_reward; F32P(P, cum_reward_info)[n] = c.cum_reward_info;
   F64P(P, bank)[n] = c.bank; F64P(P, imp)[n] = c.imp;
   F64P(P, lt_start)[n] = c.lt_start; F64P(P, lt_cur)[n] = c.lt_cur; F64P(P, lt_last)[n] = c.lt_last;
@@ -198,8 +222,7 @@ __device__ inline void car_store_late(const Params& P, int n, const Car& c) {   
   F64P(P, prev_px)[n] = c.prev_px; F64P(P, prev_py)[n] = c.prev_py;
   F64P(P, prog_hist)[n] = c.prog_hist; F64P(P, back)[n] = c.back; F64P(P, prev_back)[n] = c.prev_back;
   F64P(P, imp_at_obs)[n] = c.imp_at_obs;
-  I32P(P, awake)[n] = c.awake; I32P(P, nct)[n] = c.nct; I32P(P, overflow)[n] = c.overflow;
-  I32P(P, imp_present)[n] = c.imp_present; I32P(P, nact)[n] = c.nact;
+  I32P(P, imp_present)[n] = c.imp_present;
   I32P(P, lt_timing)[n] = c.lt_timing; I32P(P, lt_has_last)[n] = c.lt_has_last; I32P(P, lt_has_best)[n] = c.lt_has_best;
   I32P(P, lt_crossed)[n] = c.lt_crossed; I32P(P, lt_has_pos)[n] = c.lt_has_pos; I32P(P, lt_laps)[n] = c.lt_laps;
   I32P(P, disabled)[n] = c.disabled; I32P(P, has_stuck_start)[n] = c.has_stuck_start;
@@ -947,11 +970,10 @@ __global__ void __launch_bounds__(BLOCK) sensor_kernel(Params P, float* obs, flo
   }
 }
 
-__global__ void __launch_bounds__(SBLOCK) step_kernel(Params P, const void* actions, int discrete, float* obs, float* reward,
-                                                     uint8_t* car_flags, uint8_t* env_flags, int auto_reset, float* terminal_obs) {
-  __shared__ int s_laps_old[SBLOCK], s_dis_old[SBLOCK], s_laps_new[SBLOCK], s_dis_new[SBLOCK], s_lapdone[SBLOCK];
-  __shared__ int s_dis_final[SBLOCK], s_below[SBLOCK];
-  __shared__ int s_envdone[SBLOCK];
+// The env step as two launches: model_kernel (actions -> Car.update_physics -> Box2D step, one lane
+// per car; its TOI code holds it at one wave per SIMD) hands the body / listener state to logic_kernel
+// (banking, disable logic, lap timer, rewards, termination, obs, auto-reset) through the state arrays.
+__global__ void __launch_bounds__(SBLOCK) model_kernel(Params P, const void* actions, int discrete) {
   const int tid = threadIdx.x, C = P.C;
   const int el = tid / C, car = tid - el * C;
   const int slot = blockIdx.x * P.epb + el;
@@ -960,6 +982,51 @@ __global__ void __launch_bounds__(SBLOCK) step_kernel(Params P, const void* acti
   PROF_RT(14);
   PROF(0);
   __shared__ DSeg s_segs[MAX_SEG];
+  TrackDev T = P.tracks[P.blk_track[blockIdx.x]];
+  if (tid < T.nseg) s_segs[tid] = T.segs[tid];
+  __syncthreads();
+  T.segs = s_segs;
+  PROF(1);
+  if (env < 0) return;
+  const WallSet S{T.walls, T.nwall, T.bp, T.sn};
+  Car c;
+  car_load_phys(P, n, c);
+  PROF(2);
+  // actions (BaseEnv._convert_to_internal_action / _discrete_to_continuous, np.float32)
+  float tb, st;
+  if (discrete) {
+    int a = ((const int*)actions)[n];
+    tb = a == 1 ? 1.0f : (a == 2 ? -1.0f : 0.0f);
+    st = a == 3 ? -1.0f : (a == 4 ? 1.0f : 0.0f);
+  } else {
+    tb = ((const float*)actions)[2 * n]; st = ((const float*)actions)[2 * n + 1];
+  }
+  float a0, a1, a2 = st;
+  if (tb >= 0) { a0 = tb; a1 = 0.0f; } else { a0 = 0.0f; a1 = -tb; }
+  if (c.disabled) { a0 = 0.0f; a1 = 0.0f; a2 = 0.0f; }
+  c.thr_in = pymax(0.0, pymin(1.0, (double)a0));
+  c.brk_in = pymax(0.0, pymin(1.0, (double)a1));
+  c.str_in = pymax(-1.0, pymin(1.0, (double)a2));
+  car_update_physics(P, c, n, T);
+  car_store_model(P, n, c);
+  asm volatile("" ::: "memory");   // keep the model write-back ahead of the Box2D step (register pressure)
+  PROF(3);
+  b2_step(c, S, P.dt_f, P.friction);
+  PROF(4);
+  car_store_body(P, n, c);
+}
+
+__global__ void __launch_bounds__(SBLOCK) logic_kernel(Params P, float* obs, float* reward, uint8_t* car_flags,
+                                                      uint8_t* env_flags, int auto_reset, float* terminal_obs) {
+  __shared__ int s_laps_old[SBLOCK], s_dis_old[SBLOCK], s_laps_new[SBLOCK], s_dis_new[SBLOCK], s_lapdone[SBLOCK];
+  __shared__ int s_dis_final[SBLOCK], s_below[SBLOCK];
+  __shared__ int s_envdone[SBLOCK];
+  const int tid = threadIdx.x, C = P.C;
+  const int el = tid / C, car = tid - el * C;
+  const int slot = blockIdx.x * P.epb + el;
+  const int env = (el < P.epb) ? P.blk_env[slot] : -1;
+  const int n = env >= 0 ? env * C + car : 0;
+  __shared__ DSeg s_segs[MAX_SEG];
   __shared__ double s_prefix[MAX_SEG];
   __shared__ float s_obs[SBLOCK * 22];
   __shared__ int s_rowbase[SBLOCK];
@@ -967,38 +1034,15 @@ __global__ void __launch_bounds__(SBLOCK) step_kernel(Params P, const void* acti
   if (tid < T.nseg) { s_segs[tid] = T.segs[tid]; s_prefix[tid] = T.prefix[tid]; }
   __syncthreads();
   T.segs = s_segs; T.prefix = s_prefix;
-  PROF(1);
   const int nw = T.nwall;
   const WallSet S{T.walls, nw, T.bp, T.sn};
   Car c;
   bool lapdone = false;
   double sim = 0.0;
   if (env >= 0) {
-    car_load_phys(P, n, c);
+    car_load_body(P, n, c);
     sim = P.env_time[env];
-    PROF(2);
     s_dis_old[tid] = c.disabled;
-    // actions (BaseEnv._convert_to_internal_action / _discrete_to_continuous, np.float32)
-    float tb, st;
-    if (discrete) {
-      int a = ((const int*)actions)[n];
-      tb = a == 1 ? 1.0f : (a == 2 ? -1.0f : 0.0f);
-      st = a == 3 ? -1.0f : (a == 4 ? 1.0f : 0.0f);
-    } else {
-      tb = ((const float*)actions)[2 * n]; st = ((const float*)actions)[2 * n + 1];
-    }
-    float a0, a1, a2 = st;
-    if (tb >= 0) { a0 = tb; a1 = 0.0f; } else { a0 = 0.0f; a1 = -tb; }
-    if (c.disabled) { a0 = 0.0f; a1 = 0.0f; a2 = 0.0f; }
-    c.thr_in = pymax(0.0, pymin(1.0, (double)a0));
-    c.brk_in = pymax(0.0, pymin(1.0, (double)a1));
-    c.str_in = pymax(-1.0, pymin(1.0, (double)a2));
-    car_update_physics(P, c, n, T);
-    car_store_model(P, n, c);
-    asm volatile("" ::: "memory");   // the tyre state is re-read from memory for the observation
-    PROF(3);
-    b2_step(c, S, P.dt_f, P.friction);
-    PROF(4);
     car_load_logic(P, n, c);
     s_laps_old[tid] = c.lt_laps;   // the lap count does not change before lap_update
     c.bank = T.has_banking ? banking_at(T, c.xf.p.x, c.xf.p.y) : 0.0;
@@ -1141,7 +1185,7 @@ __global__ void __launch_bounds__(SBLOCK) step_kernel(Params P, const void* acti
     }
     for (int i = 0; i < 22; ++i) s_obs[tid * 22 + i] = o[i];
     if (reset_now) car_store(P, n, c);    // car_reset rewrote every field
-    else car_store_late(P, n, c);
+    else car_store_logic(P, n, c);
     PROF(10);
     if (reset_now && car == 0) {
       P.env_time[env] = 0.0;
@@ -1599,8 +1643,10 @@ extern "C" int nascar_step(NascarHandle* h, const void* actions, int32_t discret
   if (!h || !actions || !obs || !reward) return fail("null argument");
   if (prepare(h)) return -1;
   Params P = make_params(h);
-  hipLaunchKernelGGL(step_kernel, dim3(h->nblocks), dim3(SBLOCK), 0, (hipStream_t)stream, P, actions, discrete,
-                     obs, reward, car_flags, env_flags, auto_reset, terminal_obs);
+  hipLaunchKernelGGL(model_kernel, dim3(h->nblocks), dim3(SBLOCK), 0, (hipStream_t)stream, P, actions, discrete);
+  HIPCHK(hipGetLastError());
+  hipLaunchKernelGGL(logic_kernel, dim3(h->nblocks), dim3(SBLOCK), 0, (hipStream_t)stream, P, obs, reward, car_flags,
+                     env_flags, auto_reset, terminal_obs);
   HIPCHK(hipGetLastError());
   launch_sensors(h, P, obs, terminal_obs, stream);
   HIPCHK(hipGetLastError());

@@ -6,7 +6,7 @@ Reads the rocprofv3 CSVs under <out_dir>/{kt,fetch,write}, and writes
   profiles/<tag>_kernel_stats.csv  (rocprofv3 --stats summary, copied verbatim)
   profiles/<tag>_pmc_step.json     (per-dispatch FETCH_SIZE / WRITE_SIZE of the two kernels of a step)
   profiles/pmc_traffic.json        (read by bench.py for roofline.traffic)
-One env step = one step_kernel + one sensor_kernel launch.  HBM bytes = (2 * FETCH_SIZE + WRITE_SIZE)
+One env step = one model_kernel + logic_kernel + sensor_kernel launch each.  HBM bytes = (2 * FETCH_SIZE + WRITE_SIZE)
 * 1024: FETCH_SIZE/WRITE_SIZE are in KiB and gfx950 FETCH_SIZE tallies half the bytes of a wide
 coalesced read (MI355X_MICROARCH.md "HBM").
 """
@@ -19,7 +19,7 @@ import sys
 from collections import defaultdict
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNELS = ("step_kernel", "sensor_kernel")
+KERNELS = ("model_kernel", "logic_kernel", "sensor_kernel")
 
 
 def _find(d, suffix):
