@@ -28,7 +28,15 @@ __device__ unsigned long long* g_prof = nullptr;
     if (g_prof && (threadIdx.x & 63) == 0) g_prof[((size_t)blockIdx.x * (BLOCK / 64) + threadIdx.x / 64) * 16 + (ph)] = _t; } while (0)
 #define PROFS(ph) do { unsigned long long _t = __builtin_amdgcn_s_memtime(); \
     if (g_prof && (threadIdx.x & 63) == 0) g_prof[(65536 + (size_t)blockIdx.x * (BLOCK / 64) + threadIdx.x / 64) * 16 + (ph)] = _t; } while (0)
+#define PROFS_RT(ph) do { unsigned long long _t = __builtin_amdgcn_s_memrealtime(); \
+    if (g_prof && (threadIdx.x & 63) == 0) g_prof[(65536 + (size_t)blockIdx.x * (BLOCK / 64) + threadIdx.x / 64) * 16 + (ph)] = _t; } while (0)
+// event counters: same-address global atomics from every lane serialise (milliseconds per launch), so
+// they have their own build flag and never run in a stamp (timing) build
+#ifdef NASCAR_PROFILE_COUNT
 #define PCOUNT(slot, v) do { if (g_prof) atomicAdd(&g_prof[2 * 65536 * 16 + (slot)], (unsigned long long)(v)); } while (0)
+#else
+#define PCOUNT(slot, v) do { } while (0)
+#endif
 #ifdef NASCAR_PROFILE_UP   // sub-phases of update_physics in slots 11-13 instead of b2_step's
 #define PROFB(ph) do { } while (0)
 #define PROFU(ph) PROF(ph)
@@ -44,15 +52,21 @@ __device__ unsigned long long* g_prof = nullptr;
     if (g_prof && (threadIdx.x & 63) == 0) g_prof[APROF_BASE + ((size_t)blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64) * 16 + (ph)] = _t; } while (0)
 #define APROF_RT(ph) do { unsigned long long _t = __builtin_amdgcn_s_memrealtime(); \
     if (g_prof && (threadIdx.x & 63) == 0) g_prof[APROF_BASE + ((size_t)blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64) * 16 + (ph)] = _t; } while (0)
+// logic_kernel stamps: region after the actor's (4096 waves x 16 slots)
+#define LPROF_BASE (APROF_BASE + 4096 * 16)
+#define LPROF(ph) do { unsigned long long _t = __builtin_amdgcn_s_memtime(); \
+    if (g_prof && (threadIdx.x & 63) == 0) g_prof[LPROF_BASE + ((size_t)blockIdx.x * (SBLOCK / 64) + threadIdx.x / 64) * 16 + (ph)] = _t; } while (0)
 #else
 #define PROF(ph) do { } while (0)
 #define PROFS(ph) do { } while (0)
+#define PROFS_RT(ph) do { } while (0)
 #define PROFB(ph) do { } while (0)
 #define PROFU(ph) do { } while (0)
 #define PCOUNT(slot, v) do { } while (0)
 #define PROF_RT(slot) do { } while (0)
 #define APROF(ph) do { } while (0)
 #define APROF_RT(ph) do { } while (0)
+#define LPROF(ph) do { } while (0)
 #endif
 
 namespace nascar {

@@ -50,6 +50,7 @@ struct TrackDev {
   double total_length; int startline; int has_banking;
   WallGrid bp, sn;
   const float4* groups; int ngroup;   // sensor wall groups: (cx, cy, radius incl. margin, first | count << 16)
+  const float4* swall;                // [2 * nwall] sensor image: (px, py, rad + 0.25, hx), (qs, qc, hy, 0)
 };
 
 struct Params {
@@ -800,9 +801,17 @@ __device__ __forceinline__ unsigned seg_ray_mask(float ax, float ay, float bx, f
 }
 
 template <int LPC>
-__global__ void __launch_bounds__(BLOCK) sensor_kernel(Params P, float* obs, float* terminal_obs) {
+#ifndef SENSOR_WPE
+#define SENSOR_WPE 6   // 80 VGPRs: all 5 464 waves of the 8192x10 bench resident at once (measured best of 4/5/6)
+#endif
+#ifndef SENSOR_LDS_WALLS
+#define SENSOR_GLOBAL_WALLS   // walls read from global (L1-resident) beat LDS staging: 46 KB/workgroup held occupancy at 3
+#endif
+__global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(SENSOR_WPE))) sensor_kernel(Params P, float* obs,
+                                                                                                        float* terminal_obs) {
   constexpr int CPW = BLOCK / LPC;          // cars per workgroup
   constexpr int RPL = 16 / LPC;             // rays whose end points / outputs a lane owns
+  PROFS_RT(14);
   PROFS(0);
   __shared__ float s_p2[CPW * 32];          // [car][ray][x, y]: f32 ray end points (exact test)
   __shared__ float s_dir[CPW * 32];         // [car][ray][x, y]: unit ray directions (cull only)
@@ -817,6 +826,15 @@ __global__ void __launch_bounds__(BLOCK) sensor_kernel(Params P, float* obs, flo
   const int env = (el < P.epb) ? P.blk_env[b * P.epb + el] : -1;
   const TrackDev T = P.tracks[P.blk_track[b]];
   const int nw = T.nwall, ng = T.ngroup;
+#ifdef SENSOR_GLOBAL_WALLS
+  // walls and groups read straight from the track's global image (L1/L2-resident, shared by every
+  // workgroup): no staging, no dynamic LDS
+  (void)swa; (void)nw;
+  const float4* __restrict__ swall = T.swall;
+#define SW_A(j) swall[2 * (j)]
+#define SW_B(j) swall[2 * (j) + 1]
+#define SW_G(g) T.groups[g]
+#else
   float4* swb = swa + nw;
   float4* sgr = swb + nw;
   for (int j = t; j < nw; j += BLOCK) {
@@ -825,6 +843,10 @@ __global__ void __launch_bounds__(BLOCK) sensor_kernel(Params P, float* obs, flo
     swb[j] = make_float4(w.qs, w.qc, w.hy, 0.0f);
   }
   for (int g = t; g < ng; g += BLOCK) sgr[g] = T.groups[g];
+#define SW_A(j) swa[j]
+#define SW_B(j) swb[j]
+#define SW_G(g) sgr[g]
+#endif
   const int n = env >= 0 ? env * C + car : 0;
   float4 pa = make_float4(0.f, 0.f, 0.f, 0.f), pb = pa;
   int mode = 0;
@@ -872,7 +894,7 @@ __global__ void __launch_bounds__(BLOCK) sensor_kernel(Params P, float* obs, flo
 #endif
       for (int kk = beg + r; kk < end; kk += LPC) {
         CNT(c_vis);
-        const float4 G = sgr[list ? (int)list[kk] : kk];
+        const float4 G = SW_G(list ? (int)list[kk] : kk);
         const float grx = G.x - p1.x, gry = G.y - p1.y;
         const float d2 = grx * grx + gry * gry;
         if (d2 > (250.0f + G.z) * (250.0f + G.z)) continue;
@@ -882,7 +904,7 @@ __global__ void __launch_bounds__(BLOCK) sensor_kernel(Params P, float* obs, flo
         float dlo;   // lower bound of any hit fraction in the group
         if (G.z > 24.0f) {   // a single long (straight) wall: mask from its end points
           const int j = __float_as_int(G.w) & 0xFFFF;
-          const float4 wa = swa[j], wb = swb[j];
+          const float4 wa = SW_A(j), wb = SW_B(j);
           const float ex = wa.w * wb.y, ey = wa.w * wb.x;   // hx * (qc, qs)
           const float cx = wa.x - p1.x, cy = wa.y - p1.y;
           float dseg;
@@ -902,10 +924,10 @@ __global__ void __launch_bounds__(BLOCK) sensor_kernel(Params P, float* obs, flo
         CNT(c_open);
         const int first = __float_as_int(G.w) & 0xFFFF, cnt = __float_as_int(G.w) >> 16;
         for (int j = first; j < first + cnt; ++j) {
-          const float4 wa = swa[j];
+          const float4 wa = SW_A(j);
           const float rx = wa.x - p1.x, ry = wa.y - p1.y;
           const float R = wa.z;
-          const float4 wb = swb[j];
+          const float4 wb = SW_B(j);
           Rot q; q.s = wb.x; q.c = wb.y;
           const V2 l1 = rmulT(q, V(p1.x - wa.x, p1.y - wa.y));
           const float hx = wa.w, hy = wb.z;
@@ -966,8 +988,12 @@ __global__ void __launch_bounds__(BLOCK) sensor_kernel(Params P, float* obs, flo
       }
     }
     if (pass == 0) PROFS(6);
+    if (pass == 0) PROFS_RT(15);
     if (!__syncthreads_or(mode & PM_B_OBS)) break;   // barrier: best / p2 are reused by pass 1
   }
+#undef SW_A
+#undef SW_B
+#undef SW_G
 }
 
 // The env step as two launches: model_kernel (actions -> Car.update_physics -> Box2D step, one lane
@@ -1014,6 +1040,8 @@ __global__ void __launch_bounds__(SBLOCK) model_kernel(Params P, const void* act
   b2_step(c, S, P.dt_f, P.friction);
   PROF(4);
   car_store_body(P, n, c);
+  PROF(5);
+  PROF_RT(15);
 }
 
 __global__ void __launch_bounds__(SBLOCK) logic_kernel(Params P, float* obs, float* reward, uint8_t* car_flags,
@@ -1026,6 +1054,7 @@ __global__ void __launch_bounds__(SBLOCK) logic_kernel(Params P, float* obs, flo
   const int slot = blockIdx.x * P.epb + el;
   const int env = (el < P.epb) ? P.blk_env[slot] : -1;
   const int n = env >= 0 ? env * C + car : 0;
+  LPROF(0);
   __shared__ DSeg s_segs[MAX_SEG];
   __shared__ double s_prefix[MAX_SEG];
   __shared__ float s_obs[SBLOCK * 22];
@@ -1044,6 +1073,7 @@ __global__ void __launch_bounds__(SBLOCK) logic_kernel(Params P, float* obs, flo
     sim = P.env_time[env];
     s_dis_old[tid] = c.disabled;
     car_load_logic(P, n, c);
+    LPROF(1);
     s_laps_old[tid] = c.lt_laps;   // the lap count does not change before lap_update
     c.bank = T.has_banking ? banking_at(T, c.xf.p.x, c.xf.p.y) : 0.0;
     if (!c.disabled) {   // _run_single_physics_step (src/car_env.py:582-638)
@@ -1058,7 +1088,7 @@ __global__ void __launch_bounds__(SBLOCK) logic_kernel(Params P, float* obs, flo
     lapdone = lap_update(T, c, c.xf.p.x, c.xf.p.y, sim);
     s_laps_new[tid] = c.lt_laps; s_dis_new[tid] = c.disabled; s_lapdone[tid] = lapdone;
   }
-  PROF(5);
+  LPROF(2);
   __syncthreads();
   // env pass 1: lap-reset pending (src/car_env.py:672-676 with _all_active_cars_completed_lap :1640-1669,
   // evaluated in car order with cars > i not yet updated)
@@ -1100,10 +1130,10 @@ __global__ void __launch_bounds__(SBLOCK) logic_kernel(Params P, float* obs, flo
         }
       } else { c.stuck_dur = 0.0; c.has_stuck_start = 0; }
     }
-    PROF(6);
+    LPROF(3);
     car_reload_tyres(P, n, c);
     car_obs(c, o);
-    PROF(7);
+    LPROF(4);
     // _calculate_multi_rewards (src/car_env.py:980-1113)
     if (c.disabled && !c.just_disabled) rew = 0.0f;
     else {
@@ -1139,7 +1169,7 @@ __global__ void __launch_bounds__(SBLOCK) logic_kernel(Params P, float* obs, flo
     s_dis_final[tid] = c.disabled;
     s_below[tid] = (!c.disabled && c.cum_reward < -250.0f) ? 1 : 0;
   }
-  PROF(8);
+  LPROF(5);
   __syncthreads();
   // env pass 2: termination (src/car_env.py:1115-1158, 791-794)
   if (env >= 0 && car == 0) {
@@ -1173,7 +1203,7 @@ __global__ void __launch_bounds__(SBLOCK) logic_kernel(Params P, float* obs, flo
     reward[n] = rew;
     if (car_flags) car_flags[n] = flags;
     const bool reset_now = auto_reset && s_envdone[el];
-    PROF(9);
+    LPROF(6);
     if (terminal_obs) { float* t = terminal_obs + (size_t)n * 38; for (int i = 0; i < 22; ++i) t[i] = o[i]; }
     if (reset_now) {
       P.pose[n] = car_pose(c, terminal_obs ? (PM_A_TERM | PM_B_OBS) : PM_B_OBS);
@@ -1186,7 +1216,7 @@ __global__ void __launch_bounds__(SBLOCK) logic_kernel(Params P, float* obs, flo
     for (int i = 0; i < 22; ++i) s_obs[tid * 22 + i] = o[i];
     if (reset_now) car_store(P, n, c);    // car_reset rewrote every field
     else car_store_logic(P, n, c);
-    PROF(10);
+    LPROF(7);
     if (reset_now && car == 0) {
       P.env_time[env] = 0.0;
       P.env_i32[E_PENDING * P.E + env] = 0; P.env_i32[E_REASON * P.E + env] = 0;
@@ -1201,7 +1231,7 @@ __global__ void __launch_bounds__(SBLOCK) logic_kernel(Params P, float* obs, flo
     const int base = s_rowbase[row];
     if (base >= 0) obs[(size_t)base + col] = s_obs[i];
   }
-  PROF_RT(15);
+  LPROF(8);
 }
 
 __global__ void __launch_bounds__(SBLOCK) reset_kernel(Params P, const uint8_t* mask, float* obs) {
@@ -1324,6 +1354,7 @@ struct HostTrack {
   LWall* d_walls = nullptr; DSeg* d_segs = nullptr; double* d_prefix = nullptr;
   HostGrid bp, sn;
   std::vector<float4> groups; float4* d_groups = nullptr;
+  float4* d_swall = nullptr;
 };
 
 // Wall grids (see WallGrid in nascar_device.h).  Conservative by construction: the
@@ -1481,7 +1512,7 @@ extern "C" void nascar_destroy(NascarHandle* h) {
   hipFree(h->arena); hipFree(h->d_ctl); hipFree(h->d_pose); hipFree(h->d_actor);
   for (auto& t : h->tracks) {
     hipFree(t.d_walls); hipFree(t.d_segs); hipFree(t.d_prefix);
-    hipFree(t.bp.d_start); hipFree(t.bp.d_idx); hipFree(t.sn.d_start); hipFree(t.sn.d_idx); hipFree(t.d_groups);
+    hipFree(t.bp.d_start); hipFree(t.bp.d_idx); hipFree(t.sn.d_start); hipFree(t.sn.d_idx); hipFree(t.d_groups); hipFree(t.d_swall);
   }
   hipFree(h->d_tracks); hipFree(h->d_blk_track); hipFree(h->d_blk_env);
   delete h;
@@ -1549,6 +1580,16 @@ extern "C" int nascar_add_track(NascarHandle* h, const double* segments, int32_t
   if (upload_grid(t.bp) < 0 || upload_grid(t.sn) < 0) return -1;
   HIPCHK(hipMalloc(&t.d_groups, sizeof(float4) * t.groups.size()));
   HIPCHK(hipMemcpy(t.d_groups, t.groups.data(), sizeof(float4) * t.groups.size(), hipMemcpyHostToDevice));
+  {   // the sensor kernel's wall image (same f32 values it would stage: rad + 0.25 rounded once)
+    std::vector<float4> sw(2 * t.walls.size());
+    for (size_t j = 0; j < t.walls.size(); ++j) {
+      const LWall& w = t.walls[j];
+      sw[2 * j] = make_float4(w.px, w.py, w.rad + 0.25f, w.hx);
+      sw[2 * j + 1] = make_float4(w.qs, w.qc, w.hy, 0.0f);
+    }
+    HIPCHK(hipMalloc(&t.d_swall, sizeof(float4) * sw.size()));
+    HIPCHK(hipMemcpy(t.d_swall, sw.data(), sizeof(float4) * sw.size(), hipMemcpyHostToDevice));
+  }
   h->max_sensor_lds = std::max(h->max_sensor_lds, 2 * sizeof(float4) * t.walls.size() + sizeof(float4) * t.groups.size());
   h->tracks.push_back(t);
   h->max_lds = std::max(h->max_lds, lds);
@@ -1579,7 +1620,7 @@ static int prepare(NascarHandle* h) {
     TrackDev d;
     d.walls = t.d_walls; d.nwall = (int)t.walls.size(); d.segs = t.d_segs; d.nseg = (int)t.segs.size();
     d.prefix = t.d_prefix; d.total_length = t.total_length; d.startline = t.startline; d.has_banking = t.has_banking;
-    d.bp = t.bp.g; d.sn = t.sn.g; d.groups = t.d_groups; d.ngroup = (int)t.groups.size();
+    d.bp = t.bp.g; d.sn = t.sn.g; d.groups = t.d_groups; d.ngroup = (int)t.groups.size(); d.swall = t.d_swall;
     td.push_back(d);
   }
   hipFree(h->d_tracks);
@@ -1621,7 +1662,11 @@ static Params make_params(NascarHandle* h) {
 }
 
 static void launch_sensors(NascarHandle* h, const Params& P, float* obs, float* terminal_obs, void* stream) {
+#ifdef SENSOR_GLOBAL_WALLS
+  const size_t lds = 0;
+#else
   const size_t lds = h->max_sensor_lds;
+#endif
   const int sub = (SBLOCK + BLOCK / SENSOR_LPC - 1) / (BLOCK / SENSOR_LPC);
   hipLaunchKernelGGL(sensor_kernel<SENSOR_LPC>, dim3(h->nblocks * sub), dim3(BLOCK), lds, (hipStream_t)stream,
                      P, obs, terminal_obs);

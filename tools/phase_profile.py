@@ -1,9 +1,12 @@
-"""Per-phase cycle profile of step_kernel (profile build, -DNASCAR_PROFILE).
+"""Per-phase cycle profile of one env step (profile build, -DNASCAR_PROFILE).
 
-    python tools/phase_profile.py [--envs E] [--cars C] [--track daytona] [--steps S]
+    python tools/phase_profile.py [--envs E] [--cars C] [--track daytona] [--steps S] [--up]
 
-Builds tools/libnascar_prof.so, runs S steps of uniform random driving after a warm-up and prints, per
-phase, the mean/max s_memtime cycles per wave, plus the wave start/end spread (s_memrealtime, 100 MHz).
+Builds tools/libnascar_prof.so (or --lib), runs S steps of uniform random driving after a warm-up and
+prints, per kernel and phase, the mean/max s_memtime cycles per wave, plus the realtime spread of
+model_kernel waves (s_memrealtime, 100 MHz).  Stamp regions (nascar_device.h): model_kernel PROF
+slots 0-5 (+ sub-phases 11-13, realtime 14/15), sensor_kernel PROFS slots 0-6, logic_kernel LPROF
+slots 0-8, counters after the sensor region.
 """
 import argparse
 import ctypes
@@ -17,8 +20,27 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 from nascargymnasium_amd import _lib  # noqa: E402
 
-PHASES = ["stage_track+sync", "car_load", "update_physics", "b2_step", "bank/disable/lap+sync_pre",
-          "sync1+envpass1+stuck", "car_obs(sensors)", "rewards+sync_pre", "sync2+term+sync3", "obs+state store"]
+NW = 65536
+APROF_BASE = 2 * NW * 16 + 64
+LPROF_BASE = APROF_BASE + 4096 * 16
+MODEL = ["stage segments", "car_load_phys", "update_physics", "b2_step", "store body"]
+LOGIC = ["stage + load body/logic", "bank/disable/lap + sync", "env pass 1 + stuck", "car_obs",
+         "rewards + sync", "env pass 2 (termination) + sync", "reset / pose / state store", "obs rows"]
+SENSOR = ["setup (walls/groups/pose)", "ray end points (f64 sincos)", "barrier", "group/wall cull", "barrier",
+          "write obs"]
+
+
+def phases(rows, names, first, title, extra=""):
+    rows = rows[(rows[:, first] != 0) & (rows[:, first + len(names)] != 0)].astype(np.float64)
+    if not len(rows):
+        print(f"{title}: no stamped waves")
+        return rows
+    d = np.diff(rows[:, first:first + len(names) + 1], axis=1)
+    tot = d.sum(1)
+    print(f"{title}: waves {len(rows)}, mean wave cycles {tot.mean():.0f} (max {tot.max():.0f}){extra}")
+    for k, name in enumerate(names):
+        print(f"  {name:34s} mean {d[:, k].mean():9.0f}  max {d[:, k].max():9.0f}  {100 * d[:, k].mean() / tot.mean():5.1f}%")
+    return rows
 
 
 def main():
@@ -26,16 +48,20 @@ def main():
     ap.add_argument("--envs", type=int, default=8192)
     ap.add_argument("--cars", type=int, default=10)
     ap.add_argument("--track", default="daytona")
-    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=100)
     ap.add_argument("--no-build", action="store_true")
     ap.add_argument("--lib", default="libnascar_prof.so")
     ap.add_argument("--up", action="store_true", help="library built with -DNASCAR_PROFILE_UP")
+    ap.add_argument("--raw", type=int, default=0, help="print this many raw sensor stamp rows")
+    ap.add_argument("--count", action="store_true", help="library built with -DNASCAR_PROFILE_COUNT (sensor event "
+                    "counters; the atomics distort that build's sensor timings)")
     a = ap.parse_args()
     so = os.path.join(ROOT, "tools", a.lib)
     if not a.no_build:
-        subprocess.run(["hipcc"] + _lib.HIPCC_FLAGS + ["-DNASCAR_PROFILE", "-o", so,
-                        os.path.join(_lib.CSRC, "nascar_kernels.hip")], check=True)
+        subprocess.run(["hipcc"] + _lib.HIPCC_FLAGS + ["-DNASCAR_PROFILE"] + (["-DNASCAR_PROFILE_UP"] if a.up else [])
+                       + (["-DNASCAR_PROFILE_COUNT"] if a.count else [])
+                       + ["-o", so, os.path.join(_lib.CSRC, "nascar_kernels.hip")], check=True)
     _lib.LIB_PATH = so
     import torch
     from nascargymnasium_amd.batched import BatchedCarEnv
@@ -44,69 +70,54 @@ def main():
     L.nascar_debug_profile.argtypes = [ctypes.c_void_p]
     env = BatchedCarEnv(a.envs, a.cars, track_path(a.track), device="cuda:0")
     env.reset()
-    g = torch.Generator(device="cuda:0"); g.manual_seed(7)
+    g = torch.Generator(device="cuda:0")
+    g.manual_seed(7)
     for _ in range(a.warmup):
         env.step(torch.rand((a.envs, a.cars, 2), generator=g, device="cuda:0") * 2 - 1, auto_reset=True)
-    nwaves = 65536
-    buf = torch.zeros(2 * nwaves * 16 + 16, dtype=torch.int64, device="cuda:0")
+    buf = torch.zeros(LPROF_BASE + NW * 16, dtype=torch.int64, device="cuda:0")
     L.nascar_debug_profile(ctypes.c_void_p(buf.data_ptr()))
-    acc = []
-    for _ in range(a.steps):
+    for s in range(a.steps):
         acts = torch.rand((a.envs, a.cars, 2), generator=g, device="cuda:0") * 2 - 1
         buf.zero_()
         torch.cuda.synchronize()
         env.launch_step(acts, auto_reset=True)
         torch.cuda.synchronize()
-        acc.append(buf[:2 * nwaves * 16].view(2 * nwaves, 16).cpu().numpy().copy())
-        cnt = buf[2 * nwaves * 16:].cpu().numpy()
-        if cnt[6]:
-            print("sensor workgroups %d: per WG items %.1f q1 %.1f q2 %.1f | rays with a hit (any lane) %.1f | active cars %.1f"
-                  % (cnt[6], cnt[0] / cnt[6], cnt[1] / cnt[6], cnt[2] / cnt[6], cnt[3] / cnt[6], cnt[5] / cnt[6]))
+        b = buf.cpu().numpy()
+        model = b[:NW * 16].reshape(NW, 16)
+        sens = b[NW * 16:2 * NW * 16].reshape(NW, 16)
+        cnt = b[2 * NW * 16:2 * NW * 16 + 8]
+        logic = b[LPROF_BASE:LPROF_BASE + NW * 16].reshape(NW, 16)
+        print(f"--- step {s}")
+        m = phases(model, MODEL, 0, "model_kernel")
+        if len(m) and a.up:
+            sub = np.stack([m[:, 11] - m[:, 2], m[:, 12] - m[:, 11], m[:, 13] - m[:, 12], m[:, 3] - m[:, 13]], 1)
+            for k, name in enumerate(["engine force", "brake/drag/rolling + acc history", "weight transfer + tyres",
+                                      "lateral..end"]):
+                print(f"    update_physics/{name:32s} mean {sub[:, k].mean():9.0f}")
+        elif len(m):
+            sub = np.stack([m[:, 11] - m[:, 3], m[:, 12] - m[:, 11], m[:, 13] - m[:, 12], m[:, 4] - m[:, 13]], 1)
+            for k, name in enumerate(["collide", "solve", "sync_fixtures+find_new_contacts", "solve_toi"]):
+                print(f"    b2_step/{name:38s} mean {sub[:, k].mean():9.0f}")
+        if len(m):
+            st, en = m[:, 14], m[:, 15]
+            print(f"    realtime us: last start {(st.max() - st.min()) / 100:.1f}, median end {(np.median(en) - st.min()) / 100:.1f}, "
+                  f"last end {(en.max() - st.min()) / 100:.1f}")
+        phases(logic, LOGIC, 0, "logic_kernel")
+        if a.raw:
+            live = sens[sens[:, 0] != 0]
+            print("raw sensor stamps (first rows, slots 0-6):")
+            for row in live[:a.raw]:
+                print("   ", row[:7] - row[0], " realtime us:", (row[15] - row[14]) / 100)
+            rt = live[:, 15] - live[:, 14]
+            print(f"  sensor realtime per wave us: mean {rt.mean() / 100:.1f} max {rt.max() / 100:.1f}; "
+                  f"kernel span {(live[:, 15].max() - live[:, 14].min()) / 100:.1f}")
+        n = cnt[6]
+        extra = ""
+        if n:
+            extra = (f"\n  per active lane: groups visited {cnt[0] / n:.1f}, in range {cnt[1] / n:.1f}, open {cnt[2] / n:.1f}, "
+                     f"walls {cnt[3] / n:.1f}, wall-ray pairs {cnt[4] / n:.1f}, exact casts {cnt[5] / n:.1f}")
+        phases(sens, SENSOR, 0, "sensor_kernel", extra)
     L.nascar_debug_profile(ctypes.c_void_p(0))
-    sens = []
-    for b in acc:
-        sb = b[nwaves:]
-        sb = sb[(sb[:, 0] != 0) & (sb[:, 6] != 0)].astype(np.float64)
-        sens.append(np.diff(sb[:, :7], axis=1))
-    acc = [b[:nwaves] for b in acc]
-    res = []
-    for b in acc:
-        b = b[b[:, 10] != 0]
-        d = np.diff(b[:, :11].astype(np.float64), axis=1)
-        res.append((d, b[:, 14], b[:, 15]))
-    d = np.concatenate([r[0] for r in res])
-    tot = d.sum(1)
-    # b2_step sub-phases: 3 -> 11 collide, 11 -> 12 solve, 12 -> 13 broadphase update, 13 -> 4 solve_toi
-    sub = []
-    for b in acc:
-        b = b[(b[:, 10] != 0) & (b[:, 11] != 0) & (b[:, 12] != 0) & (b[:, 13] != 0)].astype(np.float64)
-        sub.append(np.stack([b[:, 11] - b[:, 3], b[:, 12] - b[:, 11], b[:, 13] - b[:, 12], b[:, 4] - b[:, 13]], 1))
-    sub = np.concatenate(sub)
-    print(f"waves/launch {len(res[0][0])}, mean wave cycles {tot.mean():.0f} (max {tot.max():.0f})")
-    for k, name in enumerate(PHASES):
-        print(f"  {name:28s} mean {d[:, k].mean():10.0f}  max {d[:, k].max():10.0f}  {100 * d[:, k].mean() / tot.mean():5.1f}%")
-    if len(sub):
-        names = (["engine force", "brake/drag/rolling + acc history", "weight transfer + tyres", "lateral..end"]
-                 if a.up else ["collide", "solve", "sync_fixtures+find_new_contacts", "solve_toi"])
-        pre = "update_physics" if a.up else "b2_step"
-        if a.up:   # slots: 2 -> 11 -> 12 -> 13 -> 3
-            sub = []
-            for b in acc:
-                b = b[(b[:, 10] != 0) & (b[:, 11] != 0) & (b[:, 12] != 0) & (b[:, 13] != 0)].astype(np.float64)
-                sub.append(np.stack([b[:, 11] - b[:, 2], b[:, 12] - b[:, 11], b[:, 13] - b[:, 12], b[:, 3] - b[:, 13]], 1))
-            sub = np.concatenate(sub)
-        for k, name in enumerate(names):
-            print(f"    {pre}/{name:34s} mean {sub[:, k].mean():10.0f}  max {sub[:, k].max():10.0f}")
-    sd = np.concatenate(sens)
-    if len(sd):
-        print(f"sensor_kernel: waves/launch {len(sens[0])}, mean wave cycles {sd.sum(1).mean():.0f}")
-        for k, name in enumerate(["setup (walls/groups/pose)", "ray end points (f64 cos/sin)", "barrier", "group/wall cull",
-                                  "barrier", "write obs"]):
-            print(f"  {name:30s} mean {sd[:, k].mean():10.0f}  max {sd[:, k].max():10.0f}")
-    for _, st, en in res[:3]:
-        t0 = st.min()
-        print(f"  realtime (us): first start 0, last start {(st.max() - t0) / 100:.1f}, "
-              f"median end {(np.median(en) - t0) / 100:.1f}, last end {(en.max() - t0) / 100:.1f}")
     env.close()
 
 
