@@ -808,7 +808,7 @@ template <int LPC>
 #define SENSOR_GLOBAL_WALLS   // walls read from global (L1-resident) beat LDS staging: 46 KB/workgroup held occupancy at 3
 #endif
 __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(SENSOR_WPE))) sensor_kernel(Params P, float* obs,
-                                                                                                        float* terminal_obs) {
+                                                                                                        float* terminal_obs, int passes) {
   constexpr int CPW = BLOCK / LPC;          // cars per workgroup
   constexpr int RPL = 16 / LPC;             // rays whose end points / outputs a lane owns
   PROFS_RT(14);
@@ -849,17 +849,16 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(SENS
 #endif
   const int n = env >= 0 ? env * C + car : 0;
   float4 pa = make_float4(0.f, 0.f, 0.f, 0.f), pb = pa;
-  int mode = 0;
+  int mode = 0;   // A bits from pose[n], the B bit from pose[N + n]
   if (env >= 0) {
-    pa = P.pose[n];
-    mode = __float_as_int(pa.w);
-    if (mode & PM_B_OBS) pb = P.pose[P.N + n];
+    if (passes & 1) { pa = P.pose[n]; mode = __float_as_int(pa.w) & (PM_A_OBS | PM_A_TERM); }
+    if (passes & 2) { pb = P.pose[P.N + n]; mode |= __float_as_int(pb.w) & PM_B_OBS; }
   }
   PROFS(1);
   unsigned* best = s_best + lc * 16;
   const float* p2s = s_p2 + lc * 32;
   const float* dirs = s_dir + lc * 32;
-  for (int pass = 0; pass < 2; ++pass) {
+  for (int pass = (passes & 1) ? 0 : 1; pass < ((passes & 2) ? 2 : 1); ++pass) {
     const bool active = env >= 0 && (pass == 0 ? (mode & (PM_A_OBS | PM_A_TERM)) != 0 : (mode & PM_B_OBS) != 0);
     const float4 ps = pass == 0 ? pa : pb;
     const V2 p1 = V(ps.x, ps.y);
@@ -999,7 +998,7 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(SENS
 // The env step as two launches: model_kernel (actions -> Car.update_physics -> Box2D step, one lane
 // per car; its TOI code holds it at one wave per SIMD) hands the body / listener state to logic_kernel
 // (banking, disable logic, lap timer, rewards, termination, obs, auto-reset) through the state arrays.
-__global__ void __launch_bounds__(SBLOCK) model_kernel(Params P, const void* actions, int discrete) {
+__global__ void __launch_bounds__(SBLOCK) model_kernel(Params P, const void* actions, int discrete, int want_term) {
   const int tid = threadIdx.x, C = P.C;
   const int el = tid / C, car = tid - el * C;
   const int slot = blockIdx.x * P.epb + el;
@@ -1040,6 +1039,7 @@ __global__ void __launch_bounds__(SBLOCK) model_kernel(Params P, const void* act
   b2_step(c, S, P.dt_f, P.friction);
   PROF(4);
   car_store_body(P, n, c);
+  P.pose[n] = car_pose(c, PM_A_OBS | (want_term ? PM_A_TERM : 0));   // sensor pass A
   PROF(5);
   PROF_RT(15);
 }
@@ -1205,13 +1205,14 @@ __global__ void __launch_bounds__(SBLOCK) logic_kernel(Params P, float* obs, flo
     const bool reset_now = auto_reset && s_envdone[el];
     LPROF(6);
     if (terminal_obs) { float* t = terminal_obs + (size_t)n * 38; for (int i = 0; i < 22; ++i) t[i] = o[i]; }
+    // sensor pass B: the reset pose of every auto-reset car (its pass-B values overwrite the pass-A
+    // ones in obs); cleared for every other car
     if (reset_now) {
-      P.pose[n] = car_pose(c, terminal_obs ? (PM_A_TERM | PM_B_OBS) : PM_B_OBS);
       car_reset(P, c, n, false, S, T);
       car_obs(c, o);
-      P.pose[P.N + n] = car_pose(c, 0);
+      P.pose[P.N + n] = car_pose(c, PM_B_OBS);
     } else {
-      P.pose[n] = car_pose(c, terminal_obs ? (PM_A_OBS | PM_A_TERM) : PM_A_OBS);
+      P.pose[P.N + n] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
     for (int i = 0; i < 22; ++i) s_obs[tid * 22 + i] = o[i];
     if (reset_now) car_store(P, n, c);    // car_reset rewrote every field
@@ -1661,7 +1662,9 @@ static Params make_params(NascarHandle* h) {
   return P;
 }
 
-static void launch_sensors(NascarHandle* h, const Params& P, float* obs, float* terminal_obs, void* stream) {
+// passes: 1 = pass A only (pose[n] with its A-mode bits: nascar_reset), 3 = pass A then pass B (the reset
+// poses pose[N + n] of auto-reset cars overwrite those cars' pass-A obs values: nascar_step)
+static void launch_sensors(NascarHandle* h, const Params& P, float* obs, float* terminal_obs, int passes, void* stream) {
 #ifdef SENSOR_GLOBAL_WALLS
   const size_t lds = 0;
 #else
@@ -1669,7 +1672,7 @@ static void launch_sensors(NascarHandle* h, const Params& P, float* obs, float* 
 #endif
   const int sub = (SBLOCK + BLOCK / SENSOR_LPC - 1) / (BLOCK / SENSOR_LPC);
   hipLaunchKernelGGL(sensor_kernel<SENSOR_LPC>, dim3(h->nblocks * sub), dim3(BLOCK), lds, (hipStream_t)stream,
-                     P, obs, terminal_obs);
+                     P, obs, terminal_obs, passes);
 }
 
 extern "C" int nascar_reset(NascarHandle* h, const uint8_t* env_mask, float* obs, void* stream) {
@@ -1678,7 +1681,7 @@ extern "C" int nascar_reset(NascarHandle* h, const uint8_t* env_mask, float* obs
   Params P = make_params(h);
   hipLaunchKernelGGL(reset_kernel, dim3(h->nblocks), dim3(SBLOCK), 0, (hipStream_t)stream, P, env_mask, obs);
   HIPCHK(hipGetLastError());
-  launch_sensors(h, P, obs, nullptr, stream);
+  launch_sensors(h, P, obs, nullptr, 1, stream);
   HIPCHK(hipGetLastError());
   return 0;
 }
@@ -1688,12 +1691,16 @@ extern "C" int nascar_step(NascarHandle* h, const void* actions, int32_t discret
   if (!h || !actions || !obs || !reward) return fail("null argument");
   if (prepare(h)) return -1;
   Params P = make_params(h);
-  hipLaunchKernelGGL(model_kernel, dim3(h->nblocks), dim3(SBLOCK), 0, (hipStream_t)stream, P, actions, discrete);
+  // model_kernel -> logic_kernel -> sensor_kernel (pass A for every car, pass B for auto-reset cars).
+  // Kept on the caller's stream: a cross-stream event hop measured 10-15 us on the MI355X box, more than
+  // running logic_kernel and sensor pass A concurrently would save.
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(model_kernel, dim3(h->nblocks), dim3(SBLOCK), 0, s, P, actions, discrete, terminal_obs != nullptr);
   HIPCHK(hipGetLastError());
-  hipLaunchKernelGGL(logic_kernel, dim3(h->nblocks), dim3(SBLOCK), 0, (hipStream_t)stream, P, obs, reward, car_flags,
+  hipLaunchKernelGGL(logic_kernel, dim3(h->nblocks), dim3(SBLOCK), 0, s, P, obs, reward, car_flags,
                      env_flags, auto_reset, terminal_obs);
   HIPCHK(hipGetLastError());
-  launch_sensors(h, P, obs, terminal_obs, stream);
+  launch_sensors(h, P, obs, terminal_obs, auto_reset ? 3 : 1, stream);
   HIPCHK(hipGetLastError());
   return 0;
 }
