@@ -23,6 +23,7 @@
 #include "../../include/nascar.h"
 #include "nascar_device.h"
 #include "nascar_actor.h"
+#include "nascar_rays.h"
 
 #pragma clang fp contract(off)
 
@@ -577,16 +578,87 @@ __device__ inline bool on_startline(const TrackDev& T, double px, double py) {
   }
   return d <= (s.width / 2.0);
 }
+
+// f32 screen of the chord searches above, for the logic kernel (segments staged in LDS as
+// (sx, sy, ex - sx, ey - sy) plus 1 / |e - s|^2, 0 for chords shorter than 1e-3 m).  A screened
+// distance is within screen_eps of the f64 one (f32 rounding of coordinates and of the projection:
+// ~1e-3 m on km-sized tracks; the term in |p| covers far-off cars), so a chord whose screened
+// distance exceeds the screened minimum by more than 2 screen_eps is strictly farther than the
+// screened minimiser in f64 too: it can neither be nor tie the reference's nearest chord.  The
+// exact f64 evaluation (with the reference's strict '<', in index order) runs on the rest only.
+struct ChordScreen { const float4* g; const float* rll; int n; };
+__device__ __forceinline__ float screen_eps(float x, float y) { return 0.05f + 4e-6f * (fabsf(x) + fabsf(y)); }
+__device__ __forceinline__ float screen_d2(const ChordScreen& S, int k, float x, float y) {
+  const float4 g = S.g[k];
+  const float rx = x - g.x, ry = y - g.y;
+  const float tt = fminf(1.0f, fmaxf(0.0f, (rx * g.z + ry * g.w) * S.rll[k]));
+  const float ex = rx - tt * g.z, ey = ry - tt * g.w;
+  return ex * ex + ey * ey;
+}
+// squared screened distance above which a chord cannot be the nearest one
+__device__ inline float screen_cut(const ChordScreen& S, float x, float y) {
+  float m = INFINITY;
+  for (int k = 0; k < S.n; ++k) m = fminf(m, screen_d2(S, k, x, y));
+  const float r = __builtin_amdgcn_sqrtf(m) + 2.0f * screen_eps(x, y);
+  return r * r * 1.0001f;
+}
+// banking_at / track_progress restricted to the chords that pass the screen (same results)
+__device__ inline double banking_at_screened(const TrackDev& T, const ChordScreen& S, float cut, double px, double py) {
+  double best = INFINITY; int bi = -1;
+  for (int k = 0; k < T.nseg; ++k) {
+    if (screen_d2(S, k, (float)px, (float)py) > cut) continue;
+    const DSeg& s = T.segs[k];
+    double ll = P2(s.ex - s.sx) + P2(s.ey - s.sy), d;
+    if (ll == 0) d = sqrt(P2(px - s.sx) + P2(py - s.sy));
+    else {
+      double tt = ((px - s.sx) * (s.ex - s.sx) + (py - s.sy) * (s.ey - s.sy)) / ll;
+      tt = pymax(0.0, pymin(1.0, tt));
+      double qx = s.sx + tt * (s.ex - s.sx), qy = s.sy + tt * (s.ey - s.sy);
+      d = sqrt(P2(px - qx) + P2(py - qy));
+    }
+    if (d < best) { best = d; bi = k; }
+  }
+  return bi >= 0 ? T.segs[bi].banking : 0.0;
+}
+__device__ inline double track_progress_screened(const TrackDev& T, const ChordScreen& S, float cut, double px, double py) {
+  double best = INFINITY; int bi = 0; double bx = 0, by = 0;
+  for (int k = 0; k < T.nseg; ++k) {
+    if (screen_d2(S, k, (float)px, (float)py) > cut) continue;
+    const DSeg& s = T.segs[k];
+    double dx = s.ex - s.sx, dy = s.ey - s.sy, ll = dx * dx + dy * dy, qx, qy;
+    if (ll < 1e-6) { qx = s.sx; qy = s.sy; }
+    else {
+      double tt = pymax(0.0, pymin(1.0, ((px - s.sx) * dx + (py - s.sy) * dy) / ll));
+      qx = s.sx + tt * dx; qy = s.sy + tt * dy;
+    }
+    double d2 = P2(px - qx) + P2(py - qy);
+    if (d2 < best) { best = d2; bi = k; bx = qx; by = qy; }
+  }
+  const DSeg& s = T.segs[bi];
+  return T.prefix[bi] + sqrt(P2(bx - s.sx) + P2(by - s.sy));
+}
+// on_startline, decided by the screen unless the screened distance is within screen_eps of width / 2
+__device__ inline bool on_startline_screened(const TrackDev& T, const ChordScreen& S, double px, double py) {
+  const float x = (float)px, y = (float)py;
+  const float d = __builtin_amdgcn_sqrtf(screen_d2(S, T.startline, x, y));
+  const float h = (float)(T.segs[T.startline].width / 2.0), e = screen_eps(x, y);
+  if (d < h - e) return true;
+  if (d > h + e) return false;
+  return on_startline(T, px, py);
+}
 // LapTimer.update (src/lap_timer.py:95-272)
-__device__ inline bool lap_update(const TrackDev& T, Car& c, double px, double py, double sim) {
+// lt_has_pos: bit 0 = a previous position is recorded, bit 1 = that position was on the start line
+// (LapTimer._is_on_start_line(previous_position), src/lap_timer.py:193, evaluated when it was current)
+__device__ inline bool lap_update(const TrackDev& T, const ChordScreen& S, Car& c, double px, double py, double sim) {
   if (c.lt_timing) c.lt_cur = sim - c.lt_start;
   if (c.lt_has_pos) {
     double dx = px - c.lt_px, dy = py - c.lt_py, d = sqrt(dx * dx + dy * dy);
     if (d < 50.0) c.lt_dist += d;
   }
   bool done = false;
+  const bool now = T.startline >= 0 && on_startline_screened(T, S, px, py);
   if (T.startline >= 0 && c.lt_has_pos) {
-    bool now = on_startline(T, px, py), before = on_startline(T, c.lt_px, c.lt_py);
+    const bool before = (c.lt_has_pos & 2) != 0;
     if (now && !before) {
       if (c.lt_crossed && c.lt_timing) {
         double minlap = T.total_length > 0 ? T.total_length * 0.95 : 100.0;
@@ -605,7 +677,7 @@ __device__ inline bool lap_update(const TrackDev& T, Car& c, double px, double p
       }
     }
   }
-  c.lt_px = px; c.lt_py = py; c.lt_has_pos = 1;
+  c.lt_px = px; c.lt_py = py; c.lt_has_pos = now ? 3 : 1;
   return done;
 }
 
@@ -754,6 +826,16 @@ __device__ __forceinline__ float sensor_value(float best) {   // DistanceSensor 
   return v < 0.0f ? 0.0f : (v > 1.0f ? 1.0f : v);
 }
 
+// ray offsets of DistanceSensor (nascar_rays.h)
+__constant__ double c_ray_cs[16][2] = NASCAR_RAY_CS_INIT;
+
+__device__ __forceinline__ V2 ray_end(double px, double py, double ang, double c0, double s0, int i,
+                                      double& dx, double& dy) {
+  float fx, fy;
+  ray_end_f32(px, py, ang, c0, s0, i, c_ray_cs, dx, dy, fx, fy);
+  return V(fx, fy);
+}
+
 // rays (pi/8 apart, ray i along ang - i*pi/8) that can meet a circle (center r from the car, radius R)
 __device__ __forceinline__ unsigned ray_mask(float rx, float ry, float d, float R, float angf) {
   if (d <= R * 1.0001f + 0.01f) return 0xFFFFu;
@@ -863,14 +945,14 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(SENS
     const float4 ps = pass == 0 ? pa : pb;
     const V2 p1 = V(ps.x, ps.y);
     const double px = ps.x, py = ps.y, ang = ps.z;
+    double s0 = 0.0, c0 = 1.0;
+    if (active) sincos(ang, &s0, &c0);   // one f64 sincos per lane; the rays rotate it (ray_end)
 #pragma unroll
     for (int q = 0; q < RPL; ++q) {
       const int i = r * RPL + q;
       if (active) {
-        double sa = -((double)i * (360.0 / 16) * RAD_PER_DEG) + ang;
-        double dy, dx;
-        sincos(sa, &dy, &dx);
-        V2 p2 = OV(px + dx * 250.0, py + dy * 250.0);
+        double dx, dy;
+        const V2 p2 = ray_end(px, py, ang, c0, s0, i, dx, dy);
         s_p2[(lc * 16 + i) * 2] = p2.x; s_p2[(lc * 16 + i) * 2 + 1] = p2.y;
         s_dir[(lc * 16 + i) * 2] = (float)dx; s_dir[(lc * 16 + i) * 2 + 1] = (float)dy;
       }
@@ -998,7 +1080,10 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(SENS
 // The env step as two launches: model_kernel (actions -> Car.update_physics -> Box2D step, one lane
 // per car; its TOI code holds it at one wave per SIMD) hands the body / listener state to logic_kernel
 // (banking, disable logic, lap timer, rewards, termination, obs, auto-reset) through the state arrays.
-__global__ void __launch_bounds__(SBLOCK) model_kernel(Params P, const void* actions, int discrete, int want_term) {
+#ifndef MODEL_WPE
+#define MODEL_WPE 2   // 256 VGPRs + 40 spilled (vs 256 + 44 AGPRs at 1 wave/SIMD): 103.6 -> 100.6 us/step
+#endif
+__global__ void __launch_bounds__(SBLOCK) __attribute__((amdgpu_waves_per_eu(MODEL_WPE))) model_kernel(Params P, const void* actions, int discrete, int want_term) {
   const int tid = threadIdx.x, C = P.C;
   const int el = tid / C, car = tid - el * C;
   const int slot = blockIdx.x * P.epb + el;
@@ -1059,10 +1144,20 @@ __global__ void __launch_bounds__(SBLOCK) logic_kernel(Params P, float* obs, flo
   __shared__ double s_prefix[MAX_SEG];
   __shared__ float s_obs[SBLOCK * 22];
   __shared__ int s_rowbase[SBLOCK];
+  __shared__ float4 s_sg[MAX_SEG];
+  __shared__ float s_rll[MAX_SEG];
   TrackDev T = P.tracks[P.blk_track[blockIdx.x]];
-  if (tid < T.nseg) { s_segs[tid] = T.segs[tid]; s_prefix[tid] = T.prefix[tid]; }
+  if (tid < T.nseg) {
+    const DSeg sg = T.segs[tid];
+    s_segs[tid] = sg; s_prefix[tid] = T.prefix[tid];
+    const double dx = sg.ex - sg.sx, dy = sg.ey - sg.sy, ll = dx * dx + dy * dy;
+    s_sg[tid] = make_float4((float)sg.sx, (float)sg.sy, (float)dx, (float)dy);
+    s_rll[tid] = ll < 1e-6 ? 0.0f : (float)(1.0 / ll);
+  }
   __syncthreads();
   T.segs = s_segs; T.prefix = s_prefix;
+  const ChordScreen CS{s_sg, s_rll, T.nseg};
+  float cut = INFINITY;
   const int nw = T.nwall;
   const WallSet S{T.walls, nw, T.bp, T.sn};
   Car c;
@@ -1075,7 +1170,8 @@ __global__ void __launch_bounds__(SBLOCK) logic_kernel(Params P, float* obs, flo
     car_load_logic(P, n, c);
     LPROF(1);
     s_laps_old[tid] = c.lt_laps;   // the lap count does not change before lap_update
-    c.bank = T.has_banking ? banking_at(T, c.xf.p.x, c.xf.p.y) : 0.0;
+    cut = screen_cut(CS, c.xf.p.x, c.xf.p.y);   // the body position is final for this step
+    c.bank = T.has_banking ? banking_at_screened(T, CS, cut, c.xf.p.x, c.xf.p.y) : 0.0;
     if (!c.disabled) {   // _run_single_physics_step (src/car_env.py:582-638)
       double imp = c.imp_present ? c.imp : 0.0;
       if (imp > 50000.0) { c.disabled = 1; c.just_disabled = 1; }
@@ -1085,7 +1181,7 @@ __global__ void __launch_bounds__(SBLOCK) logic_kernel(Params P, float* obs, flo
       if (speed < 0.5) c.stuck_dur = c.stuck_dur + P.dt_d;
       else { c.stuck_dur = 0.0; c.has_stuck_start = 0; }
     }
-    lapdone = lap_update(T, c, c.xf.p.x, c.xf.p.y, sim);
+    lapdone = lap_update(T, CS, c, c.xf.p.x, c.xf.p.y, sim);
     s_laps_new[tid] = c.lt_laps; s_dis_new[tid] = c.disabled; s_lapdone[tid] = lapdone;
   }
   LPROF(2);
@@ -1145,7 +1241,7 @@ __global__ void __launch_bounds__(SBLOCK) logic_kernel(Params P, float* obs, flo
       r += PH(P2(dx) + P2(dy)) * 0.15;
       c.prev_px = px; c.prev_py = py;
       if (!c.first_step) {
-        double prog = track_progress(T, px, py);
+        double prog = track_progress_screened(T, CS, cut, px, py);
         double L = T.total_length, pd = prog - c.prog_hist;
         if (pd > L / 2) pd -= L; else if (pd < -L / 2) pd += L;
         if (pd < 0) {
@@ -1159,7 +1255,7 @@ __global__ void __launch_bounds__(SBLOCK) logic_kernel(Params P, float* obs, flo
         } else { c.back = 0.0; c.prev_back = 0.0; }
         c.prog_hist = prog;
       } else {
-        c.prog_hist = track_progress(T, px, py);
+        c.prog_hist = track_progress_screened(T, CS, cut, px, py);
         c.first_step = 0;
       }
       if (c.lt_laps > c.prev_laps) { r += 0.0 * (c.lt_laps - c.prev_laps); c.prev_laps = c.lt_laps; }
@@ -1227,7 +1323,9 @@ __global__ void __launch_bounds__(SBLOCK) logic_kernel(Params P, float* obs, flo
   s_rowbase[tid] = env >= 0 ? n * 38 : -1;
   __syncthreads();
   // obs[:, 0:22] rows of this workgroup, written 22 consecutive floats per row by consecutive lanes
-  for (int i = tid; i < SBLOCK * 22; i += SBLOCK) {
+#pragma unroll
+  for (int k = 0; k < 22; ++k) {   // unrolled: the 22 LDS reads are issued back to back
+    const int i = tid + k * SBLOCK;
     const int row = i / 22, col = i - row * 22;
     const int base = s_rowbase[row];
     if (base >= 0) obs[(size_t)base + col] = s_obs[i];

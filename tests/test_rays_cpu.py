@@ -1,0 +1,18 @@
+"""CPU check of the sensor kernel's ray end-point arithmetic (nascargymnasium_amd/csrc/nascar_rays.h):
+the header is compiled for the host with g++ and every ray's f32 end point is compared with the direct
+Python-float evaluation of src/distance_sensor.py:95-103 (glibc sincos of sa) on random car poses."""
+import os
+import subprocess
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_ray_end_points_match_direct_evaluation(tmp_path):
+    exe = tmp_path / "rays_harness"
+    subprocess.run(["g++", "-O2", "-ffp-contract=off", "-o", str(exe),
+                    os.path.join(ROOT, "tests", "native", "rays_harness.cpp")], check=True)
+    out = subprocess.run([str(exe), "300000"], capture_output=True, text=True, check=True).stdout.split()
+    cases, bad, fallbacks = map(int, out)
+    assert cases == 300000 * 16
+    assert bad == 0
+    assert fallbacks < cases // 1000   # the direct-sincos fallback is rare (exact-angle ties only)
