@@ -16,7 +16,9 @@
 
 #pragma clang fp contract(off)
 
+#ifndef BLOCK
 #define BLOCK 256   // threads per workgroup of the sensor kernel
+#endif
 #ifndef SBLOCK
 #define SBLOCK 128  // threads per workgroup of the one-lane-per-car kernels (whole envs)
 #endif

@@ -896,7 +896,6 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(SENS
   PROFS_RT(14);
   PROFS(0);
   __shared__ float s_p2[CPW * 32];          // [car][ray][x, y]: f32 ray end points (exact test)
-  __shared__ float s_dir[CPW * 32];         // [car][ray][x, y]: unit ray directions (cull only)
   __shared__ unsigned s_best[CPW * 16];     // [car][ray]: best fraction so far (float bits, >= 0)
   float4* swa = (float4*)smem;
   constexpr int SUB = (SBLOCK + CPW - 1) / CPW;   // sensor workgroups per step-kernel workgroup
@@ -915,7 +914,8 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(SENS
   const float4* __restrict__ swall = T.swall;
 #define SW_A(j) swall[2 * (j)]
 #define SW_B(j) swall[2 * (j) + 1]
-#define SW_G(g) T.groups[g]
+  for (int g = t; g < ng; g += BLOCK) swa[g] = T.groups[g];   // groups (2-4 KB) staged in LDS; the barrier below publishes them
+#define SW_G(g) swa[g]
 #else
   float4* swb = swa + nw;
   float4* sgr = swb + nw;
@@ -939,7 +939,6 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(SENS
   PROFS(1);
   unsigned* best = s_best + lc * 16;
   const float* p2s = s_p2 + lc * 32;
-  const float* dirs = s_dir + lc * 32;
   for (int pass = (passes & 1) ? 0 : 1; pass < ((passes & 2) ? 2 : 1); ++pass) {
     const bool active = env >= 0 && (pass == 0 ? (mode & (PM_A_OBS | PM_A_TERM)) != 0 : (mode & PM_B_OBS) != 0);
     const float4 ps = pass == 0 ? pa : pb;
@@ -954,7 +953,7 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(SENS
         double dx, dy;
         const V2 p2 = ray_end(px, py, ang, c0, s0, i, dx, dy);
         s_p2[(lc * 16 + i) * 2] = p2.x; s_p2[(lc * 16 + i) * 2 + 1] = p2.y;
-        s_dir[(lc * 16 + i) * 2] = (float)dx; s_dir[(lc * 16 + i) * 2 + 1] = (float)dy;
+        (void)dx; (void)dy;
       }
       s_best[lc * 16 + i] = __float_as_uint(2.0f);
     }
@@ -1006,9 +1005,9 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(SENS
         const int first = __float_as_int(G.w) & 0xFFFF, cnt = __float_as_int(G.w) >> 16;
         for (int j = first; j < first + cnt; ++j) {
           const float4 wa = SW_A(j);
+          const float4 wb = SW_B(j);
           const float rx = wa.x - p1.x, ry = wa.y - p1.y;
           const float R = wa.z;
-          const float4 wb = SW_B(j);
           Rot q; q.s = wb.x; q.c = wb.y;
           const V2 l1 = rmulT(q, V(p1.x - wa.x, p1.y - wa.y));
           const float hx = wa.w, hy = wb.z;
@@ -1024,7 +1023,10 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(SENS
             m &= m - 1u;
             const float bi = __uint_as_float(best[i]);
             CNT(c_wr);
-            const float dx = dirs[2 * i], dy = dirs[2 * i + 1];
+            // direction from the f32 end point (cull only: error ~1e-7 rad, far inside the guards);
+            // the end point is re-read by the exact cast below
+            const float px2 = p2s[2 * i], py2 = p2s[2 * i + 1];
+            const float dx = (px2 - p1.x) * 0.004f, dy = (py2 - p1.y) * 0.004f;
             const float tc = rx * dx + ry * dy, perp = fabsf(rx * dy - ry * dx);
             if (perp > R || tc < -R || (tc - R) > 250.0f * bi) continue;
             // separating axis along the ray normal: the box must straddle the ray line (+2 cm guard)
@@ -1566,7 +1568,7 @@ struct NascarHandle {
   float4* d_pose = nullptr;  // [2][N] step/reset -> sensor_kernel hand-off
   void* d_actor = nullptr;   // SAC actor weights (nascar_set_actor), one allocation
   ActorDev actor{};
-  size_t max_lds = 0, max_sensor_lds = 0;
+  size_t max_lds = 0, max_sensor_lds = 0, max_sensor_groups_lds = 0;
   bool dirty_tracks = true;
 };
 
@@ -1690,6 +1692,11 @@ extern "C" int nascar_add_track(NascarHandle* h, const double* segments, int32_t
     HIPCHK(hipMemcpy(t.d_swall, sw.data(), sizeof(float4) * sw.size(), hipMemcpyHostToDevice));
   }
   h->max_sensor_lds = std::max(h->max_sensor_lds, 2 * sizeof(float4) * t.walls.size() + sizeof(float4) * t.groups.size());
+  h->max_sensor_groups_lds = std::max(h->max_sensor_groups_lds, sizeof(float4) * t.groups.size());
+  if (getenv("NASCAR_VERBOSE"))
+    fprintf(stderr, "nascar_add_track: %d walls, %zu groups; broadphase grid %dx%d (%zu entries), sensor grid %dx%d "
+            "(%zu entries, mean %.1f per cell)\n", nwall, t.groups.size(), t.bp.g.nx, t.bp.g.ny, t.bp.idx.size(),
+            t.sn.g.nx, t.sn.g.ny, t.sn.idx.size(), (double)t.sn.idx.size() / ((double)t.sn.g.nx * t.sn.g.ny));
   h->tracks.push_back(t);
   h->max_lds = std::max(h->max_lds, lds);
   h->dirty_tracks = true;
@@ -1764,7 +1771,7 @@ static Params make_params(NascarHandle* h) {
 // poses pose[N + n] of auto-reset cars overwrite those cars' pass-A obs values: nascar_step)
 static void launch_sensors(NascarHandle* h, const Params& P, float* obs, float* terminal_obs, int passes, void* stream) {
 #ifdef SENSOR_GLOBAL_WALLS
-  const size_t lds = 0;
+  const size_t lds = h->max_sensor_groups_lds;
 #else
   const size_t lds = h->max_sensor_lds;
 #endif
