@@ -21,26 +21,46 @@ ALGO_BYTES_PER_CAR_STEP = 1221      # 2 x 528 B state + 8 B acti
 HBM_PEAK_GBS = 8000.0               # MI355X HBM3E spec (MI355X_MICROARCH.md)
 
 
-def cpu_baseline(track, cars, budget_s=12.0):
-    """The CPU oracle (C restatement of the reference path, 1 thread) on a bounded sample of the
-    same workload: 16 envs x C cars, uniform actions, as many steps as fit in ~budget_s."""
-    sys.path.insert(0, os.path.join(ROOT, "tests"))
+def _oracle_shard(track, cars, E, seed, budget_s, out, slot):
+    """One host thread: its own OracleEnv shard of E envs x C cars, uniform actions, ~budget_s of stepping
+    (the oracle's C step releases the GIL inside ctypes, so shards on threads run in parallel)."""
     import numpy as np
     from oracle_lib import OracleEnv
-    E = 16
     env = OracleEnv(track, E, cars)
     env.reset()
-    rng = np.random.default_rng(0)
-    acts = rng.uniform(-1, 1, (64, E, cars, 2)).astype(np.float32)
+    acts = np.random.default_rng(seed).uniform(-1, 1, (64, E, cars, 2)).astype(np.float32)
     steps, t0 = 0, time.perf_counter()
     while time.perf_counter() - t0 < budget_s:
         env.step(acts[steps % 64])
         steps += 1
-    dt = time.perf_counter() - t0
+    out[slot] = (E * cars * steps, time.perf_counter() - t0)
     env.close()
-    return {"value": E * cars * steps / dt, "unit": "car-steps/s", "cores": 1, "kind": "port",
-            "sample": f"oracle (C restatement of the reference path incl. Box2D subset), {E} envs x {cars} cars x "
-                      f"{steps} steps on {os.path.basename(track)}, uniform actions, 1 host thread"}
+
+
+def cpu_baseline(track, cars, budget_s=12.0, threads=None):
+    """The CPU oracle (C restatement of the reference path) on a bounded sample of the same workload:
+    16 envs x C cars per shard, uniform actions.  First 1 thread for budget_s / 2, then one shard per
+    host thread (threads = the box's CPU share, at most 16) for budget_s / 2 of wall time; `value` is the
+    multi-thread rate (car-steps over the slowest shard's time), the 1-thread rate is in `sample`."""
+    import threading
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    E = 16
+    if threads is None:
+        threads = max(1, min(16, len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()))
+    one = [None]
+    _oracle_shard(track, cars, E, 0, budget_s / 2, one, 0)
+    rate1 = one[0][0] / one[0][1]
+    res = [None] * threads
+    th = [threading.Thread(target=_oracle_shard, args=(track, cars, E, k, budget_s / 2, res, k)) for k in range(threads)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    rate = sum(r[0] for r in res) / max(r[1] for r in res)
+    return {"value": rate, "unit": "car-steps/s", "cores": threads, "kind": "port",
+            "sample": f"oracle (C restatement of the reference path incl. Box2D subset) on {os.path.basename(track)}, "
+                      f"uniform actions: {threads} host threads x one shard of {E} envs x {cars} cars, "
+                      f"~{budget_s / 2:.0f} s each; 1 thread alone: {rate1:.0f} car-steps/s"}
 
 
 def reduce_max(values, device):
@@ -71,6 +91,11 @@ def main():
     ap.add_argument("--policy", default="uniform", choices=["uniform", "driver", "sac"],
                     help="uniform: U[-1,1]^2 resident in HBM; driver: device rule driver; sac: fused SAC actor "
                          "(random-init weights of the reference architecture) on the previous observation")
+    ap.add_argument("--mixed", action="store_true", help="env e on track e mod 8 of the sorted bundled tracks "
+                    "(BASELINE cfg5: mixed batch, divergent geometry); --track is ignored")
+    ap.add_argument("--gather", action="store_true", help="gather every step's obs/reward/flags of all ranks to "
+                    "rank 0 (RCCL, side stream; BASELINE cfg4 single-learner layout)")
+    ap.add_argument("--cpu-threads", type=int, default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     args = ap.parse_args()
@@ -89,7 +114,16 @@ def main():
     dev = torch.device("cuda", local)
     E, C, K, W = args.envs, args.cars, args.steps, args.warmup
     tpath = track_path(args.track)
-    env = BatchedCarEnv(E, C, tpath, device=dev)
+    if args.mixed:
+        from nascargymnasium_amd.track import available_tracks
+        names = available_tracks()
+        env = BatchedCarEnv(E, C, [names[e % len(names)] for e in range(E)], device=dev)
+    else:
+        env = BatchedCarEnv(E, C, tpath, device=dev)
+    gather = None
+    if args.gather:
+        from nascargymnasium_amd.gather import ObsGather
+        gather = ObsGather(E, C, dev)
     if args.policy == "sac":
         from nascargymnasium_amd.policy import random_actor
         env.set_actor(random_actor(rank))
@@ -104,7 +138,9 @@ def main():
 
     def one_step(i):
         a = acts[i] if args.policy == "uniform" else env.policy_actions(pol, seed=rank, step=i)
-        env.step(a, auto_reset=True)
+        env.launch_step(a, auto_reset=True)
+        if gather is not None:
+            gather.push(env.obs, env.reward, env.car_flags, env.env_flags)
 
     for i in range(W):
         one_step(i)
@@ -116,10 +152,9 @@ def main():
     # time between kernels on this stack, which would be charged to the throughput)
     t0 = time.perf_counter()
     for i in range(W, W + K):
-        if args.policy == "uniform":
-            env.launch_step(acts[i], auto_reset=True)
-        else:
-            env.launch_step(env.policy_actions(pol, seed=rank, step=i), auto_reset=True)
+        one_step(i)
+    if gather is not None:
+        gather.wait()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -153,9 +188,10 @@ def main():
         "value": value, "unit": "car-steps/s", "n_gpus": world, "steps": K, "warmup": W,
         "ms_per_step": elapsed / K * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
         "dtype": "f32+f64", "data": "synthetic",
-        "config": {"workload": f"{os.path.basename(tpath)[:-6]} {C}-car: {E} envs x {C} cars per GPU, "
+        "config": {"workload": f"{'mixed 8-track' if args.mixed else os.path.basename(tpath)[:-6]} {C}-car: {E} envs x {C} cars per GPU, "
                                f"{ {'uniform': 'uniform U[-1,1]^2 actions resident in HBM', 'driver': 'on-device rule driver', 'sac': 'fused SAC actor (random-init) closed loop'}[args.policy]}, auto-reset",
-                   "envs_per_gpu": E, "cars_per_env": C, "track": os.path.basename(tpath), "parallelism": f"dp{world} (env shards, no collective)"},
+                   "envs_per_gpu": E, "cars_per_env": C, "track": "mixed (env e: track e mod 8)" if args.mixed else os.path.basename(tpath),
+                   "parallelism": f"dp{world} (env shards" + (", RCCL gather of obs/reward/flags to rank 0 per step)" if gather else ", no collective)")},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel": "model_kernel + logic_kernel + sensor_kernel (one env step)", "kernel_ms": kern_ms,
@@ -163,7 +199,7 @@ def main():
         "engine_errors": errs,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(tpath, C, args.cpu_budget)
+        out["cpu_baseline"] = cpu_baseline(tpath, C, args.cpu_budget, args.cpu_threads)
     if rank == 0:
         print(json.dumps(out), flush=True)
     env.close()

@@ -43,7 +43,7 @@ static const double CAR_MAX_TORQUE = 820.0;
 
 EXPORT double or_dbg[32];
 EXPORT int or_dbg_car = -1;
-static int g_cur_car = -2;
+static _Thread_local int g_cur_car = -2;   // debug tap selector (thread-local: bench runs oracle shards on threads)
 #define ODBG(slot, val) do { if (g_cur_car == or_dbg_car) or_dbg[slot] = (double)(val); } while (0)
 static inline double pymin(double a, double b) { return b < a ? b : a; }
 static inline double pymax(double a, double b) { return b > a ? b : a; }

@@ -51,3 +51,49 @@ def test_bench_reduction_world2():
         assert elapsed == 2.0 and kern == pytest.approx(0.5)
         assert value == pytest.approx(2 * 8192 * 10 * 200 / 2.0)
         assert distinct
+
+
+def _gather_worker(rank, world, port, q):
+    import torch
+    import torch.distributed as dist
+    sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from nascargymnasium_amd.gather import ObsGather
+    E, C = 3, 2
+    g = ObsGather(E, C, torch.device("cpu"))
+    got = []
+    for step in range(2):
+        obs = torch.full((E, C, 38), 100.0 * rank + step) + torch.arange(38.0)
+        rew = torch.full((E, C), -0.05 * (rank + 1) + step)
+        cf = torch.full((E, C), 4 * rank + step, dtype=torch.uint8)
+        ef = torch.tensor([rank, step, 8 + rank], dtype=torch.uint8)
+        g.push(obs, rew, cf, ef)
+        r = g.received()
+        if r is not None:
+            got.append({k: v.clone() for k, v in r.items()})
+    q.put((rank, got))
+    dist.destroy_process_group()
+
+
+def test_obs_gather_world2():
+    """ObsGather (the optional cfg4 gather of obs/reward/flags to rank 0) over gloo, world size 2."""
+    import torch
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_gather_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res[1] == []
+    for step, r in enumerate(res[0]):
+        assert r["obs"].shape == (2, 3, 2, 38)
+        for rank in range(2):
+            assert torch.equal(r["obs"][rank], torch.full((3, 2, 38), 100.0 * rank + step) + torch.arange(38.0))
+            assert torch.equal(r["reward"][rank], torch.full((3, 2), -0.05 * (rank + 1) + step))
+            assert torch.equal(r["car_flags"][rank], torch.full((3, 2), 4 * rank + step, dtype=torch.uint8))
+            assert r["env_flags"][rank].tolist() == [rank, step, 8 + rank]
