@@ -194,7 +194,7 @@ def main():
                    "parallelism": f"dp{world} (env shards" + (", RCCL gather of obs/reward/flags to rank 0 per step)" if gather else ", no collective)")},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": "model_kernel + logic_kernel + sensor_kernel (one env step)", "kernel_ms": kern_ms,
+                     "kernel": "model_kernel + logic_kernel + ray_sensor_kernel (one env step)", "kernel_ms": kern_ms,
                      "algo_bytes_per_car_step": ALGO_BYTES_PER_CAR_STEP},
         "engine_errors": errs,
     }

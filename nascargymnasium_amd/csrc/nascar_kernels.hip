@@ -15,6 +15,8 @@
 #include <string.h>
 
 #include <algorithm>
+#include <chrono>
+#include <thread>
 #include <cmath>
 #include <string>
 #include <unordered_map>
@@ -44,6 +46,19 @@ __device__ int g_dbg_car = -1;
 struct DSeg {   // per segment, float64 (src/track_generator.py TrackSegment)
   double sx, sy, ex, ey, width, banking, la, chord;  // la: banking lateral assist (src/car.py:527-533)
 };
+// Ray-candidate lists ("beams"), built on the host (build_beams): for every BEAM_CELL-sized cell near the
+// walls and every one of BEAM_NB direction bins, the walls that a ray starting anywhere in the cell with a
+// direction in the bin can reach within 250 m, sorted by a lower bound of their distance from the cell.
+// Entry = (lower bound in cm, floored) << 16 | wall index.  A ray walks its list and stops at the first
+// entry whose lower bound exceeds its best hit so far: the minimum exact fraction over the walls visited
+// is the minimum over all walls, i.e. the reference's Box2D RayCast result.
+#define BEAM_NB 128
+struct BeamGrid {
+  float ox, oy, inv_cell; int nx, ny;
+  const int* cell;          // [nx * ny]: first list of the cell (built cell id * BEAM_NB), -1: not built
+  const uint32_t* start;    // [built cells * BEAM_NB + 1]
+  const uint32_t* ent;
+};
 struct TrackDev {
   LWall* walls; int nwall;
   DSeg* segs; int nseg;
@@ -52,6 +67,7 @@ struct TrackDev {
   WallGrid bp, sn;
   const float4* groups; int ngroup;   // sensor wall groups: (cx, cy, radius incl. margin, first | count << 16)
   const float4* swall;                // [2 * nwall] sensor image: (px, py, rad + 0.25, hx), (qs, qc, hy, 0)
+  BeamGrid beam;                      // per (cell, direction bin) candidate walls of one ray (ray_sensor_kernel)
 };
 
 struct Params {
@@ -64,6 +80,8 @@ struct Params {
   const int* blk_track; const int* blk_env;
   const TrackDev* tracks;
   float4* pose;        // [2][N] sensor hand-off: (x, y, angle, mode) -- see sensor_kernel
+  double2* pose_cs;    // [2][N] cos, sin of (double)angle for the ray end points (computed once per car)
+  const double2* ray_cs;   // [16] cos, sin of the ray offsets radians(22.5 i) (nascar_rays.h)
 };
 
 #define F32P(P, f) ((P).f32 + (size_t)F32_##f * (P).N)
@@ -766,6 +784,13 @@ __device__ inline void car_obs(const Car& c, float* o) {
 __device__ __forceinline__ float4 car_pose(const Car& c, int mode) {
   return make_float4(c.xf.p.x, c.xf.p.y, c.a, __int_as_float(mode));
 }
+// pose hand-off slot k (n: pass A, N + n: pass B) with the f64 cos / sin of the angle the rays rotate
+__device__ __forceinline__ void set_pose(const Params& P, size_t k, const Car& c, int mode) {
+  P.pose[k] = car_pose(c, mode);
+  double s0, c0;
+  sincos((double)c.a, &s0, &c0);
+  P.pose_cs[k] = make_double2(c0, s0);
+}
 
 // ------------------------------------------------------------------ reset (src/car_env.py:316-535)
 __device__ inline void car_reset(const Params& P, Car& c, int n, bool fresh, const WallSet& S, const TrackDev& T) {
@@ -827,12 +852,14 @@ __device__ __forceinline__ float sensor_value(float best) {   // DistanceSensor 
 }
 
 // ray offsets of DistanceSensor (nascar_rays.h)
-__constant__ double c_ray_cs[16][2] = NASCAR_RAY_CS_INIT;
-
-__device__ __forceinline__ V2 ray_end(double px, double py, double ang, double c0, double s0, int i,
+// The table lives in a device buffer (Params::ray_cs, filled at nascar_create) and is read with one
+// indexed load: as a __constant__ array hipcc materialised all 32 values in registers per lane,
+// selected by the (lane-varying) ray index, and spilled them.
+static const double h_ray_cs[16][2] = NASCAR_RAY_CS_INIT;
+__device__ __forceinline__ V2 ray_end(const Params& P, double px, double py, double ang, double c0, double s0, int i,
                                       double& dx, double& dy) {
   float fx, fy;
-  ray_end_f32(px, py, ang, c0, s0, i, c_ray_cs, dx, dy, fx, fy);
+  ray_end_f32(px, py, ang, c0, s0, i, (const double (*)[2])P.ray_cs, dx, dy, fx, fy);
   return V(fx, fy);
 }
 
@@ -945,13 +972,13 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(SENS
     const V2 p1 = V(ps.x, ps.y);
     const double px = ps.x, py = ps.y, ang = ps.z;
     double s0 = 0.0, c0 = 1.0;
-    if (active) sincos(ang, &s0, &c0);   // one f64 sincos per lane; the rays rotate it (ray_end)
+    if (active) { const double2 cs = P.pose_cs[pass == 0 ? (size_t)n : (size_t)P.N + n]; c0 = cs.x; s0 = cs.y; }
 #pragma unroll
     for (int q = 0; q < RPL; ++q) {
       const int i = r * RPL + q;
       if (active) {
         double dx, dy;
-        const V2 p2 = ray_end(px, py, ang, c0, s0, i, dx, dy);
+        const V2 p2 = ray_end(P, px, py, ang, c0, s0, i, dx, dy);
         s_p2[(lc * 16 + i) * 2] = p2.x; s_p2[(lc * 16 + i) * 2 + 1] = p2.y;
         (void)dx; (void)dy;
       }
@@ -1079,6 +1106,161 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(SENS
 #undef SW_G
 }
 
+// ------------------------------------------------------------------ ray_sensor_kernel: one lane per ray
+// b2PolygonShape::RayCast of one wall box for the ray p1 -> p2 (the arithmetic of sensor_kernel's inner
+// loop: same culls, same face order and f32 operations); returns min(bi, hit fraction).
+// (dx, dy): the ray direction, cull only.
+__device__ __forceinline__ float wall_cast(const float4 wa, const float4 wb, V2 p1, float p2x, float p2y, float dx,
+                                           float dy, float bi) {
+  const float rx = wa.x - p1.x, ry = wa.y - p1.y;
+  const float R = wa.z;
+  const float tc = rx * dx + ry * dy, perp = fabsf(rx * dy - ry * dx);
+  if (perp > R || tc < -R || (tc - R) > 250.0f * bi) return bi;
+  Rot q; q.s = wb.x; q.c = wb.y;
+  const float hx = wa.w, hy = wb.z;
+  if (perp > hx * fabsf(q.c * dy - q.s * dx) + hy * fabsf(q.s * dy + q.c * dx) + 0.02f) return bi;
+  const V2 l1 = rmulT(q, V(p1.x - wa.x, p1.y - wa.y));
+  const float n0 = 0.0f * ((-hx) - l1.x) + (-1.0f) * ((-hy) - l1.y);
+  const float n1 = 1.0f * (hx - l1.x) + 0.0f * ((-hy) - l1.y);
+  const float n2 = 0.0f * (hx - l1.x) + 1.0f * (hy - l1.y);
+  const float n3 = (-1.0f) * ((-hx) - l1.x) + 0.0f * (hy - l1.y);
+  const V2 l2 = rmulT(q, V(p2x - wa.x, p2y - wa.y));
+  const V2 dd = vsub(l2, l1);
+  float lower = 0.0f, upper = 1.0f; int index = -1; bool ok = true;
+  const float num[4] = {n0, n1, n2, n3};
+  const float den[4] = {0.0f * dd.x + (-1.0f) * dd.y, 1.0f * dd.x + 0.0f * dd.y, 0.0f * dd.x + 1.0f * dd.y,
+                        (-1.0f) * dd.x + 0.0f * dd.y};
+#pragma unroll
+  for (int f = 0; f < 4; ++f) {
+    if (!ok) break;
+    if (den[f] == 0.0f) { if (num[f] < 0.0f) ok = false; }
+    else if (den[f] < 0.0f && num[f] < lower * den[f]) { lower = fdiv_cr(num[f], den[f]); index = f; }
+    else if (den[f] > 0.0f && num[f] < upper * den[f]) { upper = fdiv_cr(num[f], den[f]); }
+    if (upper < lower) ok = false;
+  }
+  return (ok && index >= 0 && lower < bi) ? lower : bi;
+}
+
+// One ray without a beam list (car outside the cells build_beams covers): the sensor grid's wall groups
+// of the car's cell (all groups outside the grid), culled by range, by whether this ray is in the
+// group's angular mask and by the best hit so far, then wall_cast per wall.
+__device__ inline float ray_fallback(const TrackDev& T, V2 p1, float p2x, float p2y, float dx, float dy,
+                                           float angf, int i) {
+  int beg = 0, end = T.ngroup;
+  const uint16_t* list = nullptr;
+  if (grid_list(T.sn, p1.x, p1.y, beg, end)) list = T.sn.idx;
+  else { beg = 0; end = T.ngroup; }
+  const float4* __restrict__ sw = T.swall;
+  float bi = 2.0f;
+  for (int kk = beg; kk < end; ++kk) {
+    const float4 G = T.groups[list ? (int)list[kk] : kk];
+    const float grx = G.x - p1.x, gry = G.y - p1.y;
+    const float d2 = grx * grx + gry * gry;
+    if (d2 > (250.0f + G.z) * (250.0f + G.z)) continue;
+    const float d = __builtin_amdgcn_sqrtf(d2);
+    unsigned mask;
+    float dlo;
+    if (G.z > 24.0f) {
+      const int j = __float_as_int(G.w) & 0xFFFF;
+      const float4 wa = sw[2 * j], wb = sw[2 * j + 1];
+      const float ex = wa.w * wb.y, ey = wa.w * wb.x;
+      const float cx = wa.x - p1.x, cy = wa.y - p1.y;
+      float dseg;
+      mask = seg_ray_mask(cx - ex, cy - ey, cx + ex, cy + ey, wb.z * 1.4143f + 0.3f, angf, dseg);
+      dlo = (dseg - (wb.z * 1.4143f + 0.3f)) * (1.0f / 250.0f) - 1e-4f;
+    } else {
+      mask = ray_mask(grx, gry, d, G.z, angf);
+      dlo = (d - G.z) * (1.0f / 250.0f) - 1e-4f;
+    }
+    if (!((mask >> i) & 1u) || dlo > bi) continue;
+    const int first = __float_as_int(G.w) & 0xFFFF, cnt = __float_as_int(G.w) >> 16;
+    for (int j = first; j < first + cnt; ++j) bi = wall_cast(sw[2 * j], sw[2 * j + 1], p1, p2x, p2y, dx, dy, bi);
+  }
+  return bi;
+}
+
+// DistanceSensor.get_sensor_distances (src/distance_sensor.py:71-117) with one lane per ray: 16 lanes per
+// car, BLOCK / 16 cars per workgroup.  The lane walks its beam list (BeamGrid), so no lane waits for the
+// others and there is no LDS or barrier.  Passes and modes as sensor_kernel (pose[n]: pass A, pose[N + n]:
+// pass B for auto-reset cars).
+#ifndef RSENSOR_WPE
+#define RSENSOR_WPE 6   // 4 lanes per car at 6 waves/SIMD: 41.5 us (8 lanes 53.7, 2 lanes 44.3; 16 lanes 62.4)
+#endif
+#ifndef RAY_LPC
+#define RAY_LPC 4     // lanes per car; each lane walks the lists of 16 / RAY_LPC rays
+#endif
+__global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(RSENSOR_WPE)))
+ray_sensor_kernel(Params P, float* obs, float* terminal_obs, int passes) {
+  constexpr int CPW = BLOCK / RAY_LPC, RPL = 16 / RAY_LPC;
+  constexpr int SUB = (SBLOCK + CPW - 1) / CPW;   // sensor workgroups per step-kernel workgroup
+  const int b = blockIdx.x / SUB, sub = blockIdx.x - b * SUB;
+  const int t = threadIdx.x, lc = t / RAY_LPC, r = t - lc * RAY_LPC;
+  const int C = P.C;
+  const int slot = sub * CPW + lc;
+  const int el = slot / C, car = slot - el * C;
+  const int env = (el < P.epb) ? P.blk_env[b * P.epb + el] : -1;
+  if (env < 0) return;
+  const int n = env * C + car;
+  const TrackDev& T = P.tracks[P.blk_track[b]];
+  int mode = 0;
+  float4 pa = make_float4(0.f, 0.f, 0.f, 0.f), pb = pa;
+  if (passes & 1) { pa = P.pose[n]; mode = __float_as_int(pa.w) & (PM_A_OBS | PM_A_TERM); }
+  if (passes & 2) { pb = P.pose[P.N + n]; mode |= __float_as_int(pb.w) & PM_B_OBS; }
+  const BeamGrid G = T.beam;
+  const float4* __restrict__ sw = T.swall;
+#pragma unroll 1
+  for (int pass = 0; pass < 2; ++pass) {
+    const bool active = pass == 0 ? (mode & (PM_A_OBS | PM_A_TERM)) != 0 : (mode & PM_B_OBS) != 0;
+    if (!active) continue;
+    const float4 ps = pass == 0 ? pa : pb;
+    const V2 p1 = V(ps.x, ps.y);
+    const double px = ps.x, py = ps.y, ang = ps.z;
+    const double2 cs = P.pose_cs[pass == 0 ? (size_t)n : (size_t)P.N + n];
+    int base = -1;
+    const float fx = (p1.x - G.ox) * G.inv_cell, fy = (p1.y - G.oy) * G.inv_cell;
+    if (fx >= 0.0f && fy >= 0.0f && fx < (float)G.nx && fy < (float)G.ny) base = G.cell[(int)fy * G.nx + (int)fx];
+#ifndef RAY_UNROLL
+#define RAY_UNROLL 1
+#endif
+#pragma unroll RAY_UNROLL
+    for (int q = 0; q < RPL; ++q) {
+      const int i = r + RAY_LPC * q;
+      double dxd, dyd;
+      const V2 p2 = ray_end(P, px, py, ang, cs.x, cs.y, i, dxd, dyd);
+      const float dx = (p2.x - p1.x) * 0.004f, dy = (p2.y - p1.y) * 0.004f;   // cull only
+      float bi = 2.0f;
+      if (base >= 0) {
+        // direction bin of sa = -radians(22.5 i) + ang (f64; the lists carry a 2e-3 rad guard)
+        const double sa = -((double)i * (360.0 / 16) * RAD_PER_DEG) + ang;
+        double u = sa * (BEAM_NB / (2.0 * PI_D));
+        u -= BEAM_NB * floor(u * (1.0 / BEAM_NB));
+        const int bin = min(BEAM_NB - 1, max(0, (int)u));
+        const int sl = ((bin & 7) << 4) | (bin >> 3);   // a car's 16 rays (bins 8 apart) read 16 adjacent lists
+        const uint32_t s0 = G.start[base + sl], e0 = G.start[base + sl + 1];
+        PCOUNT(11, e0 - s0);
+        for (uint32_t k = s0; k < e0; ++k) {
+          const uint32_t v = G.ent[k];
+          if ((float)(v >> 16) * 0.01f > bi * 250.0f * 1.00001f + 0.01f) break;   // lower bound beyond the best hit
+          const int j = (int)(v & 0xFFFFu);
+          PCOUNT(10, 1);
+          bi = wall_cast(sw[2 * j], sw[2 * j + 1], p1, p2.x, p2.y, dx, dy, bi);
+        }
+      } else {
+        PCOUNT(9, 1);
+        bi = ray_fallback(T, p1, p2.x, p2.y, dx, dy, ps.z, i);
+      }
+      PCOUNT(8, 1);
+      const float val = sensor_value(bi);
+      if (pass == 0) {
+        if (mode & PM_A_OBS) obs[(size_t)n * 38 + 22 + i] = val;
+        if (mode & PM_A_TERM) terminal_obs[(size_t)n * 38 + 22 + i] = val;
+      } else {
+        obs[(size_t)n * 38 + 22 + i] = val;
+      }
+    }
+  }
+}
+
 // The env step as two launches: model_kernel (actions -> Car.update_physics -> Box2D step, one lane
 // per car; its TOI code holds it at one wave per SIMD) hands the body / listener state to logic_kernel
 // (banking, disable logic, lap timer, rewards, termination, obs, auto-reset) through the state arrays.
@@ -1126,7 +1308,7 @@ __global__ void __launch_bounds__(SBLOCK) __attribute__((amdgpu_waves_per_eu(MOD
   b2_step(c, S, P.dt_f, P.friction);
   PROF(4);
   car_store_body(P, n, c);
-  P.pose[n] = car_pose(c, PM_A_OBS | (want_term ? PM_A_TERM : 0));   // sensor pass A
+  set_pose(P, n, c, PM_A_OBS | (want_term ? PM_A_TERM : 0));   // sensor pass A
   PROF(5);
   PROF_RT(15);
 }
@@ -1308,7 +1490,7 @@ __global__ void __launch_bounds__(SBLOCK) logic_kernel(Params P, float* obs, flo
     if (reset_now) {
       car_reset(P, c, n, false, S, T);
       car_obs(c, o);
-      P.pose[P.N + n] = car_pose(c, PM_B_OBS);
+      set_pose(P, (size_t)P.N + n, c, PM_B_OBS);
     } else {
       P.pose[P.N + n] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
@@ -1352,7 +1534,7 @@ __global__ void __launch_bounds__(SBLOCK) reset_kernel(Params P, const uint8_t* 
     float o[22];
     car_obs(c, o);
     for (int i = 0; i < 22; ++i) obs[(size_t)n * 38 + i] = o[i];
-    P.pose[n] = car_pose(c, PM_A_OBS);
+    set_pose(P, n, c, PM_A_OBS);
     car_store(P, n, c);
   }
   __syncthreads();   // every lane of an env has read E_CREATED before its car 0 writes it
@@ -1454,6 +1636,12 @@ struct HostTrack {
   double total_length; int startline, has_banking;
   LWall* d_walls = nullptr; DSeg* d_segs = nullptr; double* d_prefix = nullptr;
   HostGrid bp, sn;
+  struct {
+    BeamGrid g{};
+    std::vector<int> cell; std::vector<uint32_t> start, ent;
+    int* d_cell = nullptr; uint32_t* d_start = nullptr; uint32_t* d_ent = nullptr;
+    double build_s = 0.0;
+  } beam;
   std::vector<float4> groups; float4* d_groups = nullptr;
   float4* d_swall = nullptr;
 };
@@ -1546,6 +1734,122 @@ static void build_grids(HostTrack& t) {
     }
   t.sn.start.back() = (int)t.sn.idx.size();
 }
+// Beam lists (BeamGrid).  Cells of BEAM_CELL m over the walls' extent; a cell gets lists when its centre is
+// within (largest half width + BEAM_BAND) of a wall centre line -- the corridor and a band outside each wall.
+// Per cell (centre c, disk radius rc = half diagonal + 5 cm) and wall j (centre line AB, capsule radius
+// rr = half thickness + 10 cm, which holds the box and the f32 rounding of the device's ray cast):
+//  * lb = dist(c, AB) - rr - rc bounds the distance from any ray origin in the cell to any point of the box;
+//    walls with lb > 251 m are out of the 250 m ray's reach;
+//  * the directions from the disk to the capsule lie in the arc between the directions from c to A and to
+//    B, widened by asin((rr + rc) / dist(c, AB)) (all bins when c is inside the grown capsule), plus a
+//    2e-3 rad guard for the f32 ray end points; every bin that arc touches lists the wall.
+// Both are conservative, so the walk in ray_sensor_kernel visits every wall that can be the first hit.
+static const float BEAM_CELL = 4.0f;
+static const double BEAM_BAND = 8.0;
+static void build_beams(HostTrack& t) {
+  auto t0 = std::chrono::steady_clock::now();
+  auto& B = t.beam;
+  const int nw = (int)t.walls.size();
+  std::vector<double> ax(nw), ay(nw), bx(nw), by(nw), rr(nw);
+  double lx = 1e30, ly = 1e30, ux = -1e30, uy = -1e30, hwmax = 0.0;
+  for (int j = 0; j < nw; ++j) {
+    const LWall& w = t.walls[j];
+    const double ex = (double)w.hx * w.qc, ey = (double)w.hx * w.qs;
+    ax[j] = w.px - ex; ay[j] = w.py - ey; bx[j] = w.px + ex; by[j] = w.py + ey;
+    rr[j] = (double)w.hy + 0.1;
+    lx = std::min({lx, ax[j], bx[j]}); ux = std::max({ux, ax[j], bx[j]});
+    ly = std::min({ly, ay[j], by[j]}); uy = std::max({uy, ay[j], by[j]});
+  }
+  for (auto& s : t.segs) hwmax = std::max(hwmax, s.width / 2.0);
+  const double D = hwmax + BEAM_BAND, pad = D + 2.0 * BEAM_CELL;
+  B.g.ox = (float)(lx - pad); B.g.oy = (float)(ly - pad); B.g.inv_cell = 1.0f / BEAM_CELL;
+  B.g.nx = (int)std::ceil((ux + pad - B.g.ox) / BEAM_CELL) + 1;
+  B.g.ny = (int)std::ceil((uy + pad - B.g.oy) / BEAM_CELL) + 1;
+  const int nx = B.g.nx, ny = B.g.ny;
+  auto segdist = [&](int j, double x, double y) {
+    const double sx = bx[j] - ax[j], sy = by[j] - ay[j], ll = sx * sx + sy * sy;
+    double tt = ll > 0 ? ((x - ax[j]) * sx + (y - ay[j]) * sy) / ll : 0.0;
+    tt = std::min(1.0, std::max(0.0, tt));
+    return std::hypot(x - (ax[j] + tt * sx), y - (ay[j] + tt * sy));
+  };
+  auto centre = [&](int cx, int cy, double& x, double& y) {
+    x = (double)B.g.ox + (cx + 0.5) * (double)BEAM_CELL; y = (double)B.g.oy + (cy + 0.5) * (double)BEAM_CELL;
+  };
+  // cells near a wall
+  std::vector<uint8_t> mark((size_t)nx * ny, 0);
+  for (int j = 0; j < nw; ++j) {
+    const int x0 = std::max(0, (int)std::floor((std::min(ax[j], bx[j]) - D - B.g.ox) / BEAM_CELL) - 1);
+    const int x1 = std::min(nx - 1, (int)std::floor((std::max(ax[j], bx[j]) + D - B.g.ox) / BEAM_CELL) + 1);
+    const int y0 = std::max(0, (int)std::floor((std::min(ay[j], by[j]) - D - B.g.oy) / BEAM_CELL) - 1);
+    const int y1 = std::min(ny - 1, (int)std::floor((std::max(ay[j], by[j]) + D - B.g.oy) / BEAM_CELL) + 1);
+    for (int cy = y0; cy <= y1; ++cy)
+      for (int cx = x0; cx <= x1; ++cx) {
+        double x, y;
+        centre(cx, cy, x, y);
+        if (segdist(j, x, y) <= D) mark[(size_t)cy * nx + cx] = 1;
+      }
+  }
+  B.cell.assign((size_t)nx * ny, -1);
+  std::vector<int> cells;
+  for (size_t k = 0; k < mark.size(); ++k)
+    if (mark[k]) { B.cell[k] = (int)cells.size() * BEAM_NB; cells.push_back((int)k); }
+  const int ncell = (int)cells.size();
+  const double rc = BEAM_CELL * 0.70710678 + 0.05, two_pi = 2.0 * M_PI, dbin = two_pi / BEAM_NB;
+  std::vector<std::vector<uint32_t>> lists((size_t)ncell * BEAM_NB);
+  auto work = [&](int c0, int c1) {
+    for (int ci = c0; ci < c1; ++ci) {
+      double x, y;
+      centre(cells[ci] % nx, cells[ci] / nx, x, y);
+      std::vector<uint32_t>* L = &lists[(size_t)ci * BEAM_NB];
+      for (int j = 0; j < nw; ++j) {
+        const double d = segdist(j, x, y), R = rr[j] + rc, lb = d - R;
+        if (lb > 251.0) continue;
+        const uint32_t q = (uint32_t)std::min(65535.0, std::floor(std::max(lb, 0.0) * 100.0));
+        const uint32_t e = (q << 16) | (uint32_t)j;
+        if (d <= R * 1.0001 + 1e-3) { for (int k = 0; k < BEAM_NB; ++k) L[k].push_back(e); continue; }
+        const double aA = std::atan2(ay[j] - y, ax[j] - x), aB = std::atan2(by[j] - y, bx[j] - x);
+        double dl = aB - aA;
+        while (dl > M_PI) dl -= two_pi;
+        while (dl <= -M_PI) dl += two_pi;
+        const double a0 = dl >= 0 ? aA : aB, span = std::fabs(dl);
+        const double wid = std::asin(std::min(1.0, R / d)) + 2e-3;
+        const long k0 = (long)std::floor((a0 - wid) / dbin), k1 = (long)std::floor((a0 + span + wid) / dbin);
+        if (k1 - k0 + 1 >= BEAM_NB) { for (int k = 0; k < BEAM_NB; ++k) L[k].push_back(e); continue; }
+        for (long k = k0; k <= k1; ++k) L[((k % BEAM_NB) + BEAM_NB) % BEAM_NB].push_back(e);
+      }
+      for (int k = 0; k < BEAM_NB; ++k) std::sort(L[k].begin(), L[k].end());
+    }
+  };
+  const int nth = std::max(1, std::min(16, (int)std::thread::hardware_concurrency()));
+  std::vector<std::thread> th;
+  for (int k = 0; k < nth; ++k) th.emplace_back(work, (int)((long)ncell * k / nth), (int)((long)ncell * (k + 1) / nth));
+  for (auto& x : th) x.join();
+  B.start.assign((size_t)ncell * BEAM_NB + 1, 0);
+  B.ent.clear();
+  // lists stored per cell in slot order, slot = (bin % 8) * 16 + bin / 8: the 16 rays of a car (pi/8 = 8 bins
+  // apart) read 16 adjacent lists
+  for (int ci = 0; ci < ncell; ++ci)
+    for (int slot = 0; slot < BEAM_NB; ++slot) {
+      const int bin = ((slot & 15) << 3) | (slot >> 4);
+      const auto& L = lists[(size_t)ci * BEAM_NB + bin];
+      B.start[(size_t)ci * BEAM_NB + slot] = (uint32_t)B.ent.size();
+      B.ent.insert(B.ent.end(), L.begin(), L.end());
+    }
+  B.start.back() = (uint32_t)B.ent.size();
+  B.build_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+}
+static int upload_beams(HostTrack& t) {
+  auto& B = t.beam;
+  HIPCHK(hipMalloc(&B.d_cell, sizeof(int) * B.cell.size()));
+  HIPCHK(hipMemcpy(B.d_cell, B.cell.data(), sizeof(int) * B.cell.size(), hipMemcpyHostToDevice));
+  HIPCHK(hipMalloc(&B.d_start, sizeof(uint32_t) * B.start.size()));
+  HIPCHK(hipMemcpy(B.d_start, B.start.data(), sizeof(uint32_t) * B.start.size(), hipMemcpyHostToDevice));
+  HIPCHK(hipMalloc(&B.d_ent, sizeof(uint32_t) * std::max<size_t>(B.ent.size(), 1)));
+  if (!B.ent.empty()) HIPCHK(hipMemcpy(B.d_ent, B.ent.data(), sizeof(uint32_t) * B.ent.size(), hipMemcpyHostToDevice));
+  B.g.cell = B.d_cell; B.g.start = B.d_start; B.g.ent = B.d_ent;
+  return 0;
+}
+
 static int upload_grid(HostGrid& G) {
   HIPCHK(hipMalloc(&G.d_start, sizeof(int) * G.start.size()));
   HIPCHK(hipMemcpy(G.d_start, G.start.data(), sizeof(int) * G.start.size(), hipMemcpyHostToDevice));
@@ -1566,6 +1870,8 @@ struct NascarHandle {
   std::vector<int> env_track;
   double* d_ctl = nullptr;   // rule-driver state for nascar_policy_actions
   float4* d_pose = nullptr;  // [2][N] step/reset -> sensor_kernel hand-off
+  double2* d_pose_cs = nullptr;
+  double2* d_ray_cs = nullptr;
   void* d_actor = nullptr;   // SAC actor weights (nascar_set_actor), one allocation
   ActorDev actor{};
   size_t max_lds = 0, max_sensor_lds = 0, max_sensor_groups_lds = 0;
@@ -1602,6 +1908,10 @@ extern "C" int nascar_create(const NascarConfig* cfg, NascarHandle** out) {
   hipMalloc(&h->d_ctl, sizeof(double) * 4 * N);
   if (hipMalloc(&h->d_pose, sizeof(float4) * 2 * N) != hipSuccess) { hipFree(h->arena); hipFree(h->d_ctl); delete h; return fail("hipMalloc(pose) failed"); }
   hipMemset(h->d_pose, 0, sizeof(float4) * 2 * N);
+  if (hipMalloc(&h->d_pose_cs, sizeof(double2) * 2 * N) != hipSuccess) { hipFree(h->arena); hipFree(h->d_ctl); hipFree(h->d_pose); delete h; return fail("hipMalloc(pose_cs) failed"); }
+  hipMemset(h->d_pose_cs, 0, sizeof(double2) * 2 * N);
+  HIPCHK(hipMalloc(&h->d_ray_cs, sizeof(h_ray_cs)));
+  HIPCHK(hipMemcpy(h->d_ray_cs, h_ray_cs, sizeof(h_ray_cs), hipMemcpyHostToDevice));
   hipMemset(h->d_ctl, 0, sizeof(double) * 4 * N);
   h->env_track.assign(E, 0);
   *out = h;
@@ -1610,10 +1920,11 @@ extern "C" int nascar_create(const NascarConfig* cfg, NascarHandle** out) {
 
 extern "C" void nascar_destroy(NascarHandle* h) {
   if (!h) return;
-  hipFree(h->arena); hipFree(h->d_ctl); hipFree(h->d_pose); hipFree(h->d_actor);
+  hipFree(h->arena); hipFree(h->d_ctl); hipFree(h->d_pose); hipFree(h->d_pose_cs); hipFree(h->d_ray_cs); hipFree(h->d_actor);
   for (auto& t : h->tracks) {
     hipFree(t.d_walls); hipFree(t.d_segs); hipFree(t.d_prefix);
     hipFree(t.bp.d_start); hipFree(t.bp.d_idx); hipFree(t.sn.d_start); hipFree(t.sn.d_idx); hipFree(t.d_groups); hipFree(t.d_swall);
+    hipFree(t.beam.d_cell); hipFree(t.beam.d_start); hipFree(t.beam.d_ent);
   }
   hipFree(h->d_tracks); hipFree(h->d_blk_track); hipFree(h->d_blk_env);
   delete h;
@@ -1679,6 +1990,8 @@ extern "C" int nascar_add_track(NascarHandle* h, const double* segments, int32_t
   if (nwall > 65535) return fail("track has %d walls (grid indices are 16-bit)", nwall);
   build_grids(t);
   if (upload_grid(t.bp) < 0 || upload_grid(t.sn) < 0) return -1;
+  build_beams(t);
+  if (upload_beams(t) < 0) return -1;
   HIPCHK(hipMalloc(&t.d_groups, sizeof(float4) * t.groups.size()));
   HIPCHK(hipMemcpy(t.d_groups, t.groups.data(), sizeof(float4) * t.groups.size(), hipMemcpyHostToDevice));
   {   // the sensor kernel's wall image (same f32 values it would stage: rad + 0.25 rounded once)
@@ -1697,6 +2010,13 @@ extern "C" int nascar_add_track(NascarHandle* h, const double* segments, int32_t
     fprintf(stderr, "nascar_add_track: %d walls, %zu groups; broadphase grid %dx%d (%zu entries), sensor grid %dx%d "
             "(%zu entries, mean %.1f per cell)\n", nwall, t.groups.size(), t.bp.g.nx, t.bp.g.ny, t.bp.idx.size(),
             t.sn.g.nx, t.sn.g.ny, t.sn.idx.size(), (double)t.sn.idx.size() / ((double)t.sn.g.nx * t.sn.g.ny));
+  if (getenv("NASCAR_VERBOSE"))
+    fprintf(stderr, "nascar_add_track: beam grid %dx%d, %zu cells with lists, %zu entries (mean %.2f per list), "
+            "%.1f MB, built in %.2f s\n", t.beam.g.nx, t.beam.g.ny, (t.beam.start.size() - 1) / BEAM_NB, t.beam.ent.size(),
+            (double)t.beam.ent.size() / std::max<size_t>(1, t.beam.start.size() - 1),
+            (4.0 * (t.beam.ent.size() + t.beam.start.size() + t.beam.cell.size())) / 1e6, t.beam.build_s);
+  t.beam.cell.clear(); t.beam.start.clear(); t.beam.ent.clear();   // the device copies are all the kernels use
+  t.beam.cell.shrink_to_fit(); t.beam.start.shrink_to_fit(); t.beam.ent.shrink_to_fit();
   h->tracks.push_back(t);
   h->max_lds = std::max(h->max_lds, lds);
   h->dirty_tracks = true;
@@ -1727,6 +2047,7 @@ static int prepare(NascarHandle* h) {
     d.walls = t.d_walls; d.nwall = (int)t.walls.size(); d.segs = t.d_segs; d.nseg = (int)t.segs.size();
     d.prefix = t.d_prefix; d.total_length = t.total_length; d.startline = t.startline; d.has_banking = t.has_banking;
     d.bp = t.bp.g; d.sn = t.sn.g; d.groups = t.d_groups; d.ngroup = (int)t.groups.size(); d.swall = t.d_swall;
+    d.beam = t.beam.g;
     td.push_back(d);
   }
   hipFree(h->d_tracks);
@@ -1763,13 +2084,26 @@ static Params make_params(NascarHandle* h) {
   P.acc = (double*)(a + h->off_acc); P.ct = (DContact*)(a + h->off_ct); P.act_key = (int*)(a + h->off_key);
   P.act_n = (float*)(a + h->off_n); P.env_time = (double*)(a + h->off_time); P.env_i32 = (int*)(a + h->off_ei32);
   P.blk_track = h->d_blk_track; P.blk_env = h->d_blk_env; P.tracks = h->d_tracks;
-  P.pose = h->d_pose;
+  P.pose = h->d_pose; P.pose_cs = h->d_pose_cs; P.ray_cs = h->d_ray_cs;
   return P;
 }
 
 // passes: 1 = pass A only (pose[n] with its A-mode bits: nascar_reset), 3 = pass A then pass B (the reset
 // poses pose[N + n] of auto-reset cars overwrite those cars' pass-A obs values: nascar_step)
+// NASCAR_SENSOR=groups selects the wall-group sensor kernel (A/B and cross-checks); default: beam lists
+static int sensor_impl() {
+  static int m = -1;
+  if (m < 0) { const char* e = getenv("NASCAR_SENSOR"); m = (e && !strcmp(e, "groups")) ? 0 : 1; }
+  return m;
+}
 static void launch_sensors(NascarHandle* h, const Params& P, float* obs, float* terminal_obs, int passes, void* stream) {
+  if (sensor_impl() == 1) {
+    constexpr int CPW = BLOCK / RAY_LPC;
+    const int sub = (SBLOCK + CPW - 1) / CPW;
+    hipLaunchKernelGGL(ray_sensor_kernel, dim3(h->nblocks * sub), dim3(BLOCK), 0, (hipStream_t)stream, P, obs,
+                       terminal_obs, passes);
+    return;
+  }
 #ifdef SENSOR_GLOBAL_WALLS
   const size_t lds = h->max_sensor_groups_lds;
 #else

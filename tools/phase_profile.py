@@ -117,6 +117,10 @@ def main():
             extra = (f"\n  per active lane: groups visited {cnt[0] / n:.1f}, in range {cnt[1] / n:.1f}, open {cnt[2] / n:.1f}, "
                      f"walls {cnt[3] / n:.1f}, wall-ray pairs {cnt[4] / n:.1f}, exact casts {cnt[5] / n:.1f}")
         phases(sens, SENSOR, 0, "sensor_kernel", extra)
+        cb = b[2 * NW * 16 + 8:2 * NW * 16 + 16]
+        if cb[0]:
+            print(f"ray_sensor_kernel: rays {cb[0]}, fallback rays {cb[1]} ({100 * cb[1] / cb[0]:.2f}%), "
+                  f"list entries per ray {cb[3] / max(1, cb[0] - cb[1]):.2f}, walked {cb[2] / max(1, cb[0] - cb[1]):.2f}")
     L.nascar_debug_profile(ctypes.c_void_p(0))
     env.close()
 
