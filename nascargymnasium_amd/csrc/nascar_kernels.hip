@@ -52,7 +52,14 @@ struct DSeg {   // per segment, float64 (src/track_generator.py TrackSegment)
 // Entry = (lower bound in cm, floored) << 16 | wall index.  A ray walks its list and stops at the first
 // entry whose lower bound exceeds its best hit so far: the minimum exact fraction over the walls visited
 // is the minimum over all walls, i.e. the reference's Box2D RayCast result.
-#define BEAM_NB 128
+#ifndef BEAM_NB
+#define BEAM_NB 256       // direction bins (measured 64: 44.2 us, 128: 41.7, 256: 38.7, 512: 39.1) (a multiple of 16: ray i is BEAM_NB / 16 bins from ray i + 1)
+#endif
+#define BEAM_STRIDE (BEAM_NB / 16)
+// list slot of a bin: the 16 bins of one residue mod BEAM_STRIDE are adjacent, so a car's 16 rays read
+// 16 adjacent lists
+__host__ __device__ __forceinline__ int beam_slot(int bin) { return (bin % BEAM_STRIDE) * 16 + bin / BEAM_STRIDE; }
+__host__ __device__ __forceinline__ int beam_bin(int slot) { return (slot % 16) * BEAM_STRIDE + slot / 16; }
 struct BeamGrid {
   float ox, oy, inv_cell; int nx, ny;
   const int* cell;          // [nx * ny]: first list of the cell (built cell id * BEAM_NB), -1: not built
@@ -1235,7 +1242,7 @@ ray_sensor_kernel(Params P, float* obs, float* terminal_obs, int passes) {
         double u = sa * (BEAM_NB / (2.0 * PI_D));
         u -= BEAM_NB * floor(u * (1.0 / BEAM_NB));
         const int bin = min(BEAM_NB - 1, max(0, (int)u));
-        const int sl = ((bin & 7) << 4) | (bin >> 3);   // a car's 16 rays (bins 8 apart) read 16 adjacent lists
+        const int sl = beam_slot(bin);
         const uint32_t s0 = G.start[base + sl], e0 = G.start[base + sl + 1];
         PCOUNT(11, e0 - s0);
         for (uint32_t k = s0; k < e0; ++k) {
@@ -1744,7 +1751,10 @@ static void build_grids(HostTrack& t) {
 //    B, widened by asin((rr + rc) / dist(c, AB)) (all bins when c is inside the grown capsule), plus a
 //    2e-3 rad guard for the f32 ray end points; every bin that arc touches lists the wall.
 // Both are conservative, so the walk in ray_sensor_kernel visits every wall that can be the first hit.
-static const float BEAM_CELL = 4.0f;
+#ifndef BEAM_CELL_M
+#define BEAM_CELL_M 4.0f
+#endif
+static const float BEAM_CELL = BEAM_CELL_M;
 static const double BEAM_BAND = 8.0;
 static void build_beams(HostTrack& t) {
   auto t0 = std::chrono::steady_clock::now();
@@ -1826,11 +1836,10 @@ static void build_beams(HostTrack& t) {
   for (auto& x : th) x.join();
   B.start.assign((size_t)ncell * BEAM_NB + 1, 0);
   B.ent.clear();
-  // lists stored per cell in slot order, slot = (bin % 8) * 16 + bin / 8: the 16 rays of a car (pi/8 = 8 bins
-  // apart) read 16 adjacent lists
+  // lists stored per cell in slot order (beam_slot)
   for (int ci = 0; ci < ncell; ++ci)
     for (int slot = 0; slot < BEAM_NB; ++slot) {
-      const int bin = ((slot & 15) << 3) | (slot >> 4);
+      const int bin = beam_bin(slot);
       const auto& L = lists[(size_t)ci * BEAM_NB + bin];
       B.start[(size_t)ci * BEAM_NB + slot] = (uint32_t)B.ent.size();
       B.ent.insert(B.ent.end(), L.begin(), L.end());
