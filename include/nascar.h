@@ -97,6 +97,11 @@ int nascar_actor_forward(NascarHandle* h, const float* obs, int32_t n, float* ac
  * (device pointers, n floats).  Parity tests compare it with the host libm. */
 int nascar_debug_sincosf(const float* x, float* s, float* c, int32_t n, void* stream);
 
+/* Test hook: sensors only.  poses: device float32 [E*C*3] (x, y, angle) per car, written into the sensor
+ * hand-off; impl 1 = beam-list ray kernel (the step's default), 0 = wall-group kernel; writes the 16
+ * DistanceSensor values obs[n*38 + 22 .. 37] (src/distance_sensor.py:71-117, src/car_env.py:946). */
+int nascar_debug_sensors(NascarHandle* h, const float* poses, float* obs, int32_t impl, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

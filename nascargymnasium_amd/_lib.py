@@ -90,6 +90,8 @@ def lib():
     L.nascar_actor_forward.restype = ctypes.c_int
     L.nascar_debug_sincosf.argtypes = [vp, vp, vp, i32, vp]
     L.nascar_debug_sincosf.restype = ctypes.c_int
+    L.nascar_debug_sensors.argtypes = [vp, vp, vp, i32, vp]
+    L.nascar_debug_sensors.restype = ctypes.c_int
     _lib = L
     return L
 
@@ -97,7 +99,7 @@ def lib():
 EXPORTED = ["nascar_create", "nascar_destroy", "nascar_last_error", "nascar_add_track", "nascar_set_env_tracks",
             "nascar_reset", "nascar_step", "nascar_get_info", "nascar_state_bytes", "nascar_get_state",
             "nascar_set_state", "nascar_policy_actions", "nascar_set_actor", "nascar_actor_forward",
-            "nascar_debug_sincosf"]
+            "nascar_debug_sincosf", "nascar_debug_sensors"]
 
 
 def check(rc):

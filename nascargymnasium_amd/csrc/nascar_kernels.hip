@@ -2105,8 +2105,9 @@ static int sensor_impl() {
   if (m < 0) { const char* e = getenv("NASCAR_SENSOR"); m = (e && !strcmp(e, "groups")) ? 0 : 1; }
   return m;
 }
-static void launch_sensors(NascarHandle* h, const Params& P, float* obs, float* terminal_obs, int passes, void* stream) {
-  if (sensor_impl() == 1) {
+static void launch_sensors_impl(NascarHandle* h, const Params& P, float* obs, float* terminal_obs, int passes,
+                                void* stream, int impl) {
+  if (impl == 1) {
     constexpr int CPW = BLOCK / RAY_LPC;
     const int sub = (SBLOCK + CPW - 1) / CPW;
     hipLaunchKernelGGL(ray_sensor_kernel, dim3(h->nblocks * sub), dim3(BLOCK), 0, (hipStream_t)stream, P, obs,
@@ -2121,6 +2122,9 @@ static void launch_sensors(NascarHandle* h, const Params& P, float* obs, float* 
   const int sub = (SBLOCK + BLOCK / SENSOR_LPC - 1) / (BLOCK / SENSOR_LPC);
   hipLaunchKernelGGL(sensor_kernel<SENSOR_LPC>, dim3(h->nblocks * sub), dim3(BLOCK), lds, (hipStream_t)stream,
                      P, obs, terminal_obs, passes);
+}
+static void launch_sensors(NascarHandle* h, const Params& P, float* obs, float* terminal_obs, int passes, void* stream) {
+  launch_sensors_impl(h, P, obs, terminal_obs, passes, stream, sensor_impl());
 }
 
 extern "C" int nascar_reset(NascarHandle* h, const uint8_t* env_mask, float* obs, void* stream) {
@@ -2273,6 +2277,29 @@ extern "C" int nascar_actor_forward(NascarHandle* h, const float* obs, int32_t n
 extern "C" int nascar_debug_sincosf(const float* x, float* s, float* c, int32_t n, void* stream) {
   if (!x || !s || !c || n < 0) return fail("bad argument");
   hipLaunchKernelGGL(sincos_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, x, s, c, n);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+// Sensor test hook: car n's pose hand-off set to poses[n] = (x, y, angle) (float32, the body position and
+// angle the sensors read), then one sensor launch: impl 1 = ray_sensor_kernel (beam lists), 0 = the
+// wall-group sensor_kernel.  Writes obs[n * 38 + 22 .. 37]; other obs entries are left untouched.
+__global__ void debug_pose_kernel(Params P, const float* poses) {
+  const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= P.N) return;
+  const float a = poses[3 * n + 2];
+  P.pose[n] = make_float4(poses[3 * n], poses[3 * n + 1], a, __int_as_float(PM_A_OBS));
+  double s0, c0;
+  sincos((double)a, &s0, &c0);
+  P.pose_cs[n] = make_double2(c0, s0);
+}
+extern "C" int nascar_debug_sensors(NascarHandle* h, const float* poses, float* obs, int32_t impl, void* stream) {
+  if (!h || !poses || !obs) return fail("null argument");
+  if (prepare(h)) return -1;
+  Params P = make_params(h);
+  hipLaunchKernelGGL(debug_pose_kernel, dim3((h->N + 255) / 256), dim3(256), 0, (hipStream_t)stream, P, poses);
+  HIPCHK(hipGetLastError());
+  launch_sensors_impl(h, P, obs, nullptr, 1, stream, impl);
   HIPCHK(hipGetLastError());
   return 0;
 }
