@@ -6,7 +6,7 @@ Reads the rocprofv3 CSVs under <out_dir>/{kt,fetch,write}, and writes
   profiles/<tag>_kernel_stats.csv  (rocprofv3 --stats summary, copied verbatim)
   profiles/<tag>_pmc_step.json     (per-dispatch FETCH_SIZE / WRITE_SIZE of the two kernels of a step)
   profiles/pmc_traffic.json        (read by bench.py for roofline.traffic)
-One env step = one model_kernel + logic_kernel + sensor_kernel launch each.  HBM bytes = (2 * FETCH_SIZE + WRITE_SIZE)
+One env step = one model_kernel + logic_kernel + ray_sensor_kernel launch each.  HBM bytes = (2 * FETCH_SIZE + WRITE_SIZE)
 * 1024: FETCH_SIZE/WRITE_SIZE are in KiB and gfx950 FETCH_SIZE tallies half the bytes of a wide
 coalesced read (MI355X_MICROARCH.md "HBM").
 """
@@ -19,7 +19,7 @@ import sys
 from collections import defaultdict
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNELS = ("model_kernel", "logic_kernel", "sensor_kernel")
+KERNELS = ("model_kernel", "logic_kernel", "ray_sensor_kernel")
 
 
 def _find(d, suffix):
@@ -35,10 +35,15 @@ def _bench_line(log):
     return None
 
 
+def _base(name):
+    """'void ray_sensor_kernel<4>(Params, ...)' -> 'ray_sensor_kernel'"""
+    return name.split("(")[0].replace("void ", "").split("<")[0].strip()
+
+
 def _per_dispatch(path, counter, kernel):
     vals = defaultdict(float)
     for row in csv.DictReader(open(path)):
-        if kernel not in row.get("Kernel_Name", "") or row.get("Counter_Name") != counter:
+        if _base(row.get("Kernel_Name", "")) != kernel or row.get("Counter_Name") != counter:
             continue
         vals[row["Dispatch_Id"]] += float(row["Counter_Value"])
     return list(vals.values())
@@ -54,7 +59,7 @@ def main():
         shutil.copy(stats, os.path.join(prof, f"{tag}_kernel_stats.csv"))
         for row in csv.DictReader(open(stats)):
             for kn in KERNELS:
-                if row["Name"].startswith(kn) or ("void " + kn) in row["Name"]:
+                if _base(row["Name"]) == kn:
                     res[f"{kn}_rocprof_avg_ns"] = float(row["AverageNs"])
                     res[f"{kn}_rocprof_calls"] = int(row["Calls"])
         res["step_rocprof_avg_ns"] = sum(res.get(f"{kn}_rocprof_avg_ns", 0.0) for kn in KERNELS)
