@@ -1193,6 +1193,9 @@ __device__ inline float ray_fallback(const TrackDev& T, V2 p1, float p2x, float 
 #ifndef RSENSOR_WPE
 #define RSENSOR_WPE 6   // 4 lanes per car at 6 waves/SIMD: 41.5 us (8 lanes 53.7, 2 lanes 44.3; 16 lanes 62.4)
 #endif
+#ifndef RAY_GLOBAL_WALLS
+#define RAY_LDS_WALLS   // the 23 KB wall image staged per workgroup: 38.6 -> 37.5 us
+#endif
 #ifndef RAY_LPC
 #define RAY_LPC 4     // lanes per car; each lane walks the lists of 16 / RAY_LPC rays
 #endif
@@ -1206,15 +1209,27 @@ ray_sensor_kernel(Params P, float* obs, float* terminal_obs, int passes) {
   const int slot = sub * CPW + lc;
   const int el = slot / C, car = slot - el * C;
   const int env = (el < P.epb) ? P.blk_env[b * P.epb + el] : -1;
+  const TrackDev& T = P.tracks[P.blk_track[b]];
+#ifdef RAY_LDS_WALLS
+  {
+    float4* s_w = (float4*)smem;
+    const int nw2 = 2 * T.nwall;
+    for (int k = t; k < nw2; k += BLOCK) s_w[k] = T.swall[k];
+    __syncthreads();
+  }
+#endif
   if (env < 0) return;
   const int n = env * C + car;
-  const TrackDev& T = P.tracks[P.blk_track[b]];
   int mode = 0;
   float4 pa = make_float4(0.f, 0.f, 0.f, 0.f), pb = pa;
   if (passes & 1) { pa = P.pose[n]; mode = __float_as_int(pa.w) & (PM_A_OBS | PM_A_TERM); }
   if (passes & 2) { pb = P.pose[P.N + n]; mode |= __float_as_int(pb.w) & PM_B_OBS; }
   const BeamGrid G = T.beam;
+#ifdef RAY_LDS_WALLS
+  const float4* __restrict__ sw = (const float4*)smem;   // the track's wall image staged per workgroup
+#else
   const float4* __restrict__ sw = T.swall;
+#endif
 #pragma unroll 1
   for (int pass = 0; pass < 2; ++pass) {
     const bool active = pass == 0 ? (mode & (PM_A_OBS | PM_A_TERM)) != 0 : (mode & PM_B_OBS) != 0;
@@ -2110,7 +2125,12 @@ static void launch_sensors_impl(NascarHandle* h, const Params& P, float* obs, fl
   if (impl == 1) {
     constexpr int CPW = BLOCK / RAY_LPC;
     const int sub = (SBLOCK + CPW - 1) / CPW;
-    hipLaunchKernelGGL(ray_sensor_kernel, dim3(h->nblocks * sub), dim3(BLOCK), 0, (hipStream_t)stream, P, obs,
+#ifdef RAY_LDS_WALLS
+    const size_t rlds = h->max_sensor_lds;   // >= 2 float4 per wall
+#else
+    const size_t rlds = 0;
+#endif
+    hipLaunchKernelGGL(ray_sensor_kernel, dim3(h->nblocks * sub), dim3(BLOCK), rlds, (hipStream_t)stream, P, obs,
                        terminal_obs, passes);
     return;
   }
