@@ -1352,6 +1352,13 @@ __global__ void __launch_bounds__(SBLOCK) logic_kernel(Params P, float* obs, flo
   __shared__ int s_rowbase[SBLOCK];
   __shared__ float4 s_sg[MAX_SEG];
   __shared__ float s_rll[MAX_SEG];
+  Car c;
+  double sim = 0.0;
+  if (env >= 0) {   // state loads issued before the segment staging barrier (independent round trips)
+    car_load_body(P, n, c);
+    car_load_logic(P, n, c);
+    sim = P.env_time[env];
+  }
   TrackDev T = P.tracks[P.blk_track[blockIdx.x]];
   if (tid < T.nseg) {
     const DSeg sg = T.segs[tid];
@@ -1366,14 +1373,9 @@ __global__ void __launch_bounds__(SBLOCK) logic_kernel(Params P, float* obs, flo
   float cut = INFINITY;
   const int nw = T.nwall;
   const WallSet S{T.walls, nw, T.bp, T.sn};
-  Car c;
   bool lapdone = false;
-  double sim = 0.0;
   if (env >= 0) {
-    car_load_body(P, n, c);
-    sim = P.env_time[env];
     s_dis_old[tid] = c.disabled;
-    car_load_logic(P, n, c);
     LPROF(1);
     s_laps_old[tid] = c.lt_laps;   // the lap count does not change before lap_update
     cut = screen_cut(CS, c.xf.p.x, c.xf.p.y);   // the body position is final for this step
