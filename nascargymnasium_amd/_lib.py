@@ -15,7 +15,7 @@ CSRC = os.path.join(HERE, "csrc")
 INFO_FIELDS = ["x", "y", "vx", "vy", "angle", "omega", "speed", "lap_count", "last_lap_time", "best_lap_time",
                "is_timing", "current_lap_time", "total_distance_traveled", "has_crossed_startline", "disabled",
                "cumulative_reward", "cumulative_impact_force", "on_track", "engine_rpm", "simulation_time",
-               "n_contacts", "error"]
+               "n_contacts", "error", "track_progress"]
 N_INFO = len(INFO_FIELDS)
 OBS_DIM = 38
 

@@ -228,6 +228,7 @@ class CarEnv(BaseEnv):
             self.track = load_track(track_path(self.track_file))
             self._engine.set_env_tracks([track_path(self.track_file)])
         obs = self._engine.reset()[0].cpu().numpy()
+        self._info_cache = None
         self._ready = True
         self.cars = list(range(self.num_cars))
         self.disabled_cars = set()
@@ -272,6 +273,44 @@ class CarEnv(BaseEnv):
         if C == 1:
             return obs[0], rew[0], terminated, truncated, info
         return obs, rew, terminated, truncated, info
+
+    # ------------------------------------------------------------------ race tables (src/car_env.py:1485-1637)
+    def _info_rows(self):
+        return self._info_cache if self._info_cache is not None else self._engine.info_tensor()[0].cpu().numpy()
+
+    def _calculate_race_positions(self) -> list:
+        """CarEnv._calculate_race_positions (src/car_env.py:1485-1542): (car_index, car_name, total_progress,
+        virtual_laps, current_progress) of the non-disabled cars, leader first."""
+        if not self._ready:
+            return []
+        F = {f: i for i, f in enumerate(_lib.INFO_FIELDS)}
+        rows = self._info_rows()
+        L = self.track.get_total_track_length()
+        out = []
+        for i in range(self.num_cars):
+            if i in self.disabled_cars:
+                continue
+            r = rows[i]
+            laps, prog = int(r[F["lap_count"]]), float(r[F["track_progress"]])
+            virtual = laps
+            if (bool(r[F["is_timing"]]) and bool(r[F["has_crossed_startline"]]) and prog < L * 0.15
+                    and float(r[F["total_distance_traveled"]]) > L * 0.8):
+                virtual = laps + 1
+            out.append((i, self.car_names[i], virtual * L + prog, virtual, prog))
+        out.sort(key=lambda x: (x[3], x[4]), reverse=True)
+        return out
+
+    def _get_best_lap_times_data(self) -> list:
+        """CarEnv._get_best_lap_times_data (src/car_env.py:1613-1638): (car_index, car_name, best_lap_time)
+        of the non-disabled cars with a best lap, fastest first."""
+        if not self._ready:
+            return []
+        F = {f: i for i, f in enumerate(_lib.INFO_FIELDS)}
+        rows = self._info_rows()
+        out = [(i, self.car_names[i], float(rows[i][F["best_lap_time"]])) for i in range(self.num_cars)
+               if i not in self.disabled_cars and not np.isnan(rows[i][F["best_lap_time"]])]
+        out.sort(key=lambda x: x[2])
+        return out
 
     # ------------------------------------------------------------------ info (src/car_env.py:1160-1227)
     def _make_info(self, info_np=None):

@@ -65,7 +65,12 @@ struct BeamGrid {
   const int* cell;          // [nx * ny]: first list of the cell (built cell id * BEAM_NB), -1: not built
   const uint32_t* start;    // [built cells * BEAM_NB + 1]
   const uint32_t* ent;
+  // [built cells * BEAM_NB] the first BEAM_HEAD entries of each list, padded with BEAM_PAD: one 16-byte load
+  // starts a walk (the rest of the list, ent[start[slot] + BEAM_HEAD ...], is read only past the head)
+  const uint4* head;
 };
+#define BEAM_HEAD 4
+#define BEAM_PAD 0xFFFFFFFFu   // bound 655.35 m: past every best hit (<= 2 * 250 m), so a walk always stops on it
 struct TrackDev {
   LWall* walls; int nwall;
   DSeg* segs; int nseg;
@@ -1241,6 +1246,21 @@ ray_sensor_kernel(Params P, float* obs, float* terminal_obs, int passes) {
     int base = -1;
     const float fx = (p1.x - G.ox) * G.inv_cell, fy = (p1.y - G.oy) * G.inv_cell;
     if (fx >= 0.0f && fy >= 0.0f && fx < (float)G.nx && fy < (float)G.ny) base = G.cell[(int)fy * G.nx + (int)fx];
+    // direction bin of sa = -radians(22.5 i) + ang (f64; the lists carry a 2e-3 rad guard) -> list slot
+    auto slot_of = [&](int i) {
+      const double sa = -((double)i * (360.0 / 16) * RAD_PER_DEG) + ang;
+      double u = sa * (BEAM_NB / (2.0 * PI_D));
+      u -= BEAM_NB * floor(u * (1.0 / BEAM_NB));
+      return beam_slot(min(BEAM_NB - 1, max(0, (int)u)));
+    };
+#ifdef RAY_HEAD_ALL
+    // all of the lane's list heads requested before the first walk (independent loads in flight together)
+    uint4 hd[RPL];
+#pragma unroll
+    for (int q = 0; q < RPL; ++q) hd[q] = base >= 0 ? G.head[base + slot_of(r + RAY_LPC * q)] : make_uint4(0, 0, 0, 0);
+#undef RAY_UNROLL
+#define RAY_UNROLL RPL
+#endif
 #ifndef RAY_UNROLL
 #define RAY_UNROLL 1
 #endif
@@ -1252,12 +1272,35 @@ ray_sensor_kernel(Params P, float* obs, float* terminal_obs, int passes) {
       const float dx = (p2.x - p1.x) * 0.004f, dy = (p2.y - p1.y) * 0.004f;   // cull only
       float bi = 2.0f;
       if (base >= 0) {
-        // direction bin of sa = -radians(22.5 i) + ang (f64; the lists carry a 2e-3 rad guard)
-        const double sa = -((double)i * (360.0 / 16) * RAD_PER_DEG) + ang;
-        double u = sa * (BEAM_NB / (2.0 * PI_D));
-        u -= BEAM_NB * floor(u * (1.0 / BEAM_NB));
-        const int bin = min(BEAM_NB - 1, max(0, (int)u));
-        const int sl = beam_slot(bin);
+        const int sl = slot_of(i);
+#ifndef RAY_NO_HEAD
+        // the list's first BEAM_HEAD entries in one load; the rest of the list only when all were walked
+#ifdef RAY_HEAD_ALL
+        const uint4 h = hd[q];
+#else
+        const uint4 h = G.head[base + sl];
+#endif
+        const uint32_t hv[BEAM_HEAD] = {h.x, h.y, h.z, h.w};
+        bool more = true;
+#pragma unroll
+        for (int k = 0; k < BEAM_HEAD; ++k) {
+          const uint32_t v = hv[k];
+          if ((float)(v >> 16) * 0.01f > bi * 250.0f * 1.00001f + 0.01f) { more = false; break; }
+          const int j = (int)(v & 0xFFFFu);
+          PCOUNT(10, 1);
+          bi = wall_cast(sw[2 * j], sw[2 * j + 1], p1, p2.x, p2.y, dx, dy, bi);
+        }
+        if (more) {
+          const uint32_t s0 = G.start[base + sl] + BEAM_HEAD, e0 = G.start[base + sl + 1];
+          for (uint32_t k = s0; k < e0; ++k) {
+            const uint32_t v = G.ent[k];
+            if ((float)(v >> 16) * 0.01f > bi * 250.0f * 1.00001f + 0.01f) break;
+            const int j = (int)(v & 0xFFFFu);
+            PCOUNT(10, 1);
+            bi = wall_cast(sw[2 * j], sw[2 * j + 1], p1, p2.x, p2.y, dx, dy, bi);
+          }
+        }
+#else
         const uint32_t s0 = G.start[base + sl], e0 = G.start[base + sl + 1];
         PCOUNT(11, e0 - s0);
         for (uint32_t k = s0; k < e0; ++k) {
@@ -1267,6 +1310,7 @@ ray_sensor_kernel(Params P, float* obs, float* terminal_obs, int passes) {
           PCOUNT(10, 1);
           bi = wall_cast(sw[2 * j], sw[2 * j + 1], p1, p2.x, p2.y, dx, dy, bi);
         }
+#endif
       } else {
         PCOUNT(9, 1);
         bi = ray_fallback(T, p1, p2.x, p2.y, dx, dy, ps.z, i);
@@ -1589,6 +1633,9 @@ __global__ void __launch_bounds__(SBLOCK) info_kernel(Params P, double* info) {
   o[INFO_CUM_IMPACT] = c.cum_impact;
   o[INFO_ON_TRACK] = query_on_wall(S, c.xf.p.x, c.xf.p.y, 0.5) ? 0.0 : 1.0;
   o[INFO_RPM] = c.rpm; o[INFO_SIM_TIME] = P.env_time[env]; o[INFO_NCT] = c.nct; o[INFO_ERROR] = c.overflow;
+  // CarEnv._calculate_track_progress of the current position (src/car_env.py:1544-1611): the reward pass
+  // stores it every step for every car that is not disabled (and reset_car for the start pose)
+  o[INFO_PROGRESS] = c.prog_hist;
 }
 
 // ------------------------------------------------------------------ synthetic action sources (bench)
@@ -1662,8 +1709,8 @@ struct HostTrack {
   HostGrid bp, sn;
   struct {
     BeamGrid g{};
-    std::vector<int> cell; std::vector<uint32_t> start, ent;
-    int* d_cell = nullptr; uint32_t* d_start = nullptr; uint32_t* d_ent = nullptr;
+    std::vector<int> cell; std::vector<uint32_t> start, ent; std::vector<uint4> head;
+    int* d_cell = nullptr; uint32_t* d_start = nullptr; uint32_t* d_ent = nullptr; uint4* d_head = nullptr;
     double build_s = 0.0;
   } beam;
   std::vector<float4> groups; float4* d_groups = nullptr;
@@ -1862,6 +1909,12 @@ static void build_beams(HostTrack& t) {
       B.ent.insert(B.ent.end(), L.begin(), L.end());
     }
   B.start.back() = (uint32_t)B.ent.size();
+  B.head.assign((size_t)ncell * BEAM_NB, make_uint4(BEAM_PAD, BEAM_PAD, BEAM_PAD, BEAM_PAD));
+  for (size_t s = 0; s + 1 < B.start.size(); ++s) {
+    uint32_t h[BEAM_HEAD];
+    for (int k = 0; k < BEAM_HEAD; ++k) h[k] = B.start[s] + k < B.start[s + 1] ? B.ent[B.start[s] + k] : BEAM_PAD;
+    B.head[s] = make_uint4(h[0], h[1], h[2], h[3]);
+  }
   B.build_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
 }
 static int upload_beams(HostTrack& t) {
@@ -1872,7 +1925,9 @@ static int upload_beams(HostTrack& t) {
   HIPCHK(hipMemcpy(B.d_start, B.start.data(), sizeof(uint32_t) * B.start.size(), hipMemcpyHostToDevice));
   HIPCHK(hipMalloc(&B.d_ent, sizeof(uint32_t) * std::max<size_t>(B.ent.size(), 1)));
   if (!B.ent.empty()) HIPCHK(hipMemcpy(B.d_ent, B.ent.data(), sizeof(uint32_t) * B.ent.size(), hipMemcpyHostToDevice));
-  B.g.cell = B.d_cell; B.g.start = B.d_start; B.g.ent = B.d_ent;
+  HIPCHK(hipMalloc(&B.d_head, sizeof(uint4) * std::max<size_t>(B.head.size(), 1)));
+  if (!B.head.empty()) HIPCHK(hipMemcpy(B.d_head, B.head.data(), sizeof(uint4) * B.head.size(), hipMemcpyHostToDevice));
+  B.g.cell = B.d_cell; B.g.start = B.d_start; B.g.ent = B.d_ent; B.g.head = B.d_head;
   return 0;
 }
 
@@ -1950,7 +2005,7 @@ extern "C" void nascar_destroy(NascarHandle* h) {
   for (auto& t : h->tracks) {
     hipFree(t.d_walls); hipFree(t.d_segs); hipFree(t.d_prefix);
     hipFree(t.bp.d_start); hipFree(t.bp.d_idx); hipFree(t.sn.d_start); hipFree(t.sn.d_idx); hipFree(t.d_groups); hipFree(t.d_swall);
-    hipFree(t.beam.d_cell); hipFree(t.beam.d_start); hipFree(t.beam.d_ent);
+    hipFree(t.beam.d_cell); hipFree(t.beam.d_start); hipFree(t.beam.d_ent); hipFree(t.beam.d_head);
   }
   hipFree(h->d_tracks); hipFree(h->d_blk_track); hipFree(h->d_blk_env);
   delete h;
@@ -2041,8 +2096,8 @@ extern "C" int nascar_add_track(NascarHandle* h, const double* segments, int32_t
             "%.1f MB, built in %.2f s\n", t.beam.g.nx, t.beam.g.ny, (t.beam.start.size() - 1) / BEAM_NB, t.beam.ent.size(),
             (double)t.beam.ent.size() / std::max<size_t>(1, t.beam.start.size() - 1),
             (4.0 * (t.beam.ent.size() + t.beam.start.size() + t.beam.cell.size())) / 1e6, t.beam.build_s);
-  t.beam.cell.clear(); t.beam.start.clear(); t.beam.ent.clear();   // the device copies are all the kernels use
-  t.beam.cell.shrink_to_fit(); t.beam.start.shrink_to_fit(); t.beam.ent.shrink_to_fit();
+  t.beam.cell.clear(); t.beam.start.clear(); t.beam.ent.clear(); t.beam.head.clear();   // the device copies are all the kernels use
+  t.beam.cell.shrink_to_fit(); t.beam.start.shrink_to_fit(); t.beam.ent.shrink_to_fit(); t.beam.head.shrink_to_fit();
   h->tracks.push_back(t);
   h->max_lds = std::max(h->max_lds, lds);
   h->dirty_tracks = true;

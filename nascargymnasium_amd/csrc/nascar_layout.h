@@ -58,7 +58,7 @@ enum { E_CREATED, E_PENDING, E_REASON, E_TERMINATED, E_TRUNCATED, N_EI32 };
 enum {
   INFO_X, INFO_Y, INFO_VX, INFO_VY, INFO_ANGLE, INFO_OMEGA, INFO_SPEED, INFO_LAP_COUNT, INFO_LAST_LAP,
   INFO_BEST_LAP, INFO_IS_TIMING, INFO_CUR_LAP_TIME, INFO_LAP_DIST, INFO_HAS_CROSSED, INFO_DISABLED,
-  INFO_CUM_REWARD, INFO_CUM_IMPACT, INFO_ON_TRACK, INFO_RPM, INFO_SIM_TIME, INFO_NCT, INFO_ERROR, N_INFO
+  INFO_CUM_REWARD, INFO_CUM_IMPACT, INFO_ON_TRACK, INFO_RPM, INFO_SIM_TIME, INFO_NCT, INFO_ERROR, INFO_PROGRESS, N_INFO
 };
 
 // car flag bits (nascar_step car_flags output)

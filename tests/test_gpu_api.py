@@ -115,3 +115,45 @@ def test_vec_env_auto_reset_matches_engine():
             assert infos[e]["episode"]["l"] > 0
     assert episodes > 0
     venv.close(); ref.close()
+
+
+def test_race_tables_match_oracle():
+    """CarEnv._calculate_race_positions / _get_best_lap_times_data (src/car_env.py:1485-1638) from the device
+    info vector equal the reference formulas evaluated on the CPU oracle's per-car state."""
+    import numpy as np
+    from nascargymnasium_amd import CarEnv
+    from oracle_lib import OracleEnv
+    C = 4
+    path = os.path.join(TRACKS, "martinsville.track")
+    env = CarEnv(track_file=path, num_cars=C)
+    orc = OracleEnv(path, 1, C)
+    env.reset(seed=0)
+    orc.reset()
+    L = env.track.get_total_track_length()
+    rng = np.random.default_rng(3)
+    checked = 0
+    for k in range(900):
+        a = rng.uniform(-1, 1, (C, 2)).astype(np.float32)
+        a[:, 0] = np.abs(a[:, 0]) * 0.8 + 0.2
+        a[:, 1] *= 0.3
+        env.step(a)
+        orc.step(a[None])
+        if k % 60 != 59:
+            continue
+        rows = [orc.car_info(i) for i in range(C)]
+        exp = []
+        for i, r in enumerate(rows):
+            if r["disabled"]:
+                continue
+            laps, prog = int(r["lap_count"]), r["progress"]
+            virt = laps + 1 if (r["is_timing"] and prog < L * 0.15 and r["lap_distance"] > L * 0.8) else laps
+            exp.append((i, f"Car {i}", virt * L + prog, virt, prog))
+        exp.sort(key=lambda x: (x[3], x[4]), reverse=True)
+        assert env._calculate_race_positions() == exp, f"step {k}"
+        best = sorted([(i, f"Car {i}", r["best_lap"]) for i, r in enumerate(rows)
+                       if not r["disabled"] and r["best_lap"] == r["best_lap"] and r["best_lap"] >= 0], key=lambda x: x[2])
+        got = env._get_best_lap_times_data()
+        assert [g[:2] for g in got] == [b[:2] for b in best]
+        checked += 1
+    assert checked == 15
+    env.close()
