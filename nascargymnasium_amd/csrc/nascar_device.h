@@ -221,7 +221,11 @@ struct WallGrid {
   int nx, ny;
   const int* start;        // [nx*ny + 1]
   const uint16_t* idx;
+  const float4* box;       // bp only: fat AABB (lo.x, lo.y, hi.x, hi.y) of wall idx[k], padded by BP_BATCH entries
 };
+#ifndef BP_BATCH
+#define BP_BATCH 4   // broadphase candidates whose boxes are loaded together (0: one wall record at a time)
+#endif
 struct WallSet {
   const LWall* W; int nw;
   WallGrid bp, sn;
@@ -314,6 +318,22 @@ __device__ __forceinline__ void sync_fixtures(Car& c) {
   move_proxy(c, xf1, c.xf);
 }
 
+// b2ContactManager::AddPair for wall j whose fat AABB overlaps the car's (new contacts are prepended)
+__device__ inline void add_pair(Car& c, int j) {
+    bool exists = false;
+    for (int i = 0; i < c.nct; ++i) if (c.ct[i].wall == j) { exists = true; break; }
+    if (exists) return;
+    if (c.nct >= MAXC) { c.overflow = 1; return; }
+    for (int i = c.nct; i > 0; --i) c.ct[i] = c.ct[i - 1];
+    DContact z;
+    z.wall = j; z.flags = CT_ENABLED; z.mtype = 0; z.pointCount = 0;
+    z.lnx = z.lny = z.lpx = z.lpy = 0.0f;
+    for (int q = 0; q < 2; ++q) { z.pt[q].lx = z.pt[q].ly = z.pt[q].ni = z.pt[q].ti = 0.0f; z.pt[q].id = 0u; }
+    z.toi = 1.0f; z.toiCount = 0;
+    c.ct[0] = z;
+    c.nct++;
+    set_awake(c);
+}
 // b2BroadPhase::UpdatePairs + b2ContactManager::AddPair (ascending wall proxy id, prepend)
 __device__ inline void find_new_contacts(Car& c, const WallSet& S) {
   if (!c.moved) return;
@@ -327,6 +347,25 @@ __device__ inline void find_new_contacts(Car& c, const WallSet& S) {
     if (hx <= S.bp.reach - 0.05f && hy <= S.bp.reach - 0.05f && grid_list(S.bp, cx, cy, beg, end)) list = S.bp.idx;
     else { beg = 0; end = S.nw; }
   }
+#if BP_BATCH > 0
+  if (list && S.bp.box) {
+    // the cell's candidate boxes stored in list order: BP_BATCH independent loads per round instead of a
+    // dependent (index -> wall record) pair per candidate; same candidates, same ascending order
+    const float4* __restrict__ box = S.bp.box;
+    for (int k = beg; k < end; k += BP_BATCH) {
+      float4 b[BP_BATCH];
+#pragma unroll
+      for (int u = 0; u < BP_BATCH; ++u) b[u] = box[k + u];   // in bounds: the array is padded by BP_BATCH
+#pragma unroll
+      for (int u = 0; u < BP_BATCH; ++u) {
+        if (k + u >= end) break;
+        Aabb a; a.lo = V(b[u].x, b[u].y); a.hi = V(b[u].z, b[u].w);
+        if (overlap(c.fat, a)) add_pair(c, (int)list[k + u]);
+      }
+    }
+    return;
+  }
+#endif
   for (int k = beg; k < end; ++k) {
     const int j = list ? (int)list[k] : k;
     const LWall& wl = W[j];

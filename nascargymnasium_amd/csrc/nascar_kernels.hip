@@ -1247,12 +1247,25 @@ ray_sensor_kernel(Params P, float* obs, float* terminal_obs, int passes) {
     const float fx = (p1.x - G.ox) * G.inv_cell, fy = (p1.y - G.oy) * G.inv_cell;
     if (fx >= 0.0f && fy >= 0.0f && fx < (float)G.nx && fy < (float)G.ny) base = G.cell[(int)fy * G.nx + (int)fx];
     // direction bin of sa = -radians(22.5 i) + ang (f64; the lists carry a 2e-3 rad guard) -> list slot
+#ifdef RAY_BIN_PER_RAY
     auto slot_of = [&](int i) {
       const double sa = -((double)i * (360.0 / 16) * RAD_PER_DEG) + ang;
       double u = sa * (BEAM_NB / (2.0 * PI_D));
       u -= BEAM_NB * floor(u * (1.0 / BEAM_NB));
       return beam_slot(min(BEAM_NB - 1, max(0, (int)u)));
     };
+#else
+    // ray i is exactly BEAM_STRIDE bins clockwise of ray 0 in real arithmetic, and the f64 rounding of
+    // sa_i (~1e-15 rad) is far inside the lists' 2e-3 rad guard, so bin_i = bin_0 - BEAM_STRIDE i:
+    // slot_i = (bin_0 % STRIDE) * 16 + (bin_0 / STRIDE - i) mod 16
+    int slot0;
+    {
+      double u = ang * (BEAM_NB / (2.0 * PI_D));
+      u -= BEAM_NB * floor(u * (1.0 / BEAM_NB));
+      slot0 = beam_slot(min(BEAM_NB - 1, max(0, (int)u)));
+    }
+    auto slot_of = [&](int i) { return (slot0 & ~15) | ((slot0 - i) & 15); };
+#endif
 #ifdef RAY_HEAD_ALL
     // all of the lane's list heads requested before the first walk (independent loads in flight together)
     uint4 hd[RPL];
@@ -1701,6 +1714,7 @@ struct HostGrid {
   WallGrid g{};
   std::vector<int> start; std::vector<uint16_t> idx;
   int* d_start = nullptr; uint16_t* d_idx = nullptr;
+  std::vector<float4> box; float4* d_box = nullptr;
 };
 struct HostTrack {
   std::vector<LWall> walls; std::vector<DSeg> segs; std::vector<double> prefix;
@@ -1744,9 +1758,11 @@ static void build_grids(HostTrack& t) {
         const LWall& w = t.walls[j];
         if (w.flx > x1 || w.fhx < x0 || w.fly > y1 || w.fhy < y0) continue;
         t.bp.idx.push_back((uint16_t)j);
+        t.bp.box.push_back(make_float4(w.flx, w.fly, w.fhx, w.fhy));
       }
     }
   t.bp.start.back() = (int)t.bp.idx.size();
+  for (int k = 0; k < std::max(BP_BATCH, 1); ++k) t.bp.box.push_back(make_float4(1e30f, 1e30f, -1e30f, -1e30f));
   // sensor wall groups: runs of consecutive walls (index order follows each boundary through
   // the curves) whose corners fit in a circle of radius <= SN_GROUP_R, at most SN_GROUP_N walls
   {
@@ -1936,7 +1952,12 @@ static int upload_grid(HostGrid& G) {
   HIPCHK(hipMemcpy(G.d_start, G.start.data(), sizeof(int) * G.start.size(), hipMemcpyHostToDevice));
   HIPCHK(hipMalloc(&G.d_idx, sizeof(uint16_t) * std::max<size_t>(G.idx.size(), 1)));
   if (!G.idx.empty()) HIPCHK(hipMemcpy(G.d_idx, G.idx.data(), sizeof(uint16_t) * G.idx.size(), hipMemcpyHostToDevice));
-  G.g.start = G.d_start; G.g.idx = G.d_idx;
+  G.g.start = G.d_start; G.g.idx = G.d_idx; G.g.box = nullptr;
+  if (!G.box.empty()) {
+    HIPCHK(hipMalloc(&G.d_box, sizeof(float4) * G.box.size()));
+    HIPCHK(hipMemcpy(G.d_box, G.box.data(), sizeof(float4) * G.box.size(), hipMemcpyHostToDevice));
+    G.g.box = G.d_box;
+  }
   return 0;
 }
 
@@ -2004,7 +2025,7 @@ extern "C" void nascar_destroy(NascarHandle* h) {
   hipFree(h->arena); hipFree(h->d_ctl); hipFree(h->d_pose); hipFree(h->d_pose_cs); hipFree(h->d_ray_cs); hipFree(h->d_actor);
   for (auto& t : h->tracks) {
     hipFree(t.d_walls); hipFree(t.d_segs); hipFree(t.d_prefix);
-    hipFree(t.bp.d_start); hipFree(t.bp.d_idx); hipFree(t.sn.d_start); hipFree(t.sn.d_idx); hipFree(t.d_groups); hipFree(t.d_swall);
+    hipFree(t.bp.d_start); hipFree(t.bp.d_idx); hipFree(t.bp.d_box); hipFree(t.sn.d_start); hipFree(t.sn.d_idx); hipFree(t.d_groups); hipFree(t.d_swall);
     hipFree(t.beam.d_cell); hipFree(t.beam.d_start); hipFree(t.beam.d_ent); hipFree(t.beam.d_head);
   }
   hipFree(h->d_tracks); hipFree(h->d_blk_track); hipFree(h->d_blk_env);
