@@ -94,7 +94,22 @@ struct Params {
   float4* pose;        // [2][N] sensor hand-off: (x, y, angle, mode) -- see sensor_kernel
   double2* pose_cs;    // [2][N] cos, sin of (double)angle for the ray end points (computed once per car)
   const double2* ray_cs;   // [16] cos, sin of the ray offsets radians(22.5 i) (nascar_rays.h)
+  // [N] beam-list base of pose A's cell, looked up by logic_kernel off the sensor kernel's critical path
+  // (-1: no lists there); any value < -1 (POSE_CELL_UNSET): the sensor kernel looks it up itself
+  int* pose_cell;
 };
+#define POSE_CELL_UNSET (-2)
+// Default: the sensor kernel looks its cell up itself.  -DRAY_LOGIC_CELL moves the lookup into logic_kernel
+// (measured 88.1 vs 86.4 us/step: logic_kernel's extra load and store cost more than the sensor saves).
+#ifndef RAY_LOGIC_CELL
+#define RAY_OWN_CELL
+#endif
+// BeamGrid list base (built cell id * BEAM_NB) of the cell holding (x, y); -1 outside the built cells
+__device__ __forceinline__ int beam_cell_base(const BeamGrid& G, float x, float y) {
+  const float fx = (x - G.ox) * G.inv_cell, fy = (y - G.oy) * G.inv_cell;
+  if (fx >= 0.0f && fy >= 0.0f && fx < (float)G.nx && fy < (float)G.ny) return G.cell[(int)fy * G.nx + (int)fx];
+  return -1;
+}
 
 #define F32P(P, f) ((P).f32 + (size_t)F32_##f * (P).N)
 #define F64P(P, f) ((P).f64 + (size_t)F64_##f * (P).N)
@@ -799,6 +814,7 @@ __device__ __forceinline__ float4 car_pose(const Car& c, int mode) {
 // pose hand-off slot k (n: pass A, N + n: pass B) with the f64 cos / sin of the angle the rays rotate
 __device__ __forceinline__ void set_pose(const Params& P, size_t k, const Car& c, int mode) {
   P.pose[k] = car_pose(c, mode);
+  if (k < (size_t)P.N) P.pose_cell[k] = POSE_CELL_UNSET;   // logic_kernel fills it in for the step's pose A
   double s0, c0;
   sincos((double)c.a, &s0, &c0);
   P.pose_cs[k] = make_double2(c0, s0);
@@ -1227,7 +1243,13 @@ ray_sensor_kernel(Params P, float* obs, float* terminal_obs, int passes) {
   const int n = env * C + car;
   int mode = 0;
   float4 pa = make_float4(0.f, 0.f, 0.f, 0.f), pb = pa;
-  if (passes & 1) { pa = P.pose[n]; mode = __float_as_int(pa.w) & (PM_A_OBS | PM_A_TERM); }
+  int cell_a = POSE_CELL_UNSET;
+  if (passes & 1) {
+    pa = P.pose[n]; mode = __float_as_int(pa.w) & (PM_A_OBS | PM_A_TERM);
+#ifndef RAY_OWN_CELL
+    cell_a = P.pose_cell[n];
+#endif
+  }
   if (passes & 2) { pb = P.pose[P.N + n]; mode |= __float_as_int(pb.w) & PM_B_OBS; }
   const BeamGrid G = T.beam;
 #ifdef RAY_LDS_WALLS
@@ -1243,9 +1265,8 @@ ray_sensor_kernel(Params P, float* obs, float* terminal_obs, int passes) {
     const V2 p1 = V(ps.x, ps.y);
     const double px = ps.x, py = ps.y, ang = ps.z;
     const double2 cs = P.pose_cs[pass == 0 ? (size_t)n : (size_t)P.N + n];
-    int base = -1;
-    const float fx = (p1.x - G.ox) * G.inv_cell, fy = (p1.y - G.oy) * G.inv_cell;
-    if (fx >= 0.0f && fy >= 0.0f && fx < (float)G.nx && fy < (float)G.ny) base = G.cell[(int)fy * G.nx + (int)fx];
+    const int pc = pass == 0 ? cell_a : POSE_CELL_UNSET;
+    const int base = pc >= -1 ? pc : beam_cell_base(G, p1.x, p1.y);
     // direction bin of sa = -radians(22.5 i) + ang (f64; the lists carry a 2e-3 rad guard) -> list slot
 #ifdef RAY_BIN_PER_RAY
     auto slot_of = [&](int i) {
@@ -1417,6 +1438,11 @@ __global__ void __launch_bounds__(SBLOCK) logic_kernel(Params P, float* obs, flo
     sim = P.env_time[env];
   }
   TrackDev T = P.tracks[P.blk_track[blockIdx.x]];
+#ifndef RAY_OWN_CELL
+  // the sensor kernel's beam cell of this step's pose (pose A = the body position model_kernel stored):
+  // its round trip overlaps this kernel instead of sitting on the sensor kernel's dependent chain
+  const int cell_a = env >= 0 ? beam_cell_base(T.beam, c.xf.p.x, c.xf.p.y) : -1;
+#endif
   if (tid < T.nseg) {
     const DSeg sg = T.segs[tid];
     s_segs[tid] = sg; s_prefix[tid] = T.prefix[tid];
@@ -1568,6 +1594,9 @@ __global__ void __launch_bounds__(SBLOCK) logic_kernel(Params P, float* obs, flo
     if (terminal_obs) { float* t = terminal_obs + (size_t)n * 38; for (int i = 0; i < 22; ++i) t[i] = o[i]; }
     // sensor pass B: the reset pose of every auto-reset car (its pass-B values overwrite the pass-A
     // ones in obs); cleared for every other car
+#ifndef RAY_OWN_CELL
+    P.pose_cell[n] = cell_a;
+#endif
     if (reset_now) {
       car_reset(P, c, n, false, S, T);
       car_obs(c, o);
@@ -2008,8 +2037,10 @@ extern "C" int nascar_create(const NascarConfig* cfg, NascarHandle** out) {
   if (e != hipSuccess) { delete h; return fail("hipMalloc(%zu) failed: %s", o, hipGetErrorString(e)); }
   hipMemset(h->arena, 0, o);
   hipMalloc(&h->d_ctl, sizeof(double) * 4 * N);
-  if (hipMalloc(&h->d_pose, sizeof(float4) * 2 * N) != hipSuccess) { hipFree(h->arena); hipFree(h->d_ctl); delete h; return fail("hipMalloc(pose) failed"); }
+  // pose hand-off [2][N] float4, then pose_cell [N] int (initialised < -1: POSE_CELL_UNSET)
+  if (hipMalloc(&h->d_pose, (sizeof(float4) * 2 + sizeof(int)) * N) != hipSuccess) { hipFree(h->arena); hipFree(h->d_ctl); delete h; return fail("hipMalloc(pose) failed"); }
   hipMemset(h->d_pose, 0, sizeof(float4) * 2 * N);
+  hipMemset(h->d_pose + 2 * (size_t)N, 0x80, sizeof(int) * N);
   if (hipMalloc(&h->d_pose_cs, sizeof(double2) * 2 * N) != hipSuccess) { hipFree(h->arena); hipFree(h->d_ctl); hipFree(h->d_pose); delete h; return fail("hipMalloc(pose_cs) failed"); }
   hipMemset(h->d_pose_cs, 0, sizeof(double2) * 2 * N);
   HIPCHK(hipMalloc(&h->d_ray_cs, sizeof(h_ray_cs)));
@@ -2187,6 +2218,7 @@ static Params make_params(NascarHandle* h) {
   P.act_n = (float*)(a + h->off_n); P.env_time = (double*)(a + h->off_time); P.env_i32 = (int*)(a + h->off_ei32);
   P.blk_track = h->d_blk_track; P.blk_env = h->d_blk_env; P.tracks = h->d_tracks;
   P.pose = h->d_pose; P.pose_cs = h->d_pose_cs; P.ray_cs = h->d_ray_cs;
+  P.pose_cell = (int*)(h->d_pose + 2 * (size_t)h->N);
   return P;
 }
 
@@ -2387,6 +2419,7 @@ __global__ void debug_pose_kernel(Params P, const float* poses) {
   if (n >= P.N) return;
   const float a = poses[3 * n + 2];
   P.pose[n] = make_float4(poses[3 * n], poses[3 * n + 1], a, __int_as_float(PM_A_OBS));
+  P.pose_cell[n] = POSE_CELL_UNSET;
   double s0, c0;
   sincos((double)a, &s0, &c0);
   P.pose_cs[n] = make_double2(c0, s0);
