@@ -97,7 +97,16 @@ struct Params {
   // [N] beam-list base of pose A's cell, looked up by logic_kernel off the sensor kernel's critical path
   // (-1: no lists there); any value < -1 (POSE_CELL_UNSET): the sensor kernel looks it up itself
   int* pose_cell;
+  // block map shortcuts (prepare()): map_identity = blk_env[s] is s (< E) or -1, one_track >= 0 = every
+  // block's track; they spare each kernel's first dependent load
+  int map_identity, one_track;
 };
+__device__ __forceinline__ int blk_env_of(const Params& P, int el, int s) {
+  if (el >= P.epb) return -1;
+  if (P.map_identity) return s < P.E ? s : -1;
+  return P.blk_env[s];
+}
+__device__ __forceinline__ int blk_track_of(const Params& P, int b) { return P.one_track >= 0 ? P.one_track : P.blk_track[b]; }
 #define POSE_CELL_UNSET (-2)
 // Default: the sensor kernel looks its cell up itself.  -DRAY_LOGIC_CELL moves the lookup into logic_kernel
 // (measured 88.1 vs 86.4 us/step: logic_kernel's extra load and store cost more than the sensor saves).
@@ -959,8 +968,8 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(SENS
   const int C = P.C;
   const int slot = sub * CPW + lc;          // car slot within the step kernel's workgroup b
   const int el = slot / C, car = slot - el * C;
-  const int env = (el < P.epb) ? P.blk_env[b * P.epb + el] : -1;
-  const TrackDev T = P.tracks[P.blk_track[b]];
+  const int env = blk_env_of(P, el, b * P.epb + el);
+  const TrackDev T = P.tracks[blk_track_of(P, b)];
   const int nw = T.nwall, ng = T.ngroup;
 #ifdef SENSOR_GLOBAL_WALLS
   // walls and groups read straight from the track's global image (L1/L2-resident, shared by every
@@ -1229,8 +1238,26 @@ ray_sensor_kernel(Params P, float* obs, float* terminal_obs, int passes) {
   const int C = P.C;
   const int slot = sub * CPW + lc;
   const int el = slot / C, car = slot - el * C;
-  const int env = (el < P.epb) ? P.blk_env[b * P.epb + el] : -1;
-  const TrackDev& T = P.tracks[P.blk_track[b]];
+  const int env = blk_env_of(P, el, b * P.epb + el);
+  const TrackDev& T = P.tracks[blk_track_of(P, b)];
+  // the car's pose hand-off is requested before the wall staging below, so its round trip overlaps the
+  // staging's instead of following the barrier (RAY_LATE_POSE: after it)
+  const int n = env >= 0 ? env * C + car : 0;
+  int mode = 0;
+  float4 pa = make_float4(0.f, 0.f, 0.f, 0.f), pb = pa;
+  double2 csa = make_double2(0.0, 0.0);
+  int cell_a = POSE_CELL_UNSET;
+#ifndef RAY_LATE_POSE
+  if (env >= 0) {
+    if (passes & 1) {
+      pa = P.pose[n]; csa = P.pose_cs[n];
+#ifndef RAY_OWN_CELL
+      cell_a = P.pose_cell[n];
+#endif
+    }
+    if (passes & 2) pb = P.pose[P.N + n];
+  }
+#endif
 #ifdef RAY_LDS_WALLS
   {
     float4* s_w = (float4*)smem;
@@ -1240,17 +1267,17 @@ ray_sensor_kernel(Params P, float* obs, float* terminal_obs, int passes) {
   }
 #endif
   if (env < 0) return;
-  const int n = env * C + car;
-  int mode = 0;
-  float4 pa = make_float4(0.f, 0.f, 0.f, 0.f), pb = pa;
-  int cell_a = POSE_CELL_UNSET;
+#ifdef RAY_LATE_POSE
   if (passes & 1) {
-    pa = P.pose[n]; mode = __float_as_int(pa.w) & (PM_A_OBS | PM_A_TERM);
+    pa = P.pose[n]; csa = P.pose_cs[n];
 #ifndef RAY_OWN_CELL
     cell_a = P.pose_cell[n];
 #endif
   }
-  if (passes & 2) { pb = P.pose[P.N + n]; mode |= __float_as_int(pb.w) & PM_B_OBS; }
+  if (passes & 2) pb = P.pose[P.N + n];
+#endif
+  if (passes & 1) mode = __float_as_int(pa.w) & (PM_A_OBS | PM_A_TERM);
+  if (passes & 2) mode |= __float_as_int(pb.w) & PM_B_OBS;
   const BeamGrid G = T.beam;
 #ifdef RAY_LDS_WALLS
   const float4* __restrict__ sw = (const float4*)smem;   // the track's wall image staged per workgroup
@@ -1264,7 +1291,7 @@ ray_sensor_kernel(Params P, float* obs, float* terminal_obs, int passes) {
     const float4 ps = pass == 0 ? pa : pb;
     const V2 p1 = V(ps.x, ps.y);
     const double px = ps.x, py = ps.y, ang = ps.z;
-    const double2 cs = P.pose_cs[pass == 0 ? (size_t)n : (size_t)P.N + n];
+    const double2 cs = pass == 0 ? csa : P.pose_cs[(size_t)P.N + n];
     const int pc = pass == 0 ? cell_a : POSE_CELL_UNSET;
     const int base = pc >= -1 ? pc : beam_cell_base(G, p1.x, p1.y);
     // direction bin of sa = -radians(22.5 i) + ang (f64; the lists carry a 2e-3 rad guard) -> list slot
@@ -1371,30 +1398,39 @@ __global__ void __launch_bounds__(SBLOCK) __attribute__((amdgpu_waves_per_eu(MOD
   const int tid = threadIdx.x, C = P.C;
   const int el = tid / C, car = tid - el * C;
   const int slot = blockIdx.x * P.epb + el;
-  const int env = (el < P.epb) ? P.blk_env[slot] : -1;
+  const int env = blk_env_of(P, el, slot);
   const int n = env >= 0 ? env * C + car : 0;
   PROF_RT(14);
   PROF(0);
   __shared__ DSeg s_segs[MAX_SEG];
-  TrackDev T = P.tracks[P.blk_track[blockIdx.x]];
+  Car c;
+#ifndef MODEL_LATE_LOAD
+  // car state and action requested before the segment staging barrier (their round trips overlap the
+  // staging's instead of following it: 89 -> 84 us per step)
+  if (env >= 0) car_load_phys(P, n, c);
+#endif
+  // actions (BaseEnv._convert_to_internal_action / _discrete_to_continuous, np.float32)
+  float tb = 0.0f, st = 0.0f;
+  if (env >= 0) {
+    if (discrete) {
+      int a = ((const int*)actions)[n];
+      tb = a == 1 ? 1.0f : (a == 2 ? -1.0f : 0.0f);
+      st = a == 3 ? -1.0f : (a == 4 ? 1.0f : 0.0f);
+    } else {
+      tb = ((const float*)actions)[2 * n]; st = ((const float*)actions)[2 * n + 1];
+    }
+  }
+  TrackDev T = P.tracks[blk_track_of(P, blockIdx.x)];
   if (tid < T.nseg) s_segs[tid] = T.segs[tid];
   __syncthreads();
   T.segs = s_segs;
   PROF(1);
   if (env < 0) return;
   const WallSet S{T.walls, T.nwall, T.bp, T.sn};
-  Car c;
+#ifdef MODEL_LATE_LOAD
   car_load_phys(P, n, c);
+#endif
   PROF(2);
-  // actions (BaseEnv._convert_to_internal_action / _discrete_to_continuous, np.float32)
-  float tb, st;
-  if (discrete) {
-    int a = ((const int*)actions)[n];
-    tb = a == 1 ? 1.0f : (a == 2 ? -1.0f : 0.0f);
-    st = a == 3 ? -1.0f : (a == 4 ? 1.0f : 0.0f);
-  } else {
-    tb = ((const float*)actions)[2 * n]; st = ((const float*)actions)[2 * n + 1];
-  }
   float a0, a1, a2 = st;
   if (tb >= 0) { a0 = tb; a1 = 0.0f; } else { a0 = 0.0f; a1 = -tb; }
   if (c.disabled) { a0 = 0.0f; a1 = 0.0f; a2 = 0.0f; }
@@ -1421,7 +1457,7 @@ __global__ void __launch_bounds__(SBLOCK) logic_kernel(Params P, float* obs, flo
   const int tid = threadIdx.x, C = P.C;
   const int el = tid / C, car = tid - el * C;
   const int slot = blockIdx.x * P.epb + el;
-  const int env = (el < P.epb) ? P.blk_env[slot] : -1;
+  const int env = blk_env_of(P, el, slot);
   const int n = env >= 0 ? env * C + car : 0;
   LPROF(0);
   __shared__ DSeg s_segs[MAX_SEG];
@@ -1437,7 +1473,7 @@ __global__ void __launch_bounds__(SBLOCK) logic_kernel(Params P, float* obs, flo
     car_load_logic(P, n, c);
     sim = P.env_time[env];
   }
-  TrackDev T = P.tracks[P.blk_track[blockIdx.x]];
+  TrackDev T = P.tracks[blk_track_of(P, blockIdx.x)];
 #ifndef RAY_OWN_CELL
   // the sensor kernel's beam cell of this step's pose (pose A = the body position model_kernel stored):
   // its round trip overlaps this kernel instead of sitting on the sensor kernel's dependent chain
@@ -1631,9 +1667,9 @@ __global__ void __launch_bounds__(SBLOCK) reset_kernel(Params P, const uint8_t* 
   const int tid = threadIdx.x, C = P.C;
   const int el = tid / C, car = tid - el * C;
   const int slot = blockIdx.x * P.epb + el;
-  int env = (el < P.epb) ? P.blk_env[slot] : -1;
+  int env = blk_env_of(P, el, slot);
   if (env >= 0 && mask && !mask[env]) { P.pose[env * C + car] = make_float4(0.f, 0.f, 0.f, __int_as_float(0)); env = -1; }
-  const TrackDev T = P.tracks[P.blk_track[blockIdx.x]];
+  const TrackDev T = P.tracks[blk_track_of(P, blockIdx.x)];
   const WallSet S{T.walls, T.nwall, T.bp, T.sn};
   if (env >= 0) {
     const int n = env * C + car;
@@ -1659,8 +1695,8 @@ __global__ void __launch_bounds__(SBLOCK) info_kernel(Params P, double* info) {
   const int tid = threadIdx.x, C = P.C;
   const int el = tid / C, car = tid - el * C;
   const int slot = blockIdx.x * P.epb + el;
-  const int env = (el < P.epb) ? P.blk_env[slot] : -1;
-  const TrackDev T = P.tracks[P.blk_track[blockIdx.x]];
+  const int env = blk_env_of(P, el, slot);
+  const TrackDev T = P.tracks[blk_track_of(P, blockIdx.x)];
   const WallSet S{T.walls, T.nwall, T.bp, T.sn};
   if (env < 0) return;
   const int n = env * C + car;
@@ -1998,6 +2034,7 @@ struct NascarHandle {
   std::vector<HostTrack> tracks;
   TrackDev* d_tracks = nullptr;
   int* d_blk_track = nullptr; int* d_blk_env = nullptr; int nblocks = 0;
+  int map_identity = 0, one_track = -1;   // Params shortcuts of the block map (prepare)
   std::vector<int> env_track;
   double* d_ctl = nullptr;   // rule-driver state for nascar_policy_actions
   float4* d_pose = nullptr;  // [2][N] step/reset -> sensor_kernel hand-off
@@ -2197,6 +2234,12 @@ static int prepare(NascarHandle* h) {
     }
   }
   h->nblocks = (int)blk_track.size();
+  h->map_identity = 1;
+  for (size_t s = 0; s < blk_env.size(); ++s)
+    if (blk_env[s] != ((int)s < h->E ? (int)s : -1)) { h->map_identity = 0; break; }
+  h->one_track = blk_track.empty() ? -1 : blk_track[0];
+  for (int tr : blk_track) if (tr != h->one_track) { h->one_track = -1; break; }
+  if (getenv("NASCAR_NO_MAP_SHORTCUT")) { h->map_identity = 0; h->one_track = -1; }   // A/B and tests
   hipFree(h->d_blk_track); hipFree(h->d_blk_env);
   HIPCHK(hipMalloc(&h->d_blk_track, sizeof(int) * blk_track.size()));
   HIPCHK(hipMalloc(&h->d_blk_env, sizeof(int) * blk_env.size()));
@@ -2217,6 +2260,7 @@ static Params make_params(NascarHandle* h) {
   P.acc = (double*)(a + h->off_acc); P.ct = (DContact*)(a + h->off_ct); P.act_key = (int*)(a + h->off_key);
   P.act_n = (float*)(a + h->off_n); P.env_time = (double*)(a + h->off_time); P.env_i32 = (int*)(a + h->off_ei32);
   P.blk_track = h->d_blk_track; P.blk_env = h->d_blk_env; P.tracks = h->d_tracks;
+  P.map_identity = h->map_identity; P.one_track = h->one_track;
   P.pose = h->d_pose; P.pose_cs = h->d_pose_cs; P.ray_cs = h->d_ray_cs;
   P.pose_cell = (int*)(h->d_pose + 2 * (size_t)h->N);
   return P;
