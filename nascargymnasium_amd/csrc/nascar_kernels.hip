@@ -1468,9 +1468,14 @@ __global__ void __launch_bounds__(SBLOCK) logic_kernel(Params P, float* obs, flo
   __shared__ float s_rll[MAX_SEG];
   Car c;
   double sim = 0.0;
+  int pend_in = 0, reason_in = 0;   // env state read by the env passes (car 0's lane), fetched up front
   if (env >= 0) {   // state loads issued before the segment staging barrier (independent round trips)
     car_load_body(P, n, c);
     car_load_logic(P, n, c);
+#ifndef LOGIC_LATE_LOADS
+    car_reload_tyres(P, n, c);
+    if (car == 0) { pend_in = P.env_i32[E_PENDING * P.E + env]; reason_in = P.env_i32[E_REASON * P.E + env]; }
+#endif
     sim = P.env_time[env];
   }
   TrackDev T = P.tracks[blk_track_of(P, blockIdx.x)];
@@ -1515,8 +1520,12 @@ __global__ void __launch_bounds__(SBLOCK) logic_kernel(Params P, float* obs, flo
   __syncthreads();
   // env pass 1: lap-reset pending (src/car_env.py:672-676 with _all_active_cars_completed_lap :1640-1669,
   // evaluated in car order with cars > i not yet updated)
+  int pend_env = 0;
   if (env >= 0 && car == 0) {
-    int pend = P.env_i32[E_PENDING * P.E + env];
+#ifdef LOGIC_LATE_LOADS
+    pend_in = P.env_i32[E_PENDING * P.E + env]; reason_in = P.env_i32[E_REASON * P.E + env];
+#endif
+    int pend = pend_in;
     if (P.reset_on_lap) {
       const int b = tid;
       for (int i = 0; i < C; ++i) {
@@ -1533,6 +1542,7 @@ __global__ void __launch_bounds__(SBLOCK) logic_kernel(Params P, float* obs, flo
       }
     }
     P.env_i32[E_PENDING * P.E + env] = pend;
+    pend_env = pend;
   }
   float o[22];
   float rew = 0.0f;
@@ -1554,7 +1564,9 @@ __global__ void __launch_bounds__(SBLOCK) logic_kernel(Params P, float* obs, flo
       } else { c.stuck_dur = 0.0; c.has_stuck_start = 0; }
     }
     LPROF(3);
+#ifdef LOGIC_LATE_LOADS
     car_reload_tyres(P, n, c);
+#endif
     car_obs(c, o);
     LPROF(4);
     // _calculate_multi_rewards (src/car_env.py:980-1113)
@@ -1596,15 +1608,15 @@ __global__ void __launch_bounds__(SBLOCK) logic_kernel(Params P, float* obs, flo
   __syncthreads();
   // env pass 2: termination (src/car_env.py:1115-1158, 791-794)
   if (env >= 0 && car == 0) {
-    const double st = P.env_time[env] + P.dt_d;
+    const double st = sim + P.dt_d;   // env_time is written only here
     P.env_time[env] = st;
-    int ndis = 0, active = 0, below = 0, term = 0, trunc = 0, reason = P.env_i32[E_REASON * P.E + env];
+    int ndis = 0, active = 0, below = 0, term = 0, trunc = 0, reason = reason_in;
     for (int j = 0; j < C; ++j) { ndis += s_dis_final[tid + j]; if (!s_dis_final[tid + j]) { active++; below += s_below[tid + j]; } }
     if (ndis >= C) { term = 1; reason = 1; }
     else if (active > 0 && below == active) { term = 1; reason = 2; }
     else if (P.reset_on_lap && st > 60.0) { term = 1; reason = 3; }
     else if (st > 180.0) { trunc = 1; reason = 4; }
-    if (P.env_i32[E_PENDING * P.E + env]) { P.env_i32[E_PENDING * P.E + env] = 0; term = 1; }
+    if (pend_env) { P.env_i32[E_PENDING * P.E + env] = 0; term = 1; }   // pass 1's value (same lane)
     P.env_i32[E_REASON * P.E + env] = reason;
     P.env_i32[E_TERMINATED * P.E + env] = term;
     P.env_i32[E_TRUNCATED * P.E + env] = trunc;
