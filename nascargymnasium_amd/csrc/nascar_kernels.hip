@@ -1262,6 +1262,21 @@ ray_sensor_kernel(Params P, float* obs, float* terminal_obs, int passes) {
   {
     float4* s_w = (float4*)smem;
     const int nw2 = 2 * T.nwall;
+#ifdef RAY_EARLY_CELL   // measured slower: 92.5 vs 83.2 us/step (the staged float4s held in registers)
+    constexpr int SWQ = 6;   // wall-image float4s per thread held in registers (tracks up to 768 walls)
+    if (nw2 <= SWQ * BLOCK) {
+      // staging loads issued, then pass A's beam cell looked up while they are in flight, then the LDS
+      // stores: the cell round trip leaves the post-barrier chain
+      float4 sv[SWQ];
+#pragma unroll
+      for (int q = 0; q < SWQ; ++q) if (t + q * BLOCK < nw2) sv[q] = T.swall[t + q * BLOCK];
+#ifndef RAY_LATE_POSE
+      if (env >= 0 && (passes & 1) && cell_a < -1) cell_a = beam_cell_base(T.beam, pa.x, pa.y);
+#endif
+#pragma unroll
+      for (int q = 0; q < SWQ; ++q) if (t + q * BLOCK < nw2) s_w[t + q * BLOCK] = sv[q];
+    } else
+#endif
     for (int k = t; k < nw2; k += BLOCK) s_w[k] = T.swall[k];
     __syncthreads();
   }
