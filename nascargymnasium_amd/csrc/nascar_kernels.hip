@@ -1240,59 +1240,28 @@ ray_sensor_kernel(Params P, float* obs, float* terminal_obs, int passes) {
   const int el = slot / C, car = slot - el * C;
   const int env = blk_env_of(P, el, b * P.epb + el);
   const TrackDev& T = P.tracks[blk_track_of(P, b)];
-  // the car's pose hand-off is requested before the wall staging below, so its round trip overlaps the
-  // staging's instead of following the barrier (RAY_LATE_POSE: after it)
-  const int n = env >= 0 ? env * C + car : 0;
-  int mode = 0;
-  float4 pa = make_float4(0.f, 0.f, 0.f, 0.f), pb = pa;
-  double2 csa = make_double2(0.0, 0.0);
-  int cell_a = POSE_CELL_UNSET;
-#ifndef RAY_LATE_POSE
-  if (env >= 0) {
-    if (passes & 1) {
-      pa = P.pose[n]; csa = P.pose_cs[n];
-#ifndef RAY_OWN_CELL
-      cell_a = P.pose_cell[n];
-#endif
-    }
-    if (passes & 2) pb = P.pose[P.N + n];
-  }
-#endif
 #ifdef RAY_LDS_WALLS
   {
     float4* s_w = (float4*)smem;
     const int nw2 = 2 * T.nwall;
-#ifdef RAY_EARLY_CELL   // measured slower: 92.5 vs 83.2 us/step (the staged float4s held in registers)
-    constexpr int SWQ = 6;   // wall-image float4s per thread held in registers (tracks up to 768 walls)
-    if (nw2 <= SWQ * BLOCK) {
-      // staging loads issued, then pass A's beam cell looked up while they are in flight, then the LDS
-      // stores: the cell round trip leaves the post-barrier chain
-      float4 sv[SWQ];
-#pragma unroll
-      for (int q = 0; q < SWQ; ++q) if (t + q * BLOCK < nw2) sv[q] = T.swall[t + q * BLOCK];
-#ifndef RAY_LATE_POSE
-      if (env >= 0 && (passes & 1) && cell_a < -1) cell_a = beam_cell_base(T.beam, pa.x, pa.y);
-#endif
-#pragma unroll
-      for (int q = 0; q < SWQ; ++q) if (t + q * BLOCK < nw2) s_w[t + q * BLOCK] = sv[q];
-    } else
-#endif
     for (int k = t; k < nw2; k += BLOCK) s_w[k] = T.swall[k];
     __syncthreads();
   }
 #endif
   if (env < 0) return;
-#ifdef RAY_LATE_POSE
+  // pose loads after the staging barrier: issuing them (and pass A's cos/sin) before it, or the beam-cell
+  // lookup too, measured 2.5 / 9 us slower (registers held across the staging)
+  const int n = env * C + car;
+  int mode = 0;
+  float4 pa = make_float4(0.f, 0.f, 0.f, 0.f), pb = pa;
+  int cell_a = POSE_CELL_UNSET;
   if (passes & 1) {
-    pa = P.pose[n]; csa = P.pose_cs[n];
+    pa = P.pose[n]; mode = __float_as_int(pa.w) & (PM_A_OBS | PM_A_TERM);
 #ifndef RAY_OWN_CELL
     cell_a = P.pose_cell[n];
 #endif
   }
-  if (passes & 2) pb = P.pose[P.N + n];
-#endif
-  if (passes & 1) mode = __float_as_int(pa.w) & (PM_A_OBS | PM_A_TERM);
-  if (passes & 2) mode |= __float_as_int(pb.w) & PM_B_OBS;
+  if (passes & 2) { pb = P.pose[P.N + n]; mode |= __float_as_int(pb.w) & PM_B_OBS; }
   const BeamGrid G = T.beam;
 #ifdef RAY_LDS_WALLS
   const float4* __restrict__ sw = (const float4*)smem;   // the track's wall image staged per workgroup
@@ -1306,7 +1275,7 @@ ray_sensor_kernel(Params P, float* obs, float* terminal_obs, int passes) {
     const float4 ps = pass == 0 ? pa : pb;
     const V2 p1 = V(ps.x, ps.y);
     const double px = ps.x, py = ps.y, ang = ps.z;
-    const double2 cs = pass == 0 ? csa : P.pose_cs[(size_t)P.N + n];
+    const double2 cs = P.pose_cs[pass == 0 ? (size_t)n : (size_t)P.N + n];
     const int pc = pass == 0 ? cell_a : POSE_CELL_UNSET;
     const int base = pc >= -1 ? pc : beam_cell_base(G, p1.x, p1.y);
     // direction bin of sa = -radians(22.5 i) + ang (f64; the lists carry a 2e-3 rad guard) -> list slot
