@@ -417,7 +417,8 @@ __device__ inline void update_friction(Car& c, double df) {
 __device__ __forceinline__ V2 OV(double x, double y) { return V((float)x, (float)y); }
 
 // Car.update_physics (src/car.py:329-387) and helpers (:389-892)
-__device__ inline void car_update_physics(const Params& P, Car& c, int n, const TrackDev& T) {
+__device__ inline void car_update_physics(const Params& P, Car& c, int n, const TrackDev& T,
+                                          const uint32_t* s_acc = nullptr) {
   const double dt = P.dt_d;
   c.thr = c.thr_in; c.brk = c.brk_in; c.steer = c.str_in * (45.0 * RAD_PER_DEG);
   {
@@ -498,8 +499,18 @@ __device__ inline void car_update_physics(const Params& P, Car& c, int n, const 
     double* acc = P.acc;
     const size_t N = P.N;
     double hl[10], ht[10];
+    if (s_acc) {   // copied into LDS by model_kernel at launch (dword k of slot r = k / 2 at s_acc[k][tid])
+      __builtin_amdgcn_s_waitcnt(0);   // the LDS-DMA copies have landed
+      const int tid = threadIdx.x;
 #pragma unroll
-    for (int q = 0; q < 10; ++q) { hl[q] = acc[(size_t)(2 * q) * N + n]; ht[q] = acc[(size_t)(2 * q + 1) * N + n]; }
+      for (int q = 0; q < 10; ++q) {
+        hl[q] = __hiloint2double((int)s_acc[(4 * q + 1) * SBLOCK + tid], (int)s_acc[(4 * q) * SBLOCK + tid]);
+        ht[q] = __hiloint2double((int)s_acc[(4 * q + 3) * SBLOCK + tid], (int)s_acc[(4 * q + 2) * SBLOCK + tid]);
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < 10; ++q) { hl[q] = acc[(size_t)(2 * q) * N + n]; ht[q] = acc[(size_t)(2 * q + 1) * N + n]; }
+    }
     if (c.acc_len == 10) {
 #pragma unroll
       for (int q = 0; q < 9; ++q) { hl[q] = hl[q + 1]; ht[q] = ht[q + 1]; }
@@ -1404,6 +1415,20 @@ __global__ void __launch_bounds__(SBLOCK) __attribute__((amdgpu_waves_per_eu(MOD
       tb = ((const float*)actions)[2 * n]; st = ((const float*)actions)[2 * n + 1];
     }
   }
+#ifdef MODEL_ACC_LDS   // measured slower: model_kernel 21.8 vs 20.8 us
+  // the 10-sample acceleration history (20 f64 = 40 dwords per car, read mid-way through the vehicle
+  // model) copied HBM -> LDS at launch (global_load_lds, no registers held): its round trip overlaps the
+  // staging below instead of stalling the f64 chain
+  __shared__ uint32_t s_acc[40 * SBLOCK];
+  if (env >= 0) {
+    const uint32_t* accw = (const uint32_t*)P.acc;
+    const int wb = tid & ~63;
+#pragma unroll
+    for (int k = 0; k < 40; ++k)
+      __builtin_amdgcn_global_load_lds((const void*)(accw + 2 * ((size_t)(k >> 1) * P.N + n) + (k & 1)),
+                                       (__attribute__((address_space(3))) void*)(s_acc + k * SBLOCK + wb), 4, 0, 0);
+  }
+#endif
   TrackDev T = P.tracks[blk_track_of(P, blockIdx.x)];
   if (tid < T.nseg) s_segs[tid] = T.segs[tid];
   __syncthreads();
@@ -1421,7 +1446,11 @@ __global__ void __launch_bounds__(SBLOCK) __attribute__((amdgpu_waves_per_eu(MOD
   c.thr_in = pymax(0.0, pymin(1.0, (double)a0));
   c.brk_in = pymax(0.0, pymin(1.0, (double)a1));
   c.str_in = pymax(-1.0, pymin(1.0, (double)a2));
+#ifdef MODEL_ACC_LDS
+  car_update_physics(P, c, n, T, s_acc);
+#else
   car_update_physics(P, c, n, T);
+#endif
   car_store_model(P, n, c);
   asm volatile("" ::: "memory");   // keep the model write-back ahead of the Box2D step (register pressure)
   PROF(3);
