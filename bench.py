@@ -1,14 +1,23 @@
 """Benchmark: batched CarEnv.step throughput (car-steps/s = envs x cars x steps / s).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--envs E] [--cars C] [--track daytona]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--envs E] [--cars C] [--track daytona] [--policy noisy]
     torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU, weak scaling)
 
-Workload (BASELINE.json metric "env-steps/sec (cars x envs), daytona 10-car"): E=8192 envs x C=10
-cars on daytona.track per GPU, synthetic uniform U[-1,1]^2 actions pre-generated in HBM, SB3-style
-auto-reset on done.  A "step" = one fused kernel launch over all E*C cars of a rank.
+Headline workload (BASELINE.json metric "env-steps/sec (cars x envs), daytona 10-car"; SURVEY.md 8(d) action
+source (B)): E=8192 envs x C=10 cars on daytona.track per GPU, driven closed loop by the on-device noisy rule
+driver (BaseController._fallback_control, game/control/base_controller.py:39-103, with 15 % of car-steps
+replaced by a counter-hash uniform action), SB3-style auto-reset.  Before timing, the envs are SETTLED to a
+steady state: 10 800 steps (one 180 s episode) during which env e is reset at a staggered step, so that the
+env ages at the start of the timed window are spread uniformly over the episode -- cars are spread round the
+track, touch walls, complete laps, get disabled and auto-reset inside the timed window (the rates are reported
+in `workload_stats`).  A "step" = the driver's policy kernel + one env step (model_kernel, logic_kernel,
+ray_sensor_kernel) over all E*C cars of a rank.  The uniform-U[-1,1]^2-from-reset number of round 1 is kept
+only as the labelled secondary field `uniform_from_reset`.
 Prints ONE JSON line on rank 0 (schema: see DESIGN.md "Measurement").
 """
 import argparse
+import glob
+import hashlib
 import json
 import os
 import sys
@@ -19,28 +28,48 @@ sys.path.insert(0, ROOT)
 
 ALGO_BYTES_PER_CAR_STEP = 1221      # 2 x 528 B state + 8 B action + 152 B obs + 4 B reward + 1 B flags
 HBM_PEAK_GBS = 8000.0               # MI355X HBM3E spec (MI355X_MICROARCH.md)
+EPISODE_STEPS = 10800               # 180 s time limit at dt = 1/60 (src/car_env.py:1154)
+POLICY_ID = {"uniform": 0, "driver": 1, "sac": 2, "noisy": 3}
+POLICY_TEXT = {"uniform": "uniform U[-1,1]^2 actions resident in HBM",
+               "driver": "on-device rule driver (BaseController._fallback_control), closed loop",
+               "noisy": "on-device noisy rule driver (BaseController._fallback_control, 15% of car-steps "
+                        "uniform), closed loop",
+               "sac": "fused SAC actor (random-init weights of the reference architecture), closed loop"}
+
+
+def source_sha():
+    """sha256 over the HIP sources: tags the PMC traffic file so a stale one is never reported as current."""
+    h = hashlib.sha256()
+    for p in sorted(glob.glob(os.path.join(ROOT, "nascargymnasium_amd", "csrc", "*"))):
+        h.update(open(p, "rb").read())
+    return h.hexdigest()[:16]
 
 
 def _oracle_shard(track, cars, E, seed, budget_s, out, slot):
-    """One host thread: its own OracleEnv shard of E envs x C cars, uniform actions, ~budget_s of stepping
+    """One host thread: its own OracleEnv shard of E envs x C cars driven by the host restatement of the
+    noisy rule driver (tests/drivers.py, same counter hash as the device), auto-reset, ~budget_s of stepping
     (the oracle's C step releases the GIL inside ctypes, so shards on threads run in parallel)."""
     import numpy as np
+    from drivers import NoisyRuleDriver
     from oracle_lib import OracleEnv
     env = OracleEnv(track, E, cars)
-    env.reset()
-    acts = np.random.default_rng(seed).uniform(-1, 1, (64, E, cars, 2)).astype(np.float32)
+    obs = env.reset()[0]
+    drv = NoisyRuleDriver(E * cars, seed)
     steps, t0 = 0, time.perf_counter()
     while time.perf_counter() - t0 < budget_s:
-        env.step(acts[steps % 64])
+        obs, _, _, ef = env.step(drv.actions(obs, steps))
+        for e in np.nonzero((ef[:, 0] != 0) | (ef[:, 1] != 0))[0]:
+            env.reset(int(e))
+            obs = env.outputs()[0]
         steps += 1
-    out[slot] = (E * cars * steps, time.perf_counter() - t0)
+    out[slot] = (E * cars * steps, time.perf_counter() - t0, steps)
     env.close()
 
 
 def cpu_baseline(track, cars, budget_s=12.0, threads=None):
     """The CPU oracle (C restatement of the reference path) on a bounded sample of the same workload:
-    16 envs x C cars per shard, uniform actions.  First 1 thread for budget_s / 2, then one shard per
-    host thread (threads = the box's CPU share, at most 16) for budget_s / 2 of wall time; `value` is the
+    16 envs x C cars per shard, noisy rule driver from reset.  First 1 thread for budget_s / 2, then one shard
+    per host thread (threads = the box's CPU share, at most 16) for budget_s / 2 of wall time; `value` is the
     multi-thread rate (car-steps over the slowest shard's time), the 1-thread rate is in `sample`."""
     import threading
     sys.path.insert(0, os.path.join(ROOT, "tests"))
@@ -59,7 +88,8 @@ def cpu_baseline(track, cars, budget_s=12.0, threads=None):
     rate = sum(r[0] for r in res) / max(r[1] for r in res)
     return {"value": rate, "unit": "car-steps/s", "cores": threads, "kind": "port",
             "sample": f"oracle (C restatement of the reference path incl. Box2D subset) on {os.path.basename(track)}, "
-                      f"uniform actions: {threads} host threads x one shard of {E} envs x {cars} cars, "
+                      f"noisy rule driver from reset (first ~{min(r[2] for r in res)} steps; the CPU cannot afford "
+                      f"the GPU run's 10 800-step settle): {threads} host threads x one shard of {E} envs x {cars} cars, "
                       f"~{budget_s / 2:.0f} s each; 1 thread alone: {rate1:.0f} car-steps/s"}
 
 
@@ -75,9 +105,102 @@ def reduce_max(values, device):
     return [float(x) for x in t.tolist()]
 
 
+def reduce_sum(values, device):
+    import torch
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return [float(v) for v in values]
+    t = torch.tensor([float(v) for v in values], device=device, dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return [float(x) for x in t.tolist()]
+
+
 def throughput(world, envs, cars, steps, elapsed_max):
     """whole-job car-steps/s under weak scaling: every rank steps its own envs x cars."""
     return world * envs * cars * steps / elapsed_max
+
+
+def stagger_schedule(E, settle):
+    """settle step at which env e is reset so that its age when timing starts is floor(e * 10800 / E) steps
+    (ages spread uniformly over one episode); envs whose age would exceed the settle length are not reset."""
+    import numpy as np
+    age = (np.arange(E, dtype=np.int64) * EPISODE_STEPS) // E
+    at = settle - age
+    return np.where(age < settle, at, -1)
+
+
+class Stepper:
+    """one bench step on a BatchedCarEnv: actions from the chosen source, then the env step with auto-reset."""
+
+    def __init__(self, env, policy, seed, acts=None, gather=None):
+        self.env, self.pol, self.seed, self.acts, self.gather = env, POLICY_ID[policy], seed, acts, gather
+
+    def actions(self, i):
+        if self.acts is not None:
+            return self.acts[i % self.acts.shape[0]]
+        return self.env.policy_actions(self.pol, seed=self.seed, step=i)
+
+    def __call__(self, i):
+        a = self.actions(i)
+        self.env.launch_step(a, auto_reset=True)
+        if self.gather is not None:
+            self.gather.push(self.env.obs, self.env.reward, self.env.car_flags, self.env.env_flags)
+
+
+def settle(env, step, n, stagger, dev):
+    """bring the envs to the steady state of the workload (not timed): n closed-loop steps, env e reset at
+    its staggered step."""
+    import torch
+    if n <= 0:
+        return
+    at = stagger_schedule(env.E, n) if stagger else None
+    at_dev = torch.from_numpy(at).to(dev) if stagger else None
+    steps_with_reset = set(int(x) for x in at[at >= 0]) if stagger else set()
+    for k in range(n):
+        if k in steps_with_reset:
+            env.reset((at_dev == k).to(torch.uint8))
+        step(k)
+
+
+def timed(step, first, K, world):
+    import torch
+    import torch.distributed as dist
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    # K steps back to back (no per-step events: each event record costs ~5 us of device time between kernels
+    # on this stack, which would be charged to the throughput)
+    t0 = time.perf_counter()
+    for i in range(first, first + K):
+        step(i)
+    if step.gather is not None:
+        step.gather.wait()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    return time.perf_counter() - t0
+
+
+def stats_pass(env, step, first, KR):
+    """after the timed region, KR further steps of the same workload: HIP events on the launch stream around
+    each env step (model_kernel + logic_kernel + ray_sensor_kernel; the policy kernel is outside the
+    brackets) for the roofline, and device-side tallies of what happened in those car-steps."""
+    import torch
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(KR)]
+    tally = torch.zeros(7, dtype=torch.float64, device=env.device)
+    for i in range(KR):
+        a = step.actions(first + i)
+        ev[i][0].record()
+        env.launch_step(a, auto_reset=True)
+        ev[i][1].record()
+        cf, ef = env.car_flags, env.env_flags
+        tally += torch.stack([((cf & 4) != 0).sum(), ((cf & 8) != 0).sum(), ((cf & 1) != 0).sum(),
+                              ((cf & 2) != 0).sum(), ((ef & 8) != 0).sum(), ((cf & 128) != 0).sum(),
+                              env.obs[..., 4].double().sum()]).double()
+    torch.cuda.synchronize()
+    kern_ms = sum(s.elapsed_time(e) for s, e in ev) / KR
+    return kern_ms, tally.tolist()
 
 
 def main():
@@ -88,13 +211,20 @@ def main():
     ap.add_argument("--envs", type=int, default=8192)
     ap.add_argument("--cars", type=int, default=10)
     ap.add_argument("--track", default="daytona")
-    ap.add_argument("--policy", default="uniform", choices=["uniform", "driver", "sac"],
-                    help="uniform: U[-1,1]^2 resident in HBM; driver: device rule driver; sac: fused SAC actor "
-                         "(random-init weights of the reference architecture) on the previous observation")
+    ap.add_argument("--policy", default="noisy", choices=list(POLICY_ID),
+                    help="noisy (default): device noisy rule driver; driver: device rule driver; uniform: U[-1,1]^2 "
+                         "resident in HBM; sac: fused SAC actor (random-init weights) on the previous observation")
+    ap.add_argument("--settle", type=int, default=None,
+                    help="closed-loop steps run before the warm-up to reach the steady state (default 10800 for the "
+                         "closed-loop policies, 0 for uniform)")
+    ap.add_argument("--no-stagger", action="store_true", help="all envs start together (no staggered resets)")
+    ap.add_argument("--save-state", default=None, help="write the settled state (engine arena + obs) to this file")
+    ap.add_argument("--load-state", default=None, help="start from a state written by --save-state (no settle)")
     ap.add_argument("--mixed", action="store_true", help="env e on track e mod 8 of the sorted bundled tracks "
                     "(BASELINE cfg5: mixed batch, divergent geometry); --track is ignored")
     ap.add_argument("--gather", action="store_true", help="gather every step's obs/reward/flags of all ranks to "
                     "rank 0 (RCCL, side stream; BASELINE cfg4 single-learner layout)")
+    ap.add_argument("--no-secondary", action="store_true", help="skip the uniform-from-reset secondary measurement")
     ap.add_argument("--cpu-threads", type=int, default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
@@ -113,13 +243,20 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     E, C, K, W = args.envs, args.cars, args.steps, args.warmup
+    closed = args.policy != "uniform"
+    S = args.settle if args.settle is not None else (EPISODE_STEPS if closed else 0)
+    if args.load_state:
+        S = 0
     tpath = track_path(args.track)
-    if args.mixed:
-        from nascargymnasium_amd.track import available_tracks
-        names = available_tracks()
-        env = BatchedCarEnv(E, C, [names[e % len(names)] for e in range(E)], device=dev)
-    else:
-        env = BatchedCarEnv(E, C, tpath, device=dev)
+
+    def make_env():
+        if args.mixed:
+            from nascargymnasium_amd.track import available_tracks
+            names = available_tracks()
+            return BatchedCarEnv(E, C, [names[e % len(names)] for e in range(E)], device=dev)
+        return BatchedCarEnv(E, C, tpath, device=dev)
+
+    env = make_env()
     gather = None
     if args.gather:
         from nascargymnasium_amd.gather import ObsGather
@@ -128,76 +265,93 @@ def main():
         from nascargymnasium_amd.policy import random_actor
         env.set_actor(random_actor(rank))
     env.reset()
-    gen = torch.Generator(device=dev)
-    gen.manual_seed(1234 + rank)
+    acts = None
     if args.policy == "uniform":
+        gen = torch.Generator(device=dev)
+        gen.manual_seed(1234 + rank)
         acts = torch.rand((W + K, E, C, 2), generator=gen, device=dev) * 2 - 1     # resident before timing
+    step = Stepper(env, args.policy, rank, acts, None)
+    t_settle = time.perf_counter()
+    if args.load_state:
+        blob = torch.load(args.load_state, map_location=dev, weights_only=True)
+        env.set_state(blob["state"])
+        env.obs.copy_(blob["obs"])
+        base = int(blob["step"])
+    else:
+        settle(env, step, S, closed and not args.no_stagger, dev)
+        base = S
     torch.cuda.synchronize()
-
-    pol = {"driver": 1, "sac": 2}.get(args.policy)
-
-    def one_step(i):
-        a = acts[i] if args.policy == "uniform" else env.policy_actions(pol, seed=rank, step=i)
-        env.launch_step(a, auto_reset=True)
-        if gather is not None:
-            gather.push(env.obs, env.reward, env.car_flags, env.env_flags)
-
-    for i in range(W):
-        one_step(i)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    # timed region: K steps back to back (no per-step events: each event record costs ~5 us of device
-    # time between kernels on this stack, which would be charged to the throughput)
-    t0 = time.perf_counter()
-    for i in range(W, W + K):
-        one_step(i)
-    if gather is not None:
-        gather.wait()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    # roofline pass (after the timed region): HIP events on the launch stream around each env step's
-    # kernels (model_kernel + logic_kernel + sensor_kernel), averaged over KR further steps
+    t_settle = time.perf_counter() - t_settle
+    if args.save_state:
+        torch.save({"state": env.get_state().cpu(), "obs": env.obs.cpu(), "step": base}, args.save_state)
+    step.gather = gather
+    for i in range(base, base + W):
+        step(i)
+    elapsed = timed(step, base + W, K, world)
     KR = min(K, 50)
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(KR)]
-    for i in range(KR):
-        a = acts[W + i] if args.policy == "uniform" else env.policy_actions(pol, seed=rank, step=W + K + i)
-        ev[i][0].record()
-        env.launch_step(a, auto_reset=True)
-        ev[i][1].record()
-    torch.cuda.synchronize()
-    kern_ms = sum(s.elapsed_time(e) for s, e in ev) / KR
-    errs = int(((env.car_flags & 128) != 0).sum().item())
+    kern_ms, tally = stats_pass(env, step, base + W + K, KR)
     elapsed, kern_ms = reduce_max([elapsed, kern_ms], dev)
+    tally = reduce_sum(tally, dev)
     value = throughput(world, E, C, K, elapsed)
     achieved = E * C * ALGO_BYTES_PER_CAR_STEP / (kern_ms * 1e-3) / 1e9
-    traffic = None
+    traffic, tnote = None, "no PMC file for this workload"
     tfile = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if os.path.exists(tfile):
-        try:
-            tj = json.load(open(tfile))
-            if tj.get("envs") == E and tj.get("cars") == C and tj.get("track") == os.path.basename(tpath):
-                traffic = tj.get("bytes_per_step")
-        except Exception:
-            traffic = None
+        tj = json.load(open(tfile))
+        same = (tj.get("envs") == E and tj.get("cars") == C and tj.get("track") == os.path.basename(tpath)
+                and tj.get("policy", "uniform") == args.policy and not args.mixed)
+        if not same:
+            tnote = f"profiles/pmc_traffic.json is for another workload ({tj.get('tag')})"
+        elif tj.get("source_sha") != source_sha():
+            tnote = f"stale: profiles/pmc_traffic.json ({tj.get('tag')}) was measured on other kernel sources"
+        else:
+            traffic = tj["bytes_per_step"]
+            tnote = f"rocprofv3 FETCH_SIZE/WRITE_SIZE passes of this build and workload ({tj.get('tag')}, " \
+                    f"profiles/pmc_traffic.json; not re-measured in this run)"
+    ncs = world * E * C * KR
+    wstats = {"source": POLICY_TEXT[args.policy], "settle_steps": S if not args.load_state else f"state file {args.load_state}",
+              "staggered_env_ages": closed and not args.no_stagger, "window_car_steps": ncs,
+              "contact_frac": tally[0] / ncs, "lap_completed_frac": tally[1] / ncs, "disabled_frac": tally[2] / ncs,
+              "just_disabled_frac": tally[3] / ncs, "env_reset_frac": tally[4] / (world * E * KR),
+              "mean_speed_ms": tally[6] / ncs * 111.1, "settle_s": t_settle}
+    track_name = "mixed 8-track" if args.mixed else os.path.basename(tpath)[:-6]
+    settle_txt = (f", steady state after {S} settle steps" + (" (env ages staggered over the 180 s episode)"
+                  if closed and not args.no_stagger else "")) if S else (", from a saved steady state" if args.load_state
+                                                                        else ", from reset")
     out = {
         "metric": "env-steps/sec (cars x envs), daytona 10-car",
         "value": value, "unit": "car-steps/s", "n_gpus": world, "steps": K, "warmup": W,
         "ms_per_step": elapsed / K * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
         "dtype": "f32+f64", "data": "synthetic",
-        "config": {"workload": f"{'mixed 8-track' if args.mixed else os.path.basename(tpath)[:-6]} {C}-car: {E} envs x {C} cars per GPU, "
-                               f"{ {'uniform': 'uniform U[-1,1]^2 actions resident in HBM', 'driver': 'on-device rule driver', 'sac': 'fused SAC actor (random-init) closed loop'}[args.policy]}, auto-reset",
-                   "envs_per_gpu": E, "cars_per_env": C, "track": "mixed (env e: track e mod 8)" if args.mixed else os.path.basename(tpath),
+        "config": {"workload": f"{track_name} {C}-car: {E} envs x {C} cars per GPU, {POLICY_TEXT[args.policy]}"
+                               f"{settle_txt}, auto-reset",
+                   "envs_per_gpu": E, "cars_per_env": C, "policy": args.policy,
+                   "track": "mixed (env e: track e mod 8)" if args.mixed else os.path.basename(tpath),
                    "parallelism": f"dp{world} (env shards" + (", RCCL gather of obs/reward/flags to rank 0 per step)" if gather else ", no collective)")},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": tnote,
                      "kernel": "model_kernel + logic_kernel + ray_sensor_kernel (one env step)", "kernel_ms": kern_ms,
                      "algo_bytes_per_car_step": ALGO_BYTES_PER_CAR_STEP},
-        "engine_errors": errs,
+        "workload_stats": wstats,
+        "engine_errors": int(tally[5]),
     }
+    if not args.no_secondary and args.policy != "uniform" and not args.gather:
+        # secondary, labelled: round 1's workload (uniform U[-1,1]^2 from reset) on a fresh engine
+        del step
+        env.close()
+        env2 = make_env()
+        env2.reset()
+        gen = torch.Generator(device=dev)
+        gen.manual_seed(1234 + rank)
+        acts2 = torch.rand((W + K, E, C, 2), generator=gen, device=dev) * 2 - 1
+        s2 = Stepper(env2, "uniform", rank, acts2, None)
+        for i in range(W):
+            s2(i)
+        el2 = reduce_max([timed(s2, W, K, world)], dev)[0]
+        out["uniform_from_reset"] = {"value": throughput(world, E, C, K, el2), "ms_per_step": el2 / K * 1e3,
+                                     "note": "secondary: uniform actions from reset (cars stay on the start "
+                                             "straight; no contacts, laps or resets) -- an upper bound, not the headline"}
+        env = env2
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(tpath, C, args.cpu_budget, args.cpu_threads)
     if rank == 0:

@@ -94,9 +94,6 @@ struct Params {
   float4* pose;        // [2][N] sensor hand-off: (x, y, angle, mode) -- see sensor_kernel
   double2* pose_cs;    // [2][N] cos, sin of (double)angle for the ray end points (computed once per car)
   const double2* ray_cs;   // [16] cos, sin of the ray offsets radians(22.5 i) (nascar_rays.h)
-  // [N] beam-list base of pose A's cell, looked up by logic_kernel off the sensor kernel's critical path
-  // (-1: no lists there); any value < -1 (POSE_CELL_UNSET): the sensor kernel looks it up itself
-  int* pose_cell;
   // block map shortcuts (prepare()): map_identity = blk_env[s] is s (< E) or -1, one_track >= 0 = every
   // block's track; they spare each kernel's first dependent load
   int map_identity, one_track;
@@ -107,12 +104,6 @@ __device__ __forceinline__ int blk_env_of(const Params& P, int el, int s) {
   return P.blk_env[s];
 }
 __device__ __forceinline__ int blk_track_of(const Params& P, int b) { return P.one_track >= 0 ? P.one_track : P.blk_track[b]; }
-#define POSE_CELL_UNSET (-2)
-// Default: the sensor kernel looks its cell up itself.  -DRAY_LOGIC_CELL moves the lookup into logic_kernel
-// (measured 88.1 vs 86.4 us/step: logic_kernel's extra load and store cost more than the sensor saves).
-#ifndef RAY_LOGIC_CELL
-#define RAY_OWN_CELL
-#endif
 // BeamGrid list base (built cell id * BEAM_NB) of the cell holding (x, y); -1 outside the built cells
 __device__ __forceinline__ int beam_cell_base(const BeamGrid& G, float x, float y) {
   const float fx = (x - G.ox) * G.inv_cell, fy = (y - G.oy) * G.inv_cell;
@@ -417,8 +408,7 @@ __device__ inline void update_friction(Car& c, double df) {
 __device__ __forceinline__ V2 OV(double x, double y) { return V((float)x, (float)y); }
 
 // Car.update_physics (src/car.py:329-387) and helpers (:389-892)
-__device__ inline void car_update_physics(const Params& P, Car& c, int n, const TrackDev& T,
-                                          const uint32_t* s_acc = nullptr) {
+__device__ inline void car_update_physics(const Params& P, Car& c, int n, const TrackDev& T) {
   const double dt = P.dt_d;
   c.thr = c.thr_in; c.brk = c.brk_in; c.steer = c.str_in * (45.0 * RAD_PER_DEG);
   {
@@ -499,18 +489,8 @@ __device__ inline void car_update_physics(const Params& P, Car& c, int n, const 
     double* acc = P.acc;
     const size_t N = P.N;
     double hl[10], ht[10];
-    if (s_acc) {   // copied into LDS by model_kernel at launch (dword k of slot r = k / 2 at s_acc[k][tid])
-      __builtin_amdgcn_s_waitcnt(0);   // the LDS-DMA copies have landed
-      const int tid = threadIdx.x;
 #pragma unroll
-      for (int q = 0; q < 10; ++q) {
-        hl[q] = __hiloint2double((int)s_acc[(4 * q + 1) * SBLOCK + tid], (int)s_acc[(4 * q) * SBLOCK + tid]);
-        ht[q] = __hiloint2double((int)s_acc[(4 * q + 3) * SBLOCK + tid], (int)s_acc[(4 * q + 2) * SBLOCK + tid]);
-      }
-    } else {
-#pragma unroll
-      for (int q = 0; q < 10; ++q) { hl[q] = acc[(size_t)(2 * q) * N + n]; ht[q] = acc[(size_t)(2 * q + 1) * N + n]; }
-    }
+    for (int q = 0; q < 10; ++q) { hl[q] = acc[(size_t)(2 * q) * N + n]; ht[q] = acc[(size_t)(2 * q + 1) * N + n]; }
     if (c.acc_len == 10) {
 #pragma unroll
       for (int q = 0; q < 9; ++q) { hl[q] = hl[q + 1]; ht[q] = ht[q + 1]; }
@@ -834,7 +814,6 @@ __device__ __forceinline__ float4 car_pose(const Car& c, int mode) {
 // pose hand-off slot k (n: pass A, N + n: pass B) with the f64 cos / sin of the angle the rays rotate
 __device__ __forceinline__ void set_pose(const Params& P, size_t k, const Car& c, int mode) {
   P.pose[k] = car_pose(c, mode);
-  if (k < (size_t)P.N) P.pose_cell[k] = POSE_CELL_UNSET;   // logic_kernel fills it in for the step's pose A
   double s0, c0;
   sincos((double)c.a, &s0, &c0);
   P.pose_cs[k] = make_double2(c0, s0);
@@ -961,9 +940,6 @@ template <int LPC>
 #ifndef SENSOR_WPE
 #define SENSOR_WPE 6   // 80 VGPRs: all 5 464 waves of the 8192x10 bench resident at once (measured best of 4/5/6)
 #endif
-#ifndef SENSOR_LDS_WALLS
-#define SENSOR_GLOBAL_WALLS   // walls read from global (L1-resident) beat LDS staging: 46 KB/workgroup held occupancy at 3
-#endif
 __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(SENSOR_WPE))) sensor_kernel(Params P, float* obs,
                                                                                                         float* terminal_obs, int passes) {
   constexpr int CPW = BLOCK / LPC;          // cars per workgroup
@@ -982,7 +958,6 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(SENS
   const int env = blk_env_of(P, el, b * P.epb + el);
   const TrackDev T = P.tracks[blk_track_of(P, b)];
   const int nw = T.nwall, ng = T.ngroup;
-#ifdef SENSOR_GLOBAL_WALLS
   // walls and groups read straight from the track's global image (L1/L2-resident, shared by every
   // workgroup): no staging, no dynamic LDS
   (void)swa; (void)nw;
@@ -991,19 +966,6 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(SENS
 #define SW_B(j) swall[2 * (j) + 1]
   for (int g = t; g < ng; g += BLOCK) swa[g] = T.groups[g];   // groups (2-4 KB) staged in LDS; the barrier below publishes them
 #define SW_G(g) swa[g]
-#else
-  float4* swb = swa + nw;
-  float4* sgr = swb + nw;
-  for (int j = t; j < nw; j += BLOCK) {
-    const LWall w = T.walls[j];
-    swa[j] = make_float4(w.px, w.py, w.rad + 0.25f, w.hx);
-    swb[j] = make_float4(w.qs, w.qc, w.hy, 0.0f);
-  }
-  for (int g = t; g < ng; g += BLOCK) sgr[g] = T.groups[g];
-#define SW_A(j) swa[j]
-#define SW_B(j) swb[j]
-#define SW_G(g) sgr[g]
-#endif
   const int n = env >= 0 ? env * C + car : 0;
   float4 pa = make_float4(0.f, 0.f, 0.f, 0.f), pb = pa;
   int mode = 0;   // A bits from pose[n], the B bit from pose[N + n]
@@ -1227,19 +1189,33 @@ __device__ inline float ray_fallback(const TrackDev& T, V2 p1, float p2x, float 
   return bi;
 }
 
-// DistanceSensor.get_sensor_distances (src/distance_sensor.py:71-117) with one lane per ray: 16 lanes per
-// car, BLOCK / 16 cars per workgroup.  The lane walks its beam list (BeamGrid), so no lane waits for the
-// others and there is no LDS or barrier.  Passes and modes as sensor_kernel (pose[n]: pass A, pose[N + n]:
-// pass B for auto-reset cars).
+// 4x4 transpose inside each quad of lanes (DPP quad_perm, no LDS): lane r holds v[q] = ray r + 4q on entry
+// and o[j] = ray 4r + j on exit, so each lane owns 16 contiguous bytes of the car's obs[22:38].
+template <int S> __device__ __forceinline__ float quad_rot(float x) {   // lane r of a quad reads lane (r + S) & 3
+  constexpr int ctrl = (S & 3) | (((1 + S) & 3) << 2) | (((2 + S) & 3) << 4) | (((3 + S) & 3) << 6);
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), ctrl, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float sel4(const float v[4], int k) { return k == 0 ? v[0] : k == 1 ? v[1] : k == 2 ? v[2] : v[3]; }
+__device__ __forceinline__ void put4(float o[4], int k, float x) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) o[j] = k == j ? x : o[j];
+}
+__device__ __forceinline__ void quad_transpose(const float v[4], float o[4], int r) {
+  o[0] = o[1] = o[2] = o[3] = 0.0f;
+  put4(o, r, sel4(v, r));
+  put4(o, (r + 1) & 3, quad_rot<1>(sel4(v, (r - 1) & 3)));
+  put4(o, (r + 2) & 3, quad_rot<2>(sel4(v, (r - 2) & 3)));
+  put4(o, (r + 3) & 3, quad_rot<3>(sel4(v, (r - 3) & 3)));
+}
+
+// DistanceSensor.get_sensor_distances (src/distance_sensor.py:71-117) on beam lists, 4 lanes per car
+// (rays r, r + 4, r + 8, r + 12 on lane r), BLOCK / 4 cars per workgroup, the track's wall image staged in
+// LDS.  Passes and modes as sensor_kernel (pose[n]: pass A, pose[N + n]: pass B for auto-reset cars).
+// The 16 values of a car are transposed inside its lane quad and stored as 4 x 16 contiguous bytes.
 #ifndef RSENSOR_WPE
 #define RSENSOR_WPE 6   // 4 lanes per car at 6 waves/SIMD: 41.5 us (8 lanes 53.7, 2 lanes 44.3; 16 lanes 62.4)
 #endif
-#ifndef RAY_GLOBAL_WALLS
-#define RAY_LDS_WALLS   // the 23 KB wall image staged per workgroup: 38.6 -> 37.5 us
-#endif
-#ifndef RAY_LPC
-#define RAY_LPC 4     // lanes per car; each lane walks the lists of 16 / RAY_LPC rays
-#endif
+#define RAY_LPC 4     // lanes per car; each lane walks the lists of rays r, r + 4, r + 8, r + 12
 __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(RSENSOR_WPE)))
 ray_sensor_kernel(Params P, float* obs, float* terminal_obs, int passes) {
   constexpr int CPW = BLOCK / RAY_LPC, RPL = 16 / RAY_LPC;
@@ -1251,34 +1227,22 @@ ray_sensor_kernel(Params P, float* obs, float* terminal_obs, int passes) {
   const int el = slot / C, car = slot - el * C;
   const int env = blk_env_of(P, el, b * P.epb + el);
   const TrackDev& T = P.tracks[blk_track_of(P, b)];
-#ifdef RAY_LDS_WALLS
   {
     float4* s_w = (float4*)smem;
     const int nw2 = 2 * T.nwall;
     for (int k = t; k < nw2; k += BLOCK) s_w[k] = T.swall[k];
     __syncthreads();
   }
-#endif
   if (env < 0) return;
   // pose loads after the staging barrier: issuing them (and pass A's cos/sin) before it, or the beam-cell
   // lookup too, measured 2.5 / 9 us slower (registers held across the staging)
   const int n = env * C + car;
   int mode = 0;
   float4 pa = make_float4(0.f, 0.f, 0.f, 0.f), pb = pa;
-  int cell_a = POSE_CELL_UNSET;
-  if (passes & 1) {
-    pa = P.pose[n]; mode = __float_as_int(pa.w) & (PM_A_OBS | PM_A_TERM);
-#ifndef RAY_OWN_CELL
-    cell_a = P.pose_cell[n];
-#endif
-  }
+  if (passes & 1) { pa = P.pose[n]; mode = __float_as_int(pa.w) & (PM_A_OBS | PM_A_TERM); }
   if (passes & 2) { pb = P.pose[P.N + n]; mode |= __float_as_int(pb.w) & PM_B_OBS; }
   const BeamGrid G = T.beam;
-#ifdef RAY_LDS_WALLS
   const float4* __restrict__ sw = (const float4*)smem;   // the track's wall image staged per workgroup
-#else
-  const float4* __restrict__ sw = T.swall;
-#endif
 #pragma unroll 1
   for (int pass = 0; pass < 2; ++pass) {
     const bool active = pass == 0 ? (mode & (PM_A_OBS | PM_A_TERM)) != 0 : (mode & PM_B_OBS) != 0;
@@ -1287,17 +1251,8 @@ ray_sensor_kernel(Params P, float* obs, float* terminal_obs, int passes) {
     const V2 p1 = V(ps.x, ps.y);
     const double px = ps.x, py = ps.y, ang = ps.z;
     const double2 cs = P.pose_cs[pass == 0 ? (size_t)n : (size_t)P.N + n];
-    const int pc = pass == 0 ? cell_a : POSE_CELL_UNSET;
-    const int base = pc >= -1 ? pc : beam_cell_base(G, p1.x, p1.y);
+    const int base = beam_cell_base(G, p1.x, p1.y);
     // direction bin of sa = -radians(22.5 i) + ang (f64; the lists carry a 2e-3 rad guard) -> list slot
-#ifdef RAY_BIN_PER_RAY
-    auto slot_of = [&](int i) {
-      const double sa = -((double)i * (360.0 / 16) * RAD_PER_DEG) + ang;
-      double u = sa * (BEAM_NB / (2.0 * PI_D));
-      u -= BEAM_NB * floor(u * (1.0 / BEAM_NB));
-      return beam_slot(min(BEAM_NB - 1, max(0, (int)u)));
-    };
-#else
     // ray i is exactly BEAM_STRIDE bins clockwise of ray 0 in real arithmetic, and the f64 rounding of
     // sa_i (~1e-15 rad) is far inside the lists' 2e-3 rad guard, so bin_i = bin_0 - BEAM_STRIDE i:
     // slot_i = (bin_0 % STRIDE) * 16 + (bin_0 / STRIDE - i) mod 16
@@ -1308,19 +1263,8 @@ ray_sensor_kernel(Params P, float* obs, float* terminal_obs, int passes) {
       slot0 = beam_slot(min(BEAM_NB - 1, max(0, (int)u)));
     }
     auto slot_of = [&](int i) { return (slot0 & ~15) | ((slot0 - i) & 15); };
-#endif
-#ifdef RAY_HEAD_ALL
-    // all of the lane's list heads requested before the first walk (independent loads in flight together)
-    uint4 hd[RPL];
-#pragma unroll
-    for (int q = 0; q < RPL; ++q) hd[q] = base >= 0 ? G.head[base + slot_of(r + RAY_LPC * q)] : make_uint4(0, 0, 0, 0);
-#undef RAY_UNROLL
-#define RAY_UNROLL RPL
-#endif
-#ifndef RAY_UNROLL
-#define RAY_UNROLL 1
-#endif
-#pragma unroll RAY_UNROLL
+    float v[RPL] = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll 1
     for (int q = 0; q < RPL; ++q) {
       const int i = r + RAY_LPC * q;
       double dxd, dyd;
@@ -1329,13 +1273,8 @@ ray_sensor_kernel(Params P, float* obs, float* terminal_obs, int passes) {
       float bi = 2.0f;
       if (base >= 0) {
         const int sl = slot_of(i);
-#ifndef RAY_NO_HEAD
         // the list's first BEAM_HEAD entries in one load; the rest of the list only when all were walked
-#ifdef RAY_HEAD_ALL
-        const uint4 h = hd[q];
-#else
         const uint4 h = G.head[base + sl];
-#endif
         const uint32_t hv[BEAM_HEAD] = {h.x, h.y, h.z, h.w};
         bool more = true;
 #pragma unroll
@@ -1356,30 +1295,19 @@ ray_sensor_kernel(Params P, float* obs, float* terminal_obs, int passes) {
             bi = wall_cast(sw[2 * j], sw[2 * j + 1], p1, p2.x, p2.y, dx, dy, bi);
           }
         }
-#else
-        const uint32_t s0 = G.start[base + sl], e0 = G.start[base + sl + 1];
-        PCOUNT(11, e0 - s0);
-        for (uint32_t k = s0; k < e0; ++k) {
-          const uint32_t v = G.ent[k];
-          if ((float)(v >> 16) * 0.01f > bi * 250.0f * 1.00001f + 0.01f) break;   // lower bound beyond the best hit
-          const int j = (int)(v & 0xFFFFu);
-          PCOUNT(10, 1);
-          bi = wall_cast(sw[2 * j], sw[2 * j + 1], p1, p2.x, p2.y, dx, dy, bi);
-        }
-#endif
       } else {
         PCOUNT(9, 1);
         bi = ray_fallback(T, p1, p2.x, p2.y, dx, dy, ps.z, i);
       }
       PCOUNT(8, 1);
-      const float val = sensor_value(bi);
-      if (pass == 0) {
-        if (mode & PM_A_OBS) obs[(size_t)n * 38 + 22 + i] = val;
-        if (mode & PM_A_TERM) terminal_obs[(size_t)n * 38 + 22 + i] = val;
-      } else {
-        obs[(size_t)n * 38 + 22 + i] = val;
-      }
+      put4(v, q, sensor_value(bi));
     }
+    float o[4];
+    quad_transpose(v, o, r);
+    const size_t at = (size_t)n * 38 + 22 + 4 * r;   // 8-byte aligned (rows are 152 B)
+    const float2 lo = make_float2(o[0], o[1]), hi = make_float2(o[2], o[3]);
+    if (pass == 1 || (mode & PM_A_OBS)) { *(float2*)(obs + at) = lo; *(float2*)(obs + at + 2) = hi; }
+    if (pass == 0 && (mode & PM_A_TERM)) { *(float2*)(terminal_obs + at) = lo; *(float2*)(terminal_obs + at + 2) = hi; }
   }
 }
 
@@ -1399,11 +1327,9 @@ __global__ void __launch_bounds__(SBLOCK) __attribute__((amdgpu_waves_per_eu(MOD
   PROF(0);
   __shared__ DSeg s_segs[MAX_SEG];
   Car c;
-#ifndef MODEL_LATE_LOAD
   // car state and action requested before the segment staging barrier (their round trips overlap the
   // staging's instead of following it: 89 -> 84 us per step)
   if (env >= 0) car_load_phys(P, n, c);
-#endif
   // actions (BaseEnv._convert_to_internal_action / _discrete_to_continuous, np.float32)
   float tb = 0.0f, st = 0.0f;
   if (env >= 0) {
@@ -1415,20 +1341,6 @@ __global__ void __launch_bounds__(SBLOCK) __attribute__((amdgpu_waves_per_eu(MOD
       tb = ((const float*)actions)[2 * n]; st = ((const float*)actions)[2 * n + 1];
     }
   }
-#ifdef MODEL_ACC_LDS   // measured slower: model_kernel 21.8 vs 20.8 us
-  // the 10-sample acceleration history (20 f64 = 40 dwords per car, read mid-way through the vehicle
-  // model) copied HBM -> LDS at launch (global_load_lds, no registers held): its round trip overlaps the
-  // staging below instead of stalling the f64 chain
-  __shared__ uint32_t s_acc[40 * SBLOCK];
-  if (env >= 0) {
-    const uint32_t* accw = (const uint32_t*)P.acc;
-    const int wb = tid & ~63;
-#pragma unroll
-    for (int k = 0; k < 40; ++k)
-      __builtin_amdgcn_global_load_lds((const void*)(accw + 2 * ((size_t)(k >> 1) * P.N + n) + (k & 1)),
-                                       (__attribute__((address_space(3))) void*)(s_acc + k * SBLOCK + wb), 4, 0, 0);
-  }
-#endif
   TrackDev T = P.tracks[blk_track_of(P, blockIdx.x)];
   if (tid < T.nseg) s_segs[tid] = T.segs[tid];
   __syncthreads();
@@ -1436,9 +1348,6 @@ __global__ void __launch_bounds__(SBLOCK) __attribute__((amdgpu_waves_per_eu(MOD
   PROF(1);
   if (env < 0) return;
   const WallSet S{T.walls, T.nwall, T.bp, T.sn};
-#ifdef MODEL_LATE_LOAD
-  car_load_phys(P, n, c);
-#endif
   PROF(2);
   float a0, a1, a2 = st;
   if (tb >= 0) { a0 = tb; a1 = 0.0f; } else { a0 = 0.0f; a1 = -tb; }
@@ -1446,11 +1355,7 @@ __global__ void __launch_bounds__(SBLOCK) __attribute__((amdgpu_waves_per_eu(MOD
   c.thr_in = pymax(0.0, pymin(1.0, (double)a0));
   c.brk_in = pymax(0.0, pymin(1.0, (double)a1));
   c.str_in = pymax(-1.0, pymin(1.0, (double)a2));
-#ifdef MODEL_ACC_LDS
-  car_update_physics(P, c, n, T, s_acc);
-#else
   car_update_physics(P, c, n, T);
-#endif
   car_store_model(P, n, c);
   asm volatile("" ::: "memory");   // keep the model write-back ahead of the Box2D step (register pressure)
   PROF(3);
@@ -1485,18 +1390,11 @@ __global__ void __launch_bounds__(SBLOCK) logic_kernel(Params P, float* obs, flo
   if (env >= 0) {   // state loads issued before the segment staging barrier (independent round trips)
     car_load_body(P, n, c);
     car_load_logic(P, n, c);
-#ifndef LOGIC_LATE_LOADS
     car_reload_tyres(P, n, c);
     if (car == 0) { pend_in = P.env_i32[E_PENDING * P.E + env]; reason_in = P.env_i32[E_REASON * P.E + env]; }
-#endif
     sim = P.env_time[env];
   }
   TrackDev T = P.tracks[blk_track_of(P, blockIdx.x)];
-#ifndef RAY_OWN_CELL
-  // the sensor kernel's beam cell of this step's pose (pose A = the body position model_kernel stored):
-  // its round trip overlaps this kernel instead of sitting on the sensor kernel's dependent chain
-  const int cell_a = env >= 0 ? beam_cell_base(T.beam, c.xf.p.x, c.xf.p.y) : -1;
-#endif
   if (tid < T.nseg) {
     const DSeg sg = T.segs[tid];
     s_segs[tid] = sg; s_prefix[tid] = T.prefix[tid];
@@ -1535,9 +1433,6 @@ __global__ void __launch_bounds__(SBLOCK) logic_kernel(Params P, float* obs, flo
   // evaluated in car order with cars > i not yet updated)
   int pend_env = 0;
   if (env >= 0 && car == 0) {
-#ifdef LOGIC_LATE_LOADS
-    pend_in = P.env_i32[E_PENDING * P.E + env]; reason_in = P.env_i32[E_REASON * P.E + env];
-#endif
     int pend = pend_in;
     if (P.reset_on_lap) {
       const int b = tid;
@@ -1577,9 +1472,6 @@ __global__ void __launch_bounds__(SBLOCK) logic_kernel(Params P, float* obs, flo
       } else { c.stuck_dur = 0.0; c.has_stuck_start = 0; }
     }
     LPROF(3);
-#ifdef LOGIC_LATE_LOADS
-    car_reload_tyres(P, n, c);
-#endif
     car_obs(c, o);
     LPROF(4);
     // _calculate_multi_rewards (src/car_env.py:980-1113)
@@ -1655,9 +1547,6 @@ __global__ void __launch_bounds__(SBLOCK) logic_kernel(Params P, float* obs, flo
     if (terminal_obs) { float* t = terminal_obs + (size_t)n * 38; for (int i = 0; i < 22; ++i) t[i] = o[i]; }
     // sensor pass B: the reset pose of every auto-reset car (its pass-B values overwrite the pass-A
     // ones in obs); cleared for every other car
-#ifndef RAY_OWN_CELL
-    P.pose_cell[n] = cell_a;
-#endif
     if (reset_now) {
       car_reset(P, c, n, false, S, T);
       car_obs(c, o);
@@ -1749,13 +1638,19 @@ __device__ __forceinline__ uint32_t mix32(uint64_t x) {   // splitmix64 finalise
   x ^= x >> 31;
   return (uint32_t)(x >> 32);
 }
+// Noisy rule driver (policy 3): with probability NOISE_P16 / 65536 per car-step the driver's action is
+// replaced by the uniform draw of policy 0 (the driver state still advances), as gen_golden.py's
+// "rule_noisy" mode does with a host RNG; cars of one env therefore leave the common start trajectory.
+#define NOISE_P16 9830u   // 0.15 * 65536
 __global__ void policy_kernel(int N, int policy, uint64_t seed, int64_t step, const float* obs, float* act, double* ctl) {
   const int n = blockIdx.x * blockDim.x + threadIdx.x;
   if (n >= N) return;
+  const uint64_t key = (seed * 0x100000001B3ull) ^ ((uint64_t)n << 24) ^ (uint64_t)step * 0x9E3779B1ull;
+  const float u0 = (float)(mix32(key) >> 8) * (2.0f / 16777216.0f) - 1.0f;
+  const float u1 = (float)(mix32(key ^ 0xABCDEF12345ull) >> 8) * (2.0f / 16777216.0f) - 1.0f;
   if (policy == 0) {
-    uint64_t key = (seed * 0x100000001B3ull) ^ ((uint64_t)n << 24) ^ (uint64_t)step * 0x9E3779B1ull;
-    act[2 * n] = (float)(mix32(key) >> 8) * (2.0f / 16777216.0f) - 1.0f;
-    act[2 * n + 1] = (float)(mix32(key ^ 0xABCDEF12345ull) >> 8) * (2.0f / 16777216.0f) - 1.0f;
+    act[2 * n] = u0;
+    act[2 * n + 1] = u1;
     return;
   }
   // BaseController._fallback_control (game/control/base_controller.py:39-103); state per car in ctl[4*n..]:
@@ -1778,7 +1673,11 @@ __global__ void policy_kernel(int N, int policy, uint64_t seed, int64_t step, co
   tb = tb > 1.0 ? 1.0 : tb;  tb = tb < -1.0 ? -1.0 : tb;            // max(min(tb, 1), -1)
   steer = steer > 1.0f ? 1.0f : steer;  steer = steer < -1.0f ? -1.0f : steer;
   s[0] = tb; s[1] = steer; s[2] = fwd; s[3] = lim;
-  act[2 * n] = (float)tb; act[2 * n + 1] = steer;
+  if (policy == 3 && (mix32(key ^ 0x5DEECE66Dull) >> 16) < NOISE_P16) {
+    act[2 * n] = u0; act[2 * n + 1] = u1;
+  } else {
+    act[2 * n] = (float)tb; act[2 * n + 1] = steer;
+  }
 }
 
 // =================================================================== host side / C ABI
@@ -2055,13 +1954,13 @@ struct NascarHandle {
   NascarConfig cfg;
   int N, E, C, epb;
   void* arena = nullptr; size_t arena_bytes = 0;
-  size_t off_f32, off_f64, off_i32, off_acc, off_ct, off_key, off_n, off_time, off_ei32;
+  size_t off_f32, off_f64, off_i32, off_acc, off_ct, off_key, off_n, off_time, off_ei32, off_ctl;
   std::vector<HostTrack> tracks;
   TrackDev* d_tracks = nullptr;
   int* d_blk_track = nullptr; int* d_blk_env = nullptr; int nblocks = 0;
   int map_identity = 0, one_track = -1;   // Params shortcuts of the block map (prepare)
   std::vector<int> env_track;
-  double* d_ctl = nullptr;   // rule-driver state for nascar_policy_actions
+  double* d_ctl = nullptr;   // rule-driver state for nascar_policy_actions (inside the arena: snapshots keep it)
   float4* d_pose = nullptr;  // [2][N] step/reset -> sensor_kernel hand-off
   double2* d_pose_cs = nullptr;
   double2* d_ray_cs = nullptr;
@@ -2094,20 +1993,19 @@ extern "C" int nascar_create(const NascarConfig* cfg, NascarHandle** out) {
   h->off_n = o; o = align256(o + sizeof(float) * 2 * MAXC * N);
   h->off_time = o; o = align256(o + sizeof(double) * E);
   h->off_ei32 = o; o = align256(o + sizeof(int) * N_EI32 * E);
+  h->off_ctl = o; o = align256(o + sizeof(double) * 4 * N);
   h->arena_bytes = o;
   hipError_t e = hipMalloc(&h->arena, o);
   if (e != hipSuccess) { delete h; return fail("hipMalloc(%zu) failed: %s", o, hipGetErrorString(e)); }
   hipMemset(h->arena, 0, o);
-  hipMalloc(&h->d_ctl, sizeof(double) * 4 * N);
-  // pose hand-off [2][N] float4, then pose_cell [N] int (initialised < -1: POSE_CELL_UNSET)
-  if (hipMalloc(&h->d_pose, (sizeof(float4) * 2 + sizeof(int)) * N) != hipSuccess) { hipFree(h->arena); hipFree(h->d_ctl); delete h; return fail("hipMalloc(pose) failed"); }
+  h->d_ctl = (double*)((char*)h->arena + h->off_ctl);
+  // pose hand-off [2][N] float4
+  if (hipMalloc(&h->d_pose, sizeof(float4) * 2 * N) != hipSuccess) { hipFree(h->arena); delete h; return fail("hipMalloc(pose) failed"); }
   hipMemset(h->d_pose, 0, sizeof(float4) * 2 * N);
-  hipMemset(h->d_pose + 2 * (size_t)N, 0x80, sizeof(int) * N);
-  if (hipMalloc(&h->d_pose_cs, sizeof(double2) * 2 * N) != hipSuccess) { hipFree(h->arena); hipFree(h->d_ctl); hipFree(h->d_pose); delete h; return fail("hipMalloc(pose_cs) failed"); }
+  if (hipMalloc(&h->d_pose_cs, sizeof(double2) * 2 * N) != hipSuccess) { hipFree(h->arena); hipFree(h->d_pose); delete h; return fail("hipMalloc(pose_cs) failed"); }
   hipMemset(h->d_pose_cs, 0, sizeof(double2) * 2 * N);
   HIPCHK(hipMalloc(&h->d_ray_cs, sizeof(h_ray_cs)));
   HIPCHK(hipMemcpy(h->d_ray_cs, h_ray_cs, sizeof(h_ray_cs), hipMemcpyHostToDevice));
-  hipMemset(h->d_ctl, 0, sizeof(double) * 4 * N);
   h->env_track.assign(E, 0);
   *out = h;
   return 0;
@@ -2115,7 +2013,7 @@ extern "C" int nascar_create(const NascarConfig* cfg, NascarHandle** out) {
 
 extern "C" void nascar_destroy(NascarHandle* h) {
   if (!h) return;
-  hipFree(h->arena); hipFree(h->d_ctl); hipFree(h->d_pose); hipFree(h->d_pose_cs); hipFree(h->d_ray_cs); hipFree(h->d_actor);
+  hipFree(h->arena); hipFree(h->d_pose); hipFree(h->d_pose_cs); hipFree(h->d_ray_cs); hipFree(h->d_actor);
   for (auto& t : h->tracks) {
     hipFree(t.d_walls); hipFree(t.d_segs); hipFree(t.d_prefix);
     hipFree(t.bp.d_start); hipFree(t.bp.d_idx); hipFree(t.bp.d_box); hipFree(t.sn.d_start); hipFree(t.sn.d_idx); hipFree(t.d_groups); hipFree(t.d_swall);
@@ -2287,7 +2185,6 @@ static Params make_params(NascarHandle* h) {
   P.blk_track = h->d_blk_track; P.blk_env = h->d_blk_env; P.tracks = h->d_tracks;
   P.map_identity = h->map_identity; P.one_track = h->one_track;
   P.pose = h->d_pose; P.pose_cs = h->d_pose_cs; P.ray_cs = h->d_ray_cs;
-  P.pose_cell = (int*)(h->d_pose + 2 * (size_t)h->N);
   return P;
 }
 
@@ -2304,20 +2201,12 @@ static void launch_sensors_impl(NascarHandle* h, const Params& P, float* obs, fl
   if (impl == 1) {
     constexpr int CPW = BLOCK / RAY_LPC;
     const int sub = (SBLOCK + CPW - 1) / CPW;
-#ifdef RAY_LDS_WALLS
     const size_t rlds = h->max_sensor_lds;   // >= 2 float4 per wall
-#else
-    const size_t rlds = 0;
-#endif
     hipLaunchKernelGGL(ray_sensor_kernel, dim3(h->nblocks * sub), dim3(BLOCK), rlds, (hipStream_t)stream, P, obs,
                        terminal_obs, passes);
     return;
   }
-#ifdef SENSOR_GLOBAL_WALLS
   const size_t lds = h->max_sensor_groups_lds;
-#else
-  const size_t lds = h->max_sensor_lds;
-#endif
   const int sub = (SBLOCK + BLOCK / SENSOR_LPC - 1) / (BLOCK / SENSOR_LPC);
   hipLaunchKernelGGL(sensor_kernel<SENSOR_LPC>, dim3(h->nblocks * sub), dim3(BLOCK), lds, (hipStream_t)stream,
                      P, obs, terminal_obs, passes);
@@ -2380,6 +2269,7 @@ extern "C" int nascar_set_state(NascarHandle* h, const void* src, void* stream) 
 extern "C" int nascar_policy_actions(NascarHandle* h, int32_t policy, uint64_t seed, int64_t step, const float* obs,
                                      float* actions, void* stream) {
   if (!h || !actions) return fail("null argument");
+  if (policy < 0 || policy > 3) return fail("unknown policy %d", policy);
   if (policy >= 1 && !obs) return fail("policy %d needs obs", policy);
   if (policy == 2) {
     if (!h->d_actor) return fail("policy 2 needs an actor (nascar_set_actor)");
@@ -2488,7 +2378,6 @@ __global__ void debug_pose_kernel(Params P, const float* poses) {
   if (n >= P.N) return;
   const float a = poses[3 * n + 2];
   P.pose[n] = make_float4(poses[3 * n], poses[3 * n + 1], a, __int_as_float(PM_A_OBS));
-  P.pose_cell[n] = POSE_CELL_UNSET;
   double s0, c0;
   sincos((double)a, &s0, &c0);
   P.pose_cs[n] = make_double2(c0, s0);

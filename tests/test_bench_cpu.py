@@ -1,0 +1,51 @@
+"""Host logic of bench.py and the host restatement of the device action sources (no GPU)."""
+import numpy as np
+
+import bench
+from drivers import M64, mix32, noisy_mask, uniform_actions, RuleDriver
+
+
+def _mix32_py(x):
+    x = (x + 0x9E3779B97F4A7C15) & M64
+    x = ((x ^ (x >> 30)) * 0xBF58476D1CE4E5B9) & M64
+    x = ((x ^ (x >> 27)) * 0x94D049BB133111EB) & M64
+    return (x ^ (x >> 31)) >> 32
+
+
+def test_mix32_matches_python_ints():
+    xs = np.array([0, 1, 2**63 + 5, M64, 0x123456789ABCDEF], np.uint64)
+    assert [int(v) for v in mix32(xs)] == [_mix32_py(int(v)) for v in xs]
+
+
+def test_uniform_and_noise_rates():
+    u = uniform_actions(200000, 3, 17)
+    assert u.dtype == np.float32 and u.min() >= -1 and u.max() < 1
+    assert abs(u.mean()) < 0.01
+    m = noisy_mask(200000, 3, 17)
+    assert abs(m.mean() - 0.15) < 0.005
+
+
+def test_rule_driver_steers_toward_open_side():
+    d = RuleDriver(2)
+    obs = np.zeros((2, 38), np.float32)
+    obs[:, 22] = 1.0
+    obs[0, 23], obs[0, 37] = 0.2, 0.8     # left close, right open -> steer right (+)
+    obs[1, 23], obs[1, 37] = 0.8, 0.2
+    a = d(obs)
+    assert a[0, 1] > 0 and a[1, 1] < 0
+    assert np.isclose(a[0, 1], np.float32(1) - np.float32(0.2) / np.float32(0.8))
+
+
+def test_stagger_schedule_spreads_env_ages():
+    at = bench.stagger_schedule(8192, 10800)
+    age = 10800 - at
+    assert at.min() >= 1 and at.max() <= 10800
+    assert age.min() == 0 and age.max() < 10800
+    h = np.histogram(age, bins=10, range=(0, 10800))[0]
+    assert h.min() > 0.9 * h.mean()
+    short = bench.stagger_schedule(100, 600)          # settle shorter than an episode: old envs never reset
+    assert (short == -1).sum() == 100 - ((600 * 100 + 10799) // 10800)
+
+
+def test_throughput_is_whole_job():
+    assert bench.throughput(8, 8192, 10, 200, 0.02) == 8 * 8192 * 10 * 200 / 0.02

@@ -207,3 +207,50 @@ def test_device_rule_driver_matches_reference_controller(name, car):
         assert np.array_equal(a, acts[k][car]), f"step {k}: device {a} reference {acts[k][car]}"
         env.step(torch.from_numpy(acts[k].reshape(1, C, 2).copy()).cuda())
     env.close()
+
+
+def test_noisy_driver_closed_loop_vs_oracle():
+    """The bench's steady-state workload in miniature: device noisy rule driver (policy 3) in closed loop with
+    in-launch auto-reset and staggered masked resets, 16 envs x 10 cars on daytona for 2400 steps.  Every
+    step: device actions == the host restatement (tests/drivers.py), and obs / rewards / flags == the oracle
+    (which resets the same envs).  Asserts that wall contact, a disable and an env reset all happened."""
+    from drivers import NoisyRuleDriver
+    from oracle_lib import OracleEnv
+    E, C, S = 16, 10, 2400
+    env = _env("daytona.track", E, C)
+    orc = OracleEnv(os.path.join(TRACKS, "daytona.track"), E, C)
+    env.reset()
+    oo = orc.reset()[0]
+    drv = NoisyRuleDriver(E * C, seed=7)
+    stagger = {150 * e: e for e in range(1, E)}        # env e reset at step 150 e (ages spread)
+    n_contact = n_disabled = n_reset = 0
+    for k in range(S):
+        if k in stagger:
+            e = stagger[k]
+            m = torch.zeros(E, dtype=torch.uint8, device="cuda"); m[e] = 1
+            env.reset(m)
+            orc.reset(e)
+            oo = orc.outputs()[0]
+        ga = env.policy_actions(3, seed=7, step=k).clone()
+        ha = drv.actions(oo, k)
+        assert np.array_equal(ga.cpu().numpy().reshape(-1, 2), ha), f"step {k}: driver actions differ"
+        env.launch_step(ga, auto_reset=True)
+        oo, orw, ocf, oef = orc.step(ha)
+        gr, gcf, gef = env.reward.cpu().numpy(), env.car_flags.cpu().numpy(), env.env_flags.cpu().numpy()
+        assert np.array_equal(gr, orw), f"step {k}: reward mismatch"
+        assert np.array_equal(gcf & 1, ocf & 1), f"step {k}: disabled flags"
+        done = (oef[:, 0] != 0) | (oef[:, 1] != 0)
+        assert np.array_equal((gef & 3) != 0, done), f"step {k}: done flags"
+        for e in np.nonzero(done)[0]:
+            orc.reset(int(e))
+        if done.any():
+            oo = orc.outputs()[0]
+            n_reset += int(done.sum())
+        go = env.obs.cpu().numpy()
+        bad = np.argwhere(go != oo)
+        assert len(bad) == 0, f"step {k}: obs mismatch at {bad[:5].tolist()}"
+        n_contact += int((gcf & 4).astype(bool).sum())
+        n_disabled += int((gcf & 2).astype(bool).sum())
+    assert n_contact > 0 and n_disabled > 0, (n_contact, n_disabled)
+    assert not (env.car_flags.cpu().numpy() & 128).any()
+    env.close()

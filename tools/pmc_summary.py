@@ -67,7 +67,11 @@ def main():
     if b:
         res["bench_under_rocprof"] = b
         cfg = b["config"]
-        res.update(envs=cfg["envs_per_gpu"], cars=cfg["cars_per_env"], track=cfg["track"])
+        res.update(envs=cfg["envs_per_gpu"], cars=cfg["cars_per_env"], track=cfg["track"],
+                   policy=cfg.get("policy", "uniform"), workload=cfg["workload"])
+    sha = os.path.join(os.path.dirname(os.path.abspath(out)), "prof_source_sha.txt")
+    if os.path.exists(sha):
+        res["source_sha"] = open(sha).read().strip()
         res["bench_step_ms_events"] = b["roofline"]["kernel_ms"]
     f = _find(os.path.join(out, "fetch"), "counter_collection.csv")
     w = _find(os.path.join(out, "write"), "counter_collection.csv")
@@ -90,8 +94,8 @@ def main():
             if "envs" in res:
                 res["bytes_per_car_step"] = res["bytes_per_step"] / (res["envs"] * res["cars"])
     json.dump(res, open(os.path.join(prof, f"{tag}_pmc_step.json"), "w"), indent=1)
-    if "bytes_per_step" in res and "envs" in res:
-        json.dump({k: res[k] for k in ("envs", "cars", "track", "bytes_per_step", "bytes_per_step_uncorrected",
+    if "bytes_per_step" in res and "envs" in res and "source_sha" in res:
+        json.dump({k: res[k] for k in ("envs", "cars", "track", "policy", "workload", "source_sha", "bytes_per_step", "bytes_per_step_uncorrected",
                                        "bytes_per_car_step", "fetch_size_kb", "write_size_kb", "tag")},
                   open(os.path.join(prof, "pmc_traffic.json"), "w"), indent=1)
     print(json.dumps(res, indent=1))
