@@ -507,6 +507,7 @@ __device__ inline void world_manifold(const DContact& m, Xf xfA, Xf xfB, V2* nor
 
 // b2Contact::Update
 __device__ inline void contact_update(Car& c, int ci, const LWall* W) {
+  PCOUNT(14, 1);
   DContact& ct = c.ct[ci];
   DContact old = ct;
   ct.flags |= CT_ENABLED;
@@ -1091,6 +1092,29 @@ __device__ inline void island_solve_toi(Car& c, const LWall* W, const int* cidx,
   report(c, vc, n);
 }
 
+// Exact shortcut for b2TimeOfImpact on a (car, static wall) pair.  The root finder can only report
+// TOUCHING -- the one outcome whose alpha differs from 1 -- if the swept car comes within target +
+// tolerance (0.005 + 0.00125 m) of the wall: GJK distance(t1) < target + tol, or the separating
+// function at t1 (built from the closest features at t1, so >= the distance there) <= target + tol.
+// Every car point moves at most |c - c0| + |a - a0| * R_car (R_car = circumradius; the car's centroid is
+// its origin) along the sweep, and the separating-axis maximum of the two boxes at the sweep's end pose
+// is a lower bound of their distance there.  If that bound minus the motion exceeds target + tol by a
+// 1 cm rounding margin, the swept car never comes that close and TOI would return SEPARATED or FAILED:
+// alpha = 1 without running it (identical result, verified by every GPU-vs-oracle test).
+#define TOI_CULL_DIST (0.005f + 0.00125f + 0.01f)
+__device__ __forceinline__ bool toi_far(const Car& c, const Poly* pa, const LWall& wl) {
+#ifdef NASCAR_NO_TOI_CULL   // A/B and verification builds only
+  return false;
+#endif
+  const float R_CAR = 2.80389f;   // > sqrt(CAR_HX^2 + CAR_HY^2) = 2.80323
+  const float motion = vlen(vsub(c.c, c.c0)) + fabsf(c.a - c.a0) * R_CAR;
+  Poly pb; make_box(&pb, wl.hx, wl.hy);
+  const Xf xfB = wall_xf(wl);
+  int e;
+  const float sep = fmaxb(find_max_separation(&e, pa, c.xf, &pb, xfB), find_max_separation(&e, &pb, xfB, pa, c.xf));
+  return sep - motion > TOI_CULL_DIST;
+}
+
 // b2World::SolveTOI
 __device__ inline void solve_toi(Car& c, const WallSet& S, float dt, float friction) {
   const LWall* W = S.W;
@@ -1109,6 +1133,12 @@ __device__ inline void solve_toi(Car& c, const WallSet& S, float dt, float frict
         if (!c.awake) continue;
         float alpha0 = c.alpha0;
         const LWall& wl = W[ct.wall];
+        if (toi_far(c, &pa, wl)) {
+          PCOUNT(13, 1);
+          ct.toi = 1.0f; ct.flags |= CT_TOI;
+          continue;   // alpha = 1: never below minAlpha
+        }
+        PCOUNT(12, 1);
         Poly pb; make_box(&pb, wl.hx, wl.hy);
         Sweep sA; sA.c0 = c.c0; sA.c = c.c; sA.a0 = c.a0; sA.a = c.a; sA.alpha0 = c.alpha0;
         Sweep sB; sB.c0 = V(wl.px, wl.py); sB.c = sB.c0; sB.a0 = wl.ang; sB.a = wl.ang; sB.alpha0 = 0.0f;
@@ -1121,6 +1151,7 @@ __device__ inline void solve_toi(Car& c, const WallSet& S, float dt, float frict
       if (alpha < minAlpha) { minC = i; minAlpha = alpha; }
     }
     if (minC < 0 || 1.0f - 10.0f * FLT_EPS < minAlpha) break;
+    PCOUNT(15, 1);
     V2 bc0 = c.c0, bc = c.c; float ba0 = c.a0, ba = c.a, balpha0 = c.alpha0;
     {
       float beta = fdiv_cr(minAlpha - c.alpha0, 1.0f - c.alpha0);

@@ -437,7 +437,42 @@ def reason_code(r):
     return REASONS[r]
 
 
-def run_scenario(ref, name, track, C, steps, policy, reset_on_lap=False, reset_at=(), seed=0):
+DISCRETE_P = [0.1, 0.5, 0.1, 0.15, 0.15]   # Discrete(5) draws: mostly throttle, some braking / steering
+
+
+def policy_action(mode, k, driver, obs, rng):
+    """one car's action for policy `mode` (a name, or a tuple (name, *params)) at step k"""
+    name, par = (mode[0], mode[1:]) if isinstance(mode, tuple) else (mode, ())
+    if name == "rule":
+        return driver(obs)
+    if name == "rule_noisy":
+        a = driver(obs)
+        return rng.uniform(-1, 1, 2).astype(np.float32) if rng.random() < 0.15 else a
+    if name == "rule_bias":      # full throttle, steering biased toward the outer wall (grinds it: damage)
+        a = driver(obs)
+        return np.array([1.0, min(1.0, float(a[1]) + par[0])], np.float32)
+    if name == "uturn":          # (t0, t1, throttle, steer): turn round inside (t0, t1), then the rule driver
+        a = driver(obs)
+        return np.array([par[2], par[3]], np.float32) if par[0] < k < par[1] else a
+    if name == "spin":           # (steer, period): throttle + steer, then full brake, periodically
+        on = k % par[1] < 0.6 * par[1]
+        return np.array([1.0 if on else -1.0, par[0] if on else 0.0], np.float32)
+    if name == "random":
+        return rng.uniform(-1, 1, 2).astype(np.float32)
+    if name == "throttle":
+        return np.array([1.0, 0.0], np.float32)
+    if name == "throttle_left":
+        return np.array([1.0, -0.3 if k > 100 else 0.0], np.float32)
+    if name == "idle":
+        return np.array([0.0, 0.0], np.float32)
+    if name == "brake_back":
+        return np.array([-1.0 if k % 200 < 120 else 0.6, 0.8 if k % 300 < 100 else -0.2], np.float32)
+    if name == "discrete":
+        return int(rng.choice(5, p=DISCRETE_P))
+    raise ValueError(mode)
+
+
+def run_scenario(ref, name, track, C, steps, policy, reset_on_lap=False, reset_at=(), seed=0, discrete=False):
     """Run the REFERENCE CarEnv (stub Box2D -> oracle Box2D) and record everything."""
     track_path = os.path.join(ref, "tracks", track)
     hb = oracle_lib.OracleEnv(track_path, 1, 1)
@@ -448,7 +483,8 @@ def run_scenario(ref, name, track, C, steps, policy, reset_on_lap=False, reset_a
     import io
     with contextlib.redirect_stdout(io.StringIO()):
         from src.car_env import CarEnv
-        env = CarEnv(render_mode=None, track_file=track_path, num_cars=C, reset_on_lap=reset_on_lap)
+        env = CarEnv(render_mode=None, track_file=track_path, num_cars=C, reset_on_lap=reset_on_lap,
+                     discrete_action_space=discrete)
         obs, info = env.reset()
     rng = np.random.default_rng(seed)
     drivers = [RuleDriver(ref) for _ in range(C)]
@@ -458,37 +494,22 @@ def run_scenario(ref, name, track, C, steps, policy, reset_on_lap=False, reset_a
     for k in range(steps):
         acts = []
         for i in range(C):
-            mode = policy[i % len(policy)]
-            if mode == "rule":
-                a = drivers[i](obs[i])
-            elif mode == "rule_noisy":
-                a = drivers[i](obs[i])
-                if rng.random() < 0.15:
-                    a = rng.uniform(-1, 1, 2).astype(np.float32)
-            elif mode == "random":
-                a = rng.uniform(-1, 1, 2).astype(np.float32)
-            elif mode == "throttle":
-                a = np.array([1.0, 0.0], np.float32)
-            elif mode == "throttle_left":
-                a = np.array([1.0, -0.3 if k > 100 else 0.0], np.float32)
-            elif mode == "idle":
-                a = np.array([0.0, 0.0], np.float32)
-            elif mode == "brake_back":
-                a = np.array([-1.0 if k % 200 < 120 else 0.6, 0.8 if k % 300 < 100 else -0.2], np.float32)
-            else:
-                raise ValueError(mode)
-            acts.append(np.clip(np.asarray(a, np.float32), -1, 1))
-        acts = np.stack(acts).astype(np.float32)
+            a = policy_action(policy[i % len(policy)], k, drivers[i], obs[i], rng)
+            acts.append(a if discrete else np.clip(np.asarray(a, np.float32), -1, 1))
+        acts = np.array(acts, np.int32) if discrete else np.stack(acts).astype(np.float32)
         did_reset = k in reset_at
         with contextlib.redirect_stdout(io.StringIO()):
             if did_reset:
                 obs, info = env.reset()
                 obs = obs.reshape(C, 38)
-                rec["actions"].append(np.zeros((C, 2), np.float32))
+                rec["actions"].append(np.zeros(C, np.int32) if discrete else np.zeros((C, 2), np.float32))
                 rec["obs"].append(obs.copy()); rec["rewards"].append(np.zeros(C, np.float32))
                 rec["terminated"].append(False); rec["truncated"].append(False)
             else:
-                a_in = acts[0] if C == 1 else acts
+                if discrete:
+                    a_in = int(acts[0]) if C == 1 else acts.astype(np.int64)
+                else:
+                    a_in = acts[0] if C == 1 else acts
                 obs, rew, term, trunc, info = env.step(a_in)
                 obs = obs.reshape(C, 38)
                 rec["actions"].append(acts); rec["obs"].append(obs.copy())
@@ -501,8 +522,9 @@ def run_scenario(ref, name, track, C, steps, policy, reset_on_lap=False, reset_a
     sys.path.remove(ref)
     n = len(rec["obs"])
     keep = np.arange(n) if n <= 4000 else np.unique(np.r_[np.arange(0, n, 50), np.arange(n - 20, n)])
-    out = dict(track=np.array(track), C=np.array(C), reset_on_lap=np.array(reset_on_lap),
-               actions=np.array(rec["actions"], np.float32), obs=np.array(rec["obs"], np.float32)[keep],
+    out = dict(track=np.array(track), C=np.array(C), reset_on_lap=np.array(reset_on_lap), discrete=np.array(discrete),
+               actions=np.array(rec["actions"], np.int32 if discrete else np.float32),
+               obs=np.array(rec["obs"], np.float32)[keep],
                obs_steps=keep,
                rewards=np.array(rec["rewards"], np.float32), terminated=np.array(rec["terminated"]),
                truncated=np.array(rec["truncated"]), reason=np.array(rec["reason"], np.int32),
@@ -545,7 +567,21 @@ SCENARIOS = [
     ("daytona_long", "daytona.track", 1, 10810, ["rule"], False, ()),
     ("nascar2_seam", "nascar2.track", 1, 600, ["rule_noisy"], False, ()),
     ("trioval_idle", "trioval.track", 2, 720, ["idle", "random"], False, ()),
+    # round 2: every termination reason and disable branch, discrete actions, 10 cars, all 8 tracks
+    ("martinsville_all_idle", "martinsville.track", 3, 660, ["idle"], False, ()),                 # reason 1
+    ("daytona_low_reward", "daytona.track", 2, 900, [("spin", 0.35, 300), ("spin", 0.5, 180)], False, ()),  # reason 2
+    ("daytona_damage", "daytona.track", 2, 3000, [("rule_bias", 0.1), "rule"], False, ()),     # cumulative damage
+    ("nascar_backward", "nascar.track", 2, 900, ["rule", ("uturn", 100, 200, 0.3, 1.0)], False, ()),  # backward
+    ("nascar_banked_discrete", "nascar_banked.track", 3, 900, ["discrete"], False, (), {"discrete": True}),
+    ("michigan_discrete1", "michigan.track", 1, 700, ["discrete"], False, (), {"discrete": True}),
+    ("talladega_10car", "talladega.track", 10, 1500, ["rule", "rule_noisy", "random", "throttle", "throttle_left",
+                                                      "brake_back", "idle", "rule_noisy", ("rule_bias", 0.2), "rule"],
+     False, (900,)),
 ]
+
+
+NEW = {"martinsville_all_idle", "daytona_low_reward", "daytona_damage", "nascar_backward", "nascar_banked_discrete",
+       "michigan_discrete1", "talladega_10car"}
 
 
 def main():
@@ -565,10 +601,10 @@ def main():
                 allt[f"{tr[:-6]}__{k}"] = v
         np.savez_compressed(os.path.join(args.out, "tracks.npz"), **allt)
         print("tracks.npz", len(tracks))
-    for name, track, C, steps, pol, rol, rat in SCENARIOS:
-        if args.only not in (None, name):
+    for name, track, C, steps, pol, rol, rat, *extra in SCENARIOS:
+        if args.only not in (None, name) and not (args.only == "new" and extra is not None and name in NEW):
             continue
-        d = run_scenario(args.ref, name, track, C, steps, pol, rol, rat)
+        d = run_scenario(args.ref, name, track, C, steps, pol, rol, rat, **(extra[0] if extra else {}))
         np.savez_compressed(os.path.join(args.out, f"env_{name}.npz"), **d)
         term = d["terminated"].nonzero()[0]
         print(name, "steps", len(d["obs"]), "laps", np.nanmax(d["info"][..., 0]), "disabled", d["info"][-1, :, 8],

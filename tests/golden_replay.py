@@ -18,6 +18,19 @@ def load(name):
     return {k: d[k] for k in d.files}
 
 
+DISCRETE_TO_CONTINUOUS = np.array([[0, 0], [1, 0], [-1, 0], [0, -1], [0, 1]], np.float32)  # src/base_env.py:227-252
+
+
+def is_discrete(d):
+    return bool(d.get("discrete", False))
+
+
+def continuous_actions(d, k):
+    """step k's actions as [C, 2] float32 (discrete fixtures mapped with BaseEnv._discrete_to_continuous)"""
+    a = d["actions"][k]
+    return DISCRETE_TO_CONTINUOUS[a] if is_discrete(d) else a
+
+
 def first_mismatch(a, b):
     """index of the first step whose arrays differ (== semantics, NaN==NaN), or -1"""
     a = np.asarray(a); b = np.asarray(b)

@@ -14,7 +14,9 @@ def _replay_carenv(name, steps=None):
     from nascargymnasium_amd import CarEnv
     d = load(name)
     C = int(d["C"])
-    env = CarEnv(track_file=os.path.join(TRACKS, str(d["track"])), num_cars=C, reset_on_lap=bool(d["reset_on_lap"]))
+    disc = bool(d.get("discrete", False))
+    env = CarEnv(track_file=os.path.join(TRACKS, str(d["track"])), num_cars=C, reset_on_lap=bool(d["reset_on_lap"]),
+                 discrete_action_space=disc)
     obs, info = env.reset(seed=0)
     want0 = d["obs0"][0] if C == 1 else d["obs0"]
     assert obs.shape == ((38,) if C == 1 else (C, 38)) and obs.dtype == np.float32
@@ -30,7 +32,11 @@ def _replay_carenv(name, steps=None):
                 j += 1
             continue
         a = d["actions"][k]
-        obs, rew, term, trunc, info = env.step(a[0] if C == 1 else a)
+        if disc:
+            a = a.astype(np.int64)          # what MultiDiscrete.sample() / a policy hands over
+            obs, rew, term, trunc, info = env.step(int(a[0]) if C == 1 else a)
+        else:
+            obs, rew, term, trunc, info = env.step(a[0] if C == 1 else a)
         if C == 1:
             assert isinstance(rew, np.float32) and obs.shape == (38,)
         assert bool(term) == bool(d["terminated"][k]) and bool(trunc) == bool(d["truncated"][k]), k
@@ -45,7 +51,9 @@ def _replay_carenv(name, steps=None):
     env.close()
 
 
-@pytest.mark.parametrize("name", ["daytona_mixed", "daytona_crash", "martinsville_lap", "nascar2_seam"])
+@pytest.mark.parametrize("name", ["daytona_mixed", "daytona_crash", "martinsville_lap", "nascar2_seam",
+                                  "nascar_banked_discrete", "michigan_discrete1", "talladega_10car",
+                                  "daytona_low_reward"])
 def test_carenv_golden(name):
     _replay_carenv(name)
 

@@ -10,7 +10,7 @@ import os
 import numpy as np
 import pytest
 
-from golden_replay import TRACKS, first_mismatch, load, scenarios
+from golden_replay import TRACKS, first_mismatch, is_discrete, load, scenarios
 
 pytestmark = pytest.mark.gpu
 
@@ -71,7 +71,8 @@ def test_golden_trace_gpu(name):
             o = env.reset().cpu().numpy()
             r = np.zeros((E, C), np.float32); t = tr = np.zeros(E, bool); rs = np.zeros(E, np.int64)
         else:
-            a = torch.from_numpy(np.broadcast_to(d["actions"][k], (E, C, 2)).copy()).cuda()
+            shape = (E, C) if is_discrete(d) else (E, C, 2)      # discrete: int32 actions through the kernel's mapping
+            a = torch.from_numpy(np.broadcast_to(d["actions"][k], shape).copy()).cuda()
             o, r, t, tr = env.step(a)
             o, r, t, tr = o.cpu().numpy(), r.cpu().numpy(), t.cpu().numpy(), tr.cpu().numpy()
             rs = env.termination_reason().cpu().numpy()
@@ -199,6 +200,7 @@ def test_device_rule_driver_matches_reference_controller(name, car):
     env = _env(str(d["track"]), 1, C, bool(d["reset_on_lap"]))
     env.reset()
     acts = d["actions"]
+    assert not is_discrete(d)
     for k in range(len(acts)):
         a = env.policy_actions(1).clone()[0, car].cpu().numpy()
         if d["reset"][k]:

@@ -14,7 +14,7 @@ import os
 import numpy as np
 import pytest
 
-from golden_replay import GOLDEN, TRACKS, first_mismatch, load, scenarios
+from golden_replay import GOLDEN, TRACKS, continuous_actions, first_mismatch, load, scenarios
 from oracle_lib import OracleEnv
 
 TRACK_NAMES = sorted(f[:-6] for f in os.listdir(TRACKS) if f.endswith(".track"))
@@ -60,7 +60,7 @@ def replay_oracle(d):
             r = np.zeros_like(r)
             ef = ef.copy(); ef[0, :2] = 0
         else:
-            o, r, cf, ef = env.step(d["actions"][k][None])
+            o, r, cf, ef = env.step(continuous_actions(d, k)[None])
         if keep is None or k in keep:
             O.append(o[0])
             I.append([[env.car_info(i)[f] for _, f in INFO_MAP] for i in range(C)])

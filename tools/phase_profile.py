@@ -54,13 +54,16 @@ def main():
     ap.add_argument("--lib", default="libnascar_prof.so")
     ap.add_argument("--up", action="store_true", help="library built with -DNASCAR_PROFILE_UP")
     ap.add_argument("--raw", type=int, default=0, help="print this many raw sensor stamp rows")
+    ap.add_argument("--load-state", default=None, help="start from a bench.py --save-state file (steady state); "
+                    "actions then come from the device noisy rule driver (policy 3) instead of uniform draws")
+    ap.add_argument("--define", action="append", default=[], help="extra -D for the profile build")
     ap.add_argument("--count", action="store_true", help="library built with -DNASCAR_PROFILE_COUNT (sensor event "
                     "counters; the atomics distort that build's sensor timings)")
     a = ap.parse_args()
     so = os.path.join(ROOT, "tools", a.lib)
     if not a.no_build:
         subprocess.run(["hipcc"] + _lib.HIPCC_FLAGS + ["-DNASCAR_PROFILE"] + (["-DNASCAR_PROFILE_UP"] if a.up else [])
-                       + (["-DNASCAR_PROFILE_COUNT"] if a.count else [])
+                       + (["-DNASCAR_PROFILE_COUNT"] if a.count else []) + ["-D" + d for d in a.define]
                        + ["-o", so, os.path.join(_lib.CSRC, "nascar_kernels.hip")], check=True)
     _lib.LIB_PATH = so
     import torch
@@ -72,12 +75,23 @@ def main():
     env.reset()
     g = torch.Generator(device="cuda:0")
     g.manual_seed(7)
-    for _ in range(a.warmup):
-        env.step(torch.rand((a.envs, a.cars, 2), generator=g, device="cuda:0") * 2 - 1, auto_reset=True)
+    k0 = 0
+    if a.load_state:
+        blob = torch.load(a.load_state, map_location="cuda:0", weights_only=True)
+        env.set_state(blob["state"])
+        env.obs.copy_(blob["obs"])
+        k0 = int(blob["step"])
+
+    def actions(k):
+        if a.load_state:
+            return env.policy_actions(3, seed=0, step=k).clone()
+        return torch.rand((a.envs, a.cars, 2), generator=g, device="cuda:0") * 2 - 1
+    for k in range(a.warmup):
+        env.step(actions(k0 + k), auto_reset=True)
     buf = torch.zeros(LPROF_BASE + NW * 16, dtype=torch.int64, device="cuda:0")
     L.nascar_debug_profile(ctypes.c_void_p(buf.data_ptr()))
     for s in range(a.steps):
-        acts = torch.rand((a.envs, a.cars, 2), generator=g, device="cuda:0") * 2 - 1
+        acts = actions(k0 + a.warmup + s)
         buf.zero_()
         torch.cuda.synchronize()
         env.launch_step(acts, auto_reset=True)
@@ -118,6 +132,10 @@ def main():
                      f"walls {cnt[3] / n:.1f}, wall-ray pairs {cnt[4] / n:.1f}, exact casts {cnt[5] / n:.1f}")
         phases(sens, SENSOR, 0, "sensor_kernel", extra)
         cb = b[2 * NW * 16 + 8:2 * NW * 16 + 16]
+        if cb[4] or cb[5] or cb[6]:
+            ncar = a.envs * a.cars
+            print(f"model counters per car-step: TOI solved {cb[4] / ncar:.3f}, TOI culled {cb[5] / ncar:.3f}, "
+                  f"contact updates {cb[6] / ncar:.3f}, TOI events {cb[7] / ncar:.4f}")
         if cb[0]:
             print(f"ray_sensor_kernel: rays {cb[0]}, fallback rays {cb[1]} ({100 * cb[1] / cb[0]:.2f}%), "
                   f"list entries per ray {cb[3] / max(1, cb[0] - cb[1]):.2f}, walked {cb[2] / max(1, cb[0] - cb[1]):.2f}")
