@@ -58,7 +58,11 @@ __device__ unsigned long long* g_prof = nullptr;
 #define LPROF_BASE (APROF_BASE + 4096 * 16)
 #define LPROF(ph) do { unsigned long long _t = __builtin_amdgcn_s_memtime(); \
     if (g_prof && (threadIdx.x & 63) == 0) g_prof[LPROF_BASE + ((size_t)blockIdx.x * (SBLOCK / 64) + threadIdx.x / 64) * 16 + (ph)] = _t; } while (0)
+// per-car counters of the Box2D step (model_kernel lane of car c.pid, no atomics): region after logic's
+#define CPROF_BASE (LPROF_BASE + 65536 * 16)
+#define CCOUNT(c, slot, v) do { if (g_prof) g_prof[CPROF_BASE + (size_t)(c).pid * 8 + (slot)] += (unsigned long long)(v); } while (0)
 #else
+#define CCOUNT(c, slot, v) do { } while (0)
 #define PROF(ph) do { } while (0)
 #define PROFS(ph) do { } while (0)
 #define PROFS_RT(ph) do { } while (0)
@@ -160,7 +164,7 @@ __device__ __forceinline__ float fmaxb(float a, float b) { return a > b ? a : b;
 __device__ __forceinline__ float fclamp(float a, float lo, float hi) { return fmaxb(lo, fminb(a, hi)); }
 __device__ __forceinline__ V2 vmin(V2 a, V2 b) { return V(fminb(a.x, b.x), fminb(a.y, b.y)); }
 __device__ __forceinline__ V2 vmax(V2 a, V2 b) { return V(fmaxb(a.x, b.x), fmaxb(a.y, b.y)); }
-__device__ __forceinline__ Rot rot_set(float a) { Rot q; q.s = dev_sinf(a); q.c = dev_cosf(a); return q; }
+__device__ __forceinline__ Rot rot_set(float a) { Rot q; glibc_sincosf(a, &q.s, &q.c); return q; }
 __device__ __forceinline__ V2 zero2() { return V(0.0f, 0.0f); }
 
 // ------------------------------------------------------------------ polygons
@@ -247,6 +251,7 @@ struct Car {
   V2 force; float torque; V2 c0; float a0; float alpha0;
   Aabb fat; int moved; float invdt0;
   int nct, overflow;
+  int pid;            // car index (profile builds' per-car counters only)
   // Car / TyreManager (float64 like the reference's Python)
   double thr_in, brk_in, str_in, thr, brk, steer;
   double rpm, pvx, pvy, lfm, slip, bank;
@@ -507,7 +512,7 @@ __device__ inline void world_manifold(const DContact& m, Xf xfA, Xf xfB, V2* nor
 
 // b2Contact::Update
 __device__ inline void contact_update(Car& c, int ci, const LWall* W) {
-  PCOUNT(14, 1);
+  PCOUNT(14, 1); CCOUNT(c, 5, 1);
   DContact& ct = c.ct[ci];
   DContact old = ct;
   ct.flags |= CT_ENABLED;
@@ -953,6 +958,16 @@ __device__ __forceinline__ Xf sweep_xf(const Sweep& s, float beta) {
   xf.p = vsub(xf.p, rmul(xf.q, zero2()));
   return xf;
 }
+// b2Sweep::GetTransform of a static body's sweep (c0 == c, a0 == a): the interpolated angle is usually a0
+// again, and then its rotation is q0 (rot_set(a0), computed once per TOI call) -- same values, one sincos less
+__device__ __forceinline__ Xf sweep_xf_static(const Sweep& s, float beta, Rot q0) {
+  Xf xf;
+  xf.p = vadd(vmul(1.0f - beta, s.c0), vmul(beta, s.c));
+  float angle = (1.0f - beta) * s.a0 + beta * s.a;
+  xf.q = angle == s.a0 ? q0 : rot_set(angle);
+  xf.p = vsub(xf.p, rmul(xf.q, zero2()));
+  return xf;
+}
 __device__ __forceinline__ void sweep_normalize(Sweep& s) {
   float twoPi = 2.0f * B2_PI;
   float d = twoPi * floorf(fdiv_cr(s.a0, twoPi));
@@ -960,10 +975,12 @@ __device__ __forceinline__ void sweep_normalize(Sweep& s) {
 }
 
 enum { SF_POINTS, SF_FACEA, SF_FACEB };
-struct SepFn { Sweep sA, sB; int type; V2 lp, axis; };
-__device__ inline void sep_init(SepFn& f, const SCache& cache, const Poly* pA, const Sweep& sA, const Poly* pB, const Sweep& sB, float t1) {
-  f.sA = sA; f.sB = sB;
-  Xf xfA = sweep_xf(f.sA, t1), xfB = sweep_xf(f.sB, t1);
+// body B (the wall) is static in every TOI here: its sweep transforms go through sweep_xf_static with qB
+struct SepFn { Sweep sA, sB; Rot qB; int type; V2 lp, axis; };
+__device__ inline void sep_init(SepFn& f, const SCache& cache, const Poly* pA, const Sweep& sA, const Poly* pB, const Sweep& sB,
+                                Rot qB, float t1) {
+  f.sA = sA; f.sB = sB; f.qB = qB;
+  Xf xfA = sweep_xf(f.sA, t1), xfB = sweep_xf_static(f.sB, t1, qB);
   if (cache.count == 1) {
     f.type = SF_POINTS;
     V2 pointA = xmul(xfA, pv(pA, cache.iA[0])), pointB = xmul(xfB, pv(pB, cache.iB[0]));
@@ -993,7 +1010,7 @@ __device__ inline void sep_init(SepFn& f, const SCache& cache, const Poly* pA, c
   }
 }
 __device__ inline float sep_find_min(const SepFn& f, const Poly* pA, const Poly* pB, int* iA, int* iB, float t) {
-  Xf xfA = sweep_xf(f.sA, t), xfB = sweep_xf(f.sB, t);
+  Xf xfA = sweep_xf(f.sA, t), xfB = sweep_xf_static(f.sB, t, f.qB);
   if (f.type == SF_POINTS) {
     V2 axisA = rmulT(xfA.q, f.axis), axisB = rmulT(xfB.q, vneg(f.axis));
     *iA = support(pA, axisA); *iB = support(pB, axisB);
@@ -1014,7 +1031,7 @@ __device__ inline float sep_find_min(const SepFn& f, const Poly* pA, const Poly*
   }
 }
 __device__ inline float sep_eval(const SepFn& f, const Poly* pA, const Poly* pB, int iA, int iB, float t) {
-  Xf xfA = sweep_xf(f.sA, t), xfB = sweep_xf(f.sB, t);
+  Xf xfA = sweep_xf(f.sA, t), xfB = sweep_xf_static(f.sB, t, f.qB);
   if (f.type == SF_POINTS) {
     V2 pointA = xmul(xfA, pv(pA, iA)), pointB = xmul(xfB, pv(pB, iB));
     return vdot(vsub(pointB, pointA), f.axis);
@@ -1027,11 +1044,13 @@ __device__ inline float sep_eval(const SepFn& f, const Poly* pA, const Poly* pB,
   }
 }
 enum { TOI_UNKNOWN, TOI_FAILED, TOI_OVERLAPPED, TOI_TOUCHING, TOI_SEPARATED };
-__device__ inline float time_of_impact(int* state, const Poly* pA, const Sweep& sweepA, const Poly* pB, const Sweep& sweepB, float tMax) {
+__device__ inline float time_of_impact(int* state, const Poly* pA, const Sweep& sweepA, const Poly* pB, const Sweep& sweepB, float tMax,
+                                      int* prof_iters = nullptr) {
   *state = TOI_UNKNOWN;
   float out_t = tMax;
   Sweep sA = sweepA, sB = sweepB;
   sweep_normalize(sA); sweep_normalize(sB);
+  const Rot qB = rot_set(sB.a0);
   float totalRadius = pA->radius + pB->radius;
   float target = fmaxb(LINEAR_SLOP, totalRadius - 3.0f * LINEAR_SLOP);
   float tolerance = 0.25f * LINEAR_SLOP;
@@ -1039,12 +1058,12 @@ __device__ inline float time_of_impact(int* state, const Poly* pA, const Sweep& 
   int iter = 0;
   SCache cache; cache.count = 0; cache.metric = 0.0f;
   for (;;) {
-    Xf xfA = sweep_xf(sA, t1), xfB = sweep_xf(sB, t1);
+    Xf xfA = sweep_xf(sA, t1), xfB = sweep_xf_static(sB, t1, qB);
     float distance = gjk_distance(cache, pA, xfA, pB, xfB);
     if (distance <= 0.0f) { *state = TOI_OVERLAPPED; out_t = 0.0f; break; }
     if (distance < target + tolerance) { *state = TOI_TOUCHING; out_t = t1; break; }
     SepFn fcn;
-    sep_init(fcn, cache, pA, sA, pB, sB, t1);
+    sep_init(fcn, cache, pA, sA, pB, sB, qB, t1);
     bool done = false;
     float t2 = tMax;
     int pushBackIter = 0;
@@ -1063,6 +1082,9 @@ __device__ inline float time_of_impact(int* state, const Poly* pA, const Sweep& 
         if (rootIterCount & 1) t = a1 + fdiv_cr((target - s1) * (a2 - a1), s2 - s1);
         else t = 0.5f * (a1 + a2);
         ++rootIterCount;
+#ifdef NASCAR_PROFILE
+        if (prof_iters) ++prof_iters[1];
+#endif
         float s = sep_eval(fcn, pA, pB, indexA, indexB, t);
         if (fabsf(s - target) < tolerance) { t2 = t; break; }
         if (s > target) { a1 = t; s1 = s; } else { a2 = t; s2 = s; }
@@ -1072,6 +1094,9 @@ __device__ inline float time_of_impact(int* state, const Poly* pA, const Sweep& 
       if (pushBackIter == 8) break;
     }
     ++iter;
+#ifdef NASCAR_PROFILE
+    if (prof_iters) ++prof_iters[0];
+#endif
     if (done) break;
     if (iter == 20) { *state = TOI_FAILED; out_t = t1; break; }
   }
@@ -1134,16 +1159,23 @@ __device__ inline void solve_toi(Car& c, const WallSet& S, float dt, float frict
         float alpha0 = c.alpha0;
         const LWall& wl = W[ct.wall];
         if (toi_far(c, &pa, wl)) {
-          PCOUNT(13, 1);
+          PCOUNT(13, 1); CCOUNT(c, 3, 1);
           ct.toi = 1.0f; ct.flags |= CT_TOI;
           continue;   // alpha = 1: never below minAlpha
         }
-        PCOUNT(12, 1);
+        PCOUNT(12, 1); CCOUNT(c, 2, 1);
         Poly pb; make_box(&pb, wl.hx, wl.hy);
         Sweep sA; sA.c0 = c.c0; sA.c = c.c; sA.a0 = c.a0; sA.a = c.a; sA.alpha0 = c.alpha0;
         Sweep sB; sB.c0 = V(wl.px, wl.py); sB.c = sB.c0; sB.a0 = wl.ang; sB.a = wl.ang; sB.alpha0 = 0.0f;
         int state;
+#ifdef NASCAR_PROFILE
+        int pit[2] = {0, 0};
+        float beta = time_of_impact(&state, &pa, sA, &pb, sB, 1.0f, pit);
+        CCOUNT(c, 6, pit[0]); CCOUNT(c, 7, pit[1]);
+        if (state == TOI_FAILED) CCOUNT(c, 1, 1000);
+#else
         float beta = time_of_impact(&state, &pa, sA, &pb, sB, 1.0f);
+#endif
         if (state == TOI_TOUCHING) alpha = fminb(alpha0 + (1.0f - alpha0) * beta, 1.0f);
         else alpha = 1.0f;
         ct.toi = alpha; ct.flags |= CT_TOI;
@@ -1151,7 +1183,7 @@ __device__ inline void solve_toi(Car& c, const WallSet& S, float dt, float frict
       if (alpha < minAlpha) { minC = i; minAlpha = alpha; }
     }
     if (minC < 0 || 1.0f - 10.0f * FLT_EPS < minAlpha) break;
-    PCOUNT(15, 1);
+    PCOUNT(15, 1); CCOUNT(c, 4, 1);
     V2 bc0 = c.c0, bc = c.c; float ba0 = c.a0, ba = c.a, balpha0 = c.alpha0;
     {
       float beta = fdiv_cr(minAlpha - c.alpha0, 1.0f - c.alpha0);
@@ -1198,11 +1230,22 @@ __device__ inline void b2_step(Car& c, const WallSet& S, float dt, float frictio
   const LWall* W = S.W;
   float inv_dt = dt > 0.0f ? fdiv_cr(1.0f, dt) : 0.0f;
   float dtRatio = c.invdt0 * dt;
+#ifdef NASCAR_PROFILE
+  const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+  CCOUNT(c, 1, c.nct);
+#endif
   collide(c, W);
   PROFB(11);
   solve(c, S, dt, dtRatio, friction);
   PROFB(13);
+#ifdef NASCAR_PROFILE
+  const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+#endif
   solve_toi(c, S, dt, friction);
+#ifdef NASCAR_PROFILE
+  const unsigned long long t2 = __builtin_amdgcn_s_memtime();
+  CCOUNT(c, 0, t2 - t0); (void)t1;
+#endif
   c.invdt0 = inv_dt;
   c.force = zero2(); c.torque = 0.0f;
 }

@@ -1330,6 +1330,7 @@ __global__ void __launch_bounds__(SBLOCK) __attribute__((amdgpu_waves_per_eu(MOD
   // car state and action requested before the segment staging barrier (their round trips overlap the
   // staging's instead of following it: 89 -> 84 us per step)
   if (env >= 0) car_load_phys(P, n, c);
+  c.pid = n;
   // actions (BaseEnv._convert_to_internal_action / _discrete_to_continuous, np.float32)
   float tb = 0.0f, st = 0.0f;
   if (env >= 0) {
@@ -2287,7 +2288,7 @@ extern "C" int nascar_policy_actions(NascarHandle* h, int32_t policy, uint64_t s
 // ------------------------------------------------------------------ test hook: b2Rot::Set numerics
 __global__ void sincos_kernel(const float* x, float* s, float* c, int n) {
   int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) { s[i] = dev_sinf(x[i]); c[i] = dev_cosf(x[i]); }
+  if (i < n) glibc_sincosf(x[i], &s[i], &c[i]);
 }
 static uint16_t f32_to_bf16_rne(float f) {
   uint32_t u; memcpy(&u, &f, 4);

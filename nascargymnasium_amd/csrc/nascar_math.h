@@ -23,57 +23,71 @@ namespace nascar {
 __device__ __forceinline__ float fsqrt_cr(float x) { return sqrtf(x); }
 __device__ __forceinline__ float fdiv_cr(float a, float b) { return a / b; }
 
-struct SinCosTable {
-  double sign[4], hpi_inv, hpi, c0, c1, s1, c2, s2, c3, s3, c4;
-};
+// glibc's __sincosf_table (sysdeps/ieee754/flt-32/s_sincosf.h) as immediates: its second row is the first with
+// every cosine coefficient negated (sine coefficients equal), and negating all coefficients of a fused
+// multiply-add chain negates its result exactly, so the row choice becomes a final sign flip.  No table
+// loads are left on the chain (a lane-dependent row index had turned them into per-lane memory loads).
+#define SC_HPI_INV 0x1.45f306dc9c883p+23
+#define SC_HPI 0x1.921fb54442d18p+0
+#define SC_C0 0x1p0
+#define SC_C1 (-0x1.ffffffd0c621cp-2)
+#define SC_S1 (-0x1.555545995a603p-3)
+#define SC_C2 0x1.55553e1068f19p-5
+#define SC_S2 0x1.1107605230bc4p-7
+#define SC_C3 (-0x1.6c087e89a359dp-10)
+#define SC_S3 (-0x1.994eb3774cf24p-13)
+#define SC_C4 0x1.99343027bf8c3p-16
 
-__device__ __constant__ const SinCosTable kSC[2] = {
-    {{1.0, -1.0, -1.0, 1.0}, 0x1.45f306dc9c883p+23, 0x1.921fb54442d18p+0, 0x1p0, -0x1.ffffffd0c621cp-2,
-     -0x1.555545995a603p-3, 0x1.55553e1068f19p-5, 0x1.1107605230bc4p-7, -0x1.6c087e89a359dp-10,
-     -0x1.994eb3774cf24p-13, 0x1.99343027bf8c3p-16},
-    {{1.0, -1.0, -1.0, 1.0}, 0x1.45f306dc9c883p+23, 0x1.921fb54442d18p+0, -0x1p0, 0x1.ffffffd0c621cp-2,
-     -0x1.555545995a603p-3, -0x1.55553e1068f19p-5, 0x1.1107605230bc4p-7, 0x1.6c087e89a359dp-10,
-     -0x1.994eb3774cf24p-13, -0x1.99343027bf8c3p-16}};
+__host__ __device__ __forceinline__ uint32_t f_as_u(float f) {
+  union { float f; uint32_t u; } v; v.f = f; return v.u;
+}
+__host__ __device__ __forceinline__ uint32_t top12(float x) { return (f_as_u(x) >> 20) & 0x7ff; }
 
-__device__ __constant__ const uint32_t kInvPio4[24] = {
-    0xa2,       0xa2f9,     0xa2f983,   0xa2f9836e, 0xf9836e4e, 0x836e4e44, 0x6e4e4415, 0x4e441529,
-    0x441529fc, 0x1529fc27, 0x29fc2757, 0xfc2757d1, 0x2757d1f5, 0x57d1f534, 0xd1f534dd, 0xf534ddc0,
-    0x34ddc0db, 0xddc0db62, 0xc0db6295, 0xdb629599, 0x6295993c, 0x95993c43, 0x993c4390, 0x3c439041};
-
-__device__ __forceinline__ uint32_t f_as_u(float f) { return __float_as_uint(f); }
-__device__ __forceinline__ uint32_t top12(float x) { return (f_as_u(x) >> 20) & 0x7ff; }
-
-__device__ __forceinline__ float sc_poly(double x, double x2, const SinCosTable* p, int n) {
+// glibc sinf_poly (FMA variant): the sine polynomial for even n, the cosine polynomial (negated for the
+// second table row, neg != 0) for odd n
+__host__ __device__ __forceinline__ float sc_poly(double x, double x2, int n, int neg) {
   if ((n & 1) == 0) {
     double x3 = x * x2;
-    double s1 = __fma_rn(x2, p->s3, p->s2);
+    double s1 = fma(x2, SC_S3, SC_S2);
     double x7 = x3 * x2;
-    double s = __fma_rn(x3, p->s1, x);
-    return (float)__fma_rn(x7, s1, s);
-  } else {
-    double x4 = x2 * x2;
-    double c2 = __fma_rn(x2, p->c4, p->c3);
-    double c1 = __fma_rn(x2, p->c1, p->c0);
-    double x6 = x4 * x2;
-    double c = __fma_rn(x4, p->c2, c1);
-    return (float)__fma_rn(x6, c2, c);
+    double s = fma(x3, SC_S1, x);
+    return (float)fma(x7, s1, s);
   }
+  double x4 = x2 * x2;
+  double c2 = fma(x2, SC_C4, SC_C3);
+  double c1 = fma(x2, SC_C1, SC_C0);
+  double x6 = x4 * x2;
+  double c = fma(x4, SC_C2, c1);
+  float r = (float)fma(x6, c2, c);
+  return neg ? -r : r;
 }
-__device__ __forceinline__ double reduce_fast(double x, const SinCosTable* p, int* np) {
-  double r = x * p->hpi_inv;
+__host__ __device__ __forceinline__ double reduce_fast(double x, int* np) {
+  double r = x * SC_HPI_INV;
   int n = ((int32_t)r + 0x800000) >> 24;
   *np = n;
-  return __fma_rn(-(double)n, p->hpi, x);
+  return fma(-(double)n, SC_HPI, x);
 }
-__device__ __forceinline__ double reduce_large(uint32_t xi, int* np) {
-  const uint32_t* arr = &kInvPio4[(xi >> 26) & 15];
+#define SC_INV_PIO4 {0xa2,       0xa2f9,     0xa2f983,   0xa2f9836e, 0xf9836e4e, 0x836e4e44, 0x6e4e4415, 0x4e441529, \
+                     0x441529fc, 0x1529fc27, 0x29fc2757, 0xfc2757d1, 0x2757d1f5, 0x57d1f534, 0xd1f534dd, 0xf534ddc0, \
+                     0x34ddc0db, 0xddc0db62, 0xc0db6295, 0xdb629599, 0x6295993c, 0x95993c43, 0x993c4390, 0x3c439041}
+__device__ __constant__ const uint32_t kInvPio4[24] = SC_INV_PIO4;   // glibc __inv_pio4
+static const uint32_t kInvPio4Host[24] = SC_INV_PIO4;
+__host__ __device__ __forceinline__ uint32_t inv_pio4(int i) {
+#ifdef __HIP_DEVICE_COMPILE__
+  return kInvPio4[i];
+#else
+  return kInvPio4Host[i];
+#endif
+}
+__host__ __device__ inline double reduce_large(uint32_t xi, int* np) {   // |y| >= 120: rare (wound-up angles)
+  const int k = (xi >> 26) & 15;
   int shift = (xi >> 23) & 7;
   uint64_t n, res0, res1, res2;
   xi = (xi & 0xffffff) | 0x800000;
   xi <<= shift;
-  res0 = xi * arr[0];
-  res1 = (uint64_t)xi * arr[4];
-  res2 = (uint64_t)xi * arr[8];
+  res0 = xi * inv_pio4(k);
+  res1 = (uint64_t)xi * inv_pio4(k + 4);
+  res2 = (uint64_t)xi * inv_pio4(k + 8);
   res0 = (res2 >> 32) | (res0 << 32);
   res0 += res1;
   n = (res0 + (1ULL << 61)) >> 62;
@@ -82,53 +96,34 @@ __device__ __forceinline__ double reduce_large(uint32_t xi, int* np) {
   *np = (int)n;
   return x * 0x1.921FB54442D18p-62;
 }
-// glibc sinf (sysdeps/ieee754/flt-32/s_sinf.c), FMA variant
-__device__ inline float dev_sinf(float y) {
-  double x = y, s;
-  int n;
-  const SinCosTable* p = &kSC[0];
+// glibc sinf and cosf (sysdeps/ieee754/flt-32/s_sinf.c, s_cosf.c; FMA variant) of the same argument in one
+// pass: both share the range reduction, and each result is bit-identical to the separate call (the same
+// operations on the same values).  b2Rot::Set calls sinf then cosf.
+__host__ __device__ inline void glibc_sincosf(float y, float* sp, float* cp) {
+  double x = y;
+  int n = 0, row = 0;
+  double sgn = 1.0;
   const float pio4 = 0x1.921FB6p-1f;
   if (top12(y) < top12(pio4)) {
+    if (top12(y) < top12(0x1p-12f)) { *sp = y; *cp = 1.0f; return; }
     double x2 = x * x;
-    if (top12(y) < top12(0x1p-12f)) return y;
-    return sc_poly(x, x2, p, 0);
+    *sp = sc_poly(x, x2, 0, 0);
+    *cp = sc_poly(x, x2, 1, 0);
+    return;
   } else if (top12(y) < top12(120.0f)) {
-    x = reduce_fast(x, p, &n);
-    s = p->sign[n & 3];
-    if (n & 2) p = &kSC[1];
-    return sc_poly(x * s, x * x, p, n);
+    x = reduce_fast(x, &n);
+    sgn = ((n + 1) & 2) ? -1.0 : 1.0;   // {1, -1, -1, 1}[n & 3]
+    row = n & 2;
   } else {
     uint32_t xi = f_as_u(y);
     int sign = xi >> 31;
     x = reduce_large(xi, &n);
-    s = p->sign[(n + sign) & 3];
-    if ((n + sign) & 2) p = &kSC[1];
-    return sc_poly(x * s, x * x, p, n);
+    sgn = ((n + sign + 1) & 2) ? -1.0 : 1.0;
+    row = (n + sign) & 2;
   }
-}
-// glibc cosf (sysdeps/ieee754/flt-32/s_cosf.c), FMA variant
-__device__ inline float dev_cosf(float y) {
-  double x = y, s;
-  int n;
-  const SinCosTable* p = &kSC[0];
-  const float pio4 = 0x1.921FB6p-1f;
-  if (top12(y) < top12(pio4)) {
-    double x2 = x * x;
-    if (top12(y) < top12(0x1p-12f)) return 1.0f;
-    return sc_poly(x, x2, p, 1);
-  } else if (top12(y) < top12(120.0f)) {
-    x = reduce_fast(x, p, &n);
-    s = p->sign[n & 3];
-    if (n & 2) p = &kSC[1];
-    return sc_poly(x * s, x * x, p, n ^ 1);
-  } else {
-    uint32_t xi = f_as_u(y);
-    int sign = xi >> 31;
-    x = reduce_large(xi, &n);
-    s = p->sign[(n + sign) & 3];
-    if ((n + sign) & 2) p = &kSC[1];
-    return sc_poly(x * s, x * x, p, n ^ 1);
-  }
+  const double xs = x * sgn, x2 = x * x;
+  *sp = sc_poly(xs, x2, n, row);
+  *cp = sc_poly(xs, x2, n ^ 1, row);
 }
 
 // Python float64 helpers

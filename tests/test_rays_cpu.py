@@ -16,3 +16,14 @@ def test_ray_end_points_match_direct_evaluation(tmp_path):
     assert cases == 300000 * 16
     assert bad == 0
     assert fallbacks < cases // 1000   # the direct-sincos fallback is rare (exact-angle ties only)
+
+
+def test_glibc_sincosf_restatement_matches_host_libm(tmp_path):
+    """nascar_math.h glibc_sincosf (b2Rot::Set's sinf/cosf on the device, load-free fused form) equals the host
+    glibc on every 61st float bit pattern (the whole float range was checked the same way with stride 1)."""
+    exe = tmp_path / "sincosf_harness"
+    subprocess.run(["hipcc", "-O2", "-ffp-contract=off", "-o", str(exe),
+                    os.path.join(ROOT, "tests", "native", "sincosf_harness.cpp")], check=True)
+    checked, bad = map(int, subprocess.run([str(exe), "61", "8"], capture_output=True, text=True,
+                                           check=True).stdout.split())
+    assert checked > 60_000_000 and bad == 0

@@ -88,7 +88,9 @@ def main():
         return torch.rand((a.envs, a.cars, 2), generator=g, device="cuda:0") * 2 - 1
     for k in range(a.warmup):
         env.step(actions(k0 + k), auto_reset=True)
-    buf = torch.zeros(LPROF_BASE + NW * 16, dtype=torch.int64, device="cuda:0")
+    CPROF_BASE = LPROF_BASE + NW * 16
+    N = a.envs * a.cars
+    buf = torch.zeros(CPROF_BASE + N * 8, dtype=torch.int64, device="cuda:0")
     L.nascar_debug_profile(ctypes.c_void_p(buf.data_ptr()))
     for s in range(a.steps):
         acts = actions(k0 + a.warmup + s)
@@ -116,6 +118,22 @@ def main():
             st, en = m[:, 14], m[:, 15]
             print(f"    realtime us: last start {(st.max() - st.min()) / 100:.1f}, median end {(np.median(en) - st.min()) / 100:.1f}, "
                   f"last end {(en.max() - st.min()) / 100:.1f}")
+        cp = b[CPROF_BASE:CPROF_BASE + N * 8].reshape(N, 8)
+        if cp[:, 0].any():
+            cyc = cp[:, 0]
+            print(f"  per-car b2_step cycles: mean {cyc.mean():.0f}, p50 {np.percentile(cyc, 50):.0f}, "
+                  f"p99 {np.percentile(cyc, 99):.0f}, p99.9 {np.percentile(cyc, 99.9):.0f}, max {cyc.max()}")
+            print("  slowest waves' cars: car, wave b2 cycles, contacts at start (+1000 per FAILED TOI), TOI solved, TOI culled, "
+                  "TOI events, contact updates, TOI outer iterations, root-finder iterations")
+            for i in np.argsort(-cyc)[:24]:
+                print("   ", i, *cp[i, [0, 1, 2, 3, 4, 5, 6, 7]].tolist())
+            it = cp[:, 7]
+            print(f"  root-finder iterations per car-step: mean {it.mean():.2f}, max {it.max()}, cars > 100: {(it > 100).sum()}, "
+                  f"FAILED TOIs {(cp[:, 1] // 1000).sum()}")
+            for lo, hi in [(0, 1), (1, 2), (2, 4), (4, 8), (8, 17)]:
+                m = (cp[:, 1] >= lo) & (cp[:, 1] < hi)
+                if m.any():
+                    print(f"  cars with {lo}-{hi - 1} contacts: {m.mean() * 100:5.1f}%  mean b2 cycles {cyc[m].mean():.0f}")
         phases(logic, LOGIC, 0, "logic_kernel")
         if a.raw:
             live = sens[sens[:, 0] != 0]
