@@ -60,9 +60,13 @@ __device__ unsigned long long* g_prof = nullptr;
     if (g_prof && (threadIdx.x & 63) == 0) g_prof[LPROF_BASE + ((size_t)blockIdx.x * (SBLOCK / 64) + threadIdx.x / 64) * 16 + (ph)] = _t; } while (0)
 // per-car counters of the Box2D step (model_kernel lane of car c.pid, no atomics): region after logic's
 #define CPROF_BASE (LPROF_BASE + 65536 * 16)
-#define CCOUNT(c, slot, v) do { if (g_prof) g_prof[CPROF_BASE + (size_t)(c).pid * 8 + (slot)] += (unsigned long long)(v); } while (0)
+#define CCOUNT(c, slot, v) do { if (g_prof) g_prof[CPROF_BASE + (size_t)(c).pid * 16 + (slot)] += (unsigned long long)(v); } while (0)
+#define CTIME_BEGIN() const unsigned long long _ct0 = __builtin_amdgcn_s_memtime()
+#define CTIME_END(c, slot) CCOUNT(c, slot, __builtin_amdgcn_s_memtime() - _ct0)
 #else
 #define CCOUNT(c, slot, v) do { } while (0)
+#define CTIME_BEGIN() do { } while (0)
+#define CTIME_END(c, slot) do { } while (0)
 #define PROF(ph) do { } while (0)
 #define PROFS(ph) do { } while (0)
 #define PROFS_RT(ph) do { } while (0)
@@ -168,18 +172,22 @@ __device__ __forceinline__ Rot rot_set(float a) { Rot q; glibc_sincosf(a, &q.s, 
 __device__ __forceinline__ V2 zero2() { return V(0.0f, 0.0f); }
 
 // ------------------------------------------------------------------ polygons
-// b2PolygonShape::SetAsBox(hx, hy).  The vertices/normals are kept in arrays: generating
-// them with selects on the vertex index (to save registers) was miscompiled by ROCm 7.2
-// hipcc -O3 inside find_incident_edge (wrong second incident vertex; standalone harness vs a
-// host reference: 50% of cases wrong, the array form 0%), so that is not done.
-struct Poly { V2 v[4]; V2 n[4]; float radius; };
-__device__ __forceinline__ void make_box(Poly* p, float hx, float hy) {
-  p->radius = POLY_RADIUS;
-  p->v[0] = V(-hx, -hy); p->v[1] = V(hx, -hy); p->v[2] = V(hx, hy); p->v[3] = V(-hx, hy);
-  p->n[0] = V(0.0f, -1.0f); p->n[1] = V(1.0f, 0.0f); p->n[2] = V(0.0f, 1.0f); p->n[3] = V(-1.0f, 0.0f);
+// b2PolygonShape::SetAsBox(hx, hy): vertices (-hx,-hy), (hx,-hy), (hx,hy), (-hx,hy) and normals (0,-1),
+// (1,0), (0,1), (-1,0).  Every polygon here is such a box, so vertex / normal i is generated from i by
+// sign-bit arithmetic (exact, zeros are +0 as in Box2D).  An array form sat in scratch memory under the
+// lane-varying vertex indices of the contact / GJK / TOI code (hundreds of cycles per access on the
+// serial chain of a touching car); an earlier select-chain form was miscompiled by hipcc -O3.
+struct Poly { float hx, hy, radius; };
+__device__ __forceinline__ void make_box(Poly* p, float hx, float hy) { p->hx = hx; p->hy = hy; p->radius = POLY_RADIUS; }
+__device__ __forceinline__ float with_sign(float m, uint32_t neg) { return __uint_as_float(__float_as_uint(m) | (neg << 31)); }
+__device__ __forceinline__ V2 pv(const Poly* p, int i) {
+  const uint32_t u = (uint32_t)i;
+  return V(with_sign(p->hx, (((u + 1u) >> 1) & 1u) ^ 1u), with_sign(p->hy, ((u >> 1) & 1u) ^ 1u));
 }
-__device__ __forceinline__ V2 pv(const Poly* p, int i) { return p->v[i]; }
-__device__ __forceinline__ V2 pn(const Poly* p, int i) { return p->n[i]; }
+__device__ __forceinline__ V2 pn(const Poly* p, int i) {
+  const uint32_t u = (uint32_t)i, odd = u & 1u, hi = (u >> 1) & 1u;
+  return V(with_sign((float)odd, hi & odd), with_sign((float)(odd ^ 1u), (hi ^ 1u) & (odd ^ 1u)));
+}
 __device__ __forceinline__ Aabb poly_aabb(const Poly* p, Xf xf) {
   V2 lower = xmul(xf, pv(p, 0)), upper = lower;
 #pragma unroll
@@ -350,7 +358,8 @@ __device__ inline void find_new_contacts(Car& c, const WallSet& S) {
     const float hx = 0.5f * (c.fat.hi.x - c.fat.lo.x), hy = 0.5f * (c.fat.hi.y - c.fat.lo.y);
     const float cx = 0.5f * (c.fat.hi.x + c.fat.lo.x), cy = 0.5f * (c.fat.hi.y + c.fat.lo.y);
     if (hx <= S.bp.reach - 0.05f && hy <= S.bp.reach - 0.05f && grid_list(S.bp, cx, cy, beg, end)) list = S.bp.idx;
-    else { beg = 0; end = S.nw; }
+    else { beg = 0; end = S.nw; CCOUNT(c, 8, 1); }
+    CCOUNT(c, 9, end - beg);
   }
 #if BP_BATCH > 0
   if (list && S.bp.box) {
@@ -413,24 +422,27 @@ __device__ inline float find_max_separation(int* edgeIndex, const Poly* p1, Xf x
   *edgeIndex = best;
   return maxSep;
 }
-__device__ inline void find_incident_edge(Clip c[2], const Poly* p1, Xf xf1, int edge1, const Poly* p2, Xf xf2) {
+__device__ inline void find_incident_edge(Clip& c0, Clip& c1, const Poly* p1, Xf xf1, int edge1, const Poly* p2, Xf xf2) {
   V2 normal1 = rmulT(xf2.q, rmul(xf1.q, pn(p1, edge1)));
   int index = 0; float minDot = FLT_BIG;
   for (int i = 0; i < 4; ++i) { float d = vdot(normal1, pn(p2, i)); if (d < minDot) { minDot = d; index = i; } }
   int i1 = index, i2 = i1 + 1 < 4 ? i1 + 1 : 0;
-  c[0].v = xmul(xf2, pv(p2, i1)); c[0].id = cf_key(edge1, i1, 1, 0);
-  c[1].v = xmul(xf2, pv(p2, i2)); c[1].id = cf_key(edge1, i2, 1, 0);
+  c0.v = xmul(xf2, pv(p2, i1)); c0.id = cf_key(edge1, i1, 1, 0);
+  c1.v = xmul(xf2, pv(p2, i2)); c1.id = cf_key(edge1, i2, 1, 0);
 }
-__device__ inline int clip_segment(Clip vOut[2], const Clip vIn[2], V2 normal, float offset, int vertexIndexA) {
+// b2ClipSegmentToLine with the two outputs as named values (no dynamically indexed array)
+__device__ inline int clip_segment(Clip& o0, Clip& o1, const Clip& i0, const Clip& i1, V2 normal, float offset, int vertexIndexA) {
   int numOut = 0;
-  float d0 = vdot(normal, vIn[0].v) - offset;
-  float d1 = vdot(normal, vIn[1].v) - offset;
-  if (d0 <= 0.0f) vOut[numOut++] = vIn[0];
-  if (d1 <= 0.0f) vOut[numOut++] = vIn[1];
-  if (d0 * d1 < 0.0f) {
+  float d0 = vdot(normal, i0.v) - offset;
+  float d1 = vdot(normal, i1.v) - offset;
+  if (d0 <= 0.0f) { o0 = i0; numOut = 1; }
+  if (d1 <= 0.0f) { if (numOut == 0) o0 = i1; else o1 = i1; ++numOut; }
+  if (d0 * d1 < 0.0f) {   // d0, d1 of opposite signs: exactly one was kept, the new point is the second
     float interp = fdiv_cr(d0, d0 - d1);
-    vOut[numOut].v = vadd(vIn[0].v, vmul(interp, vsub(vIn[1].v, vIn[0].v)));
-    vOut[numOut].id = cf_key(vertexIndexA, (int)((vIn[0].id >> 8) & 255), 0, 1);
+    Clip cv;
+    cv.v = vadd(i0.v, vmul(interp, vsub(i1.v, i0.v)));
+    cv.id = cf_key(vertexIndexA, (int)((i0.id >> 8) & 255), 0, 1);
+    if (numOut == 0) o0 = cv; else o1 = cv;
     ++numOut;
   }
   return numOut;
@@ -447,8 +459,8 @@ __device__ inline void collide_polygons(DContact& m, const Poly* pA, Xf xfA, con
   const float k_tol = 0.1f * LINEAR_SLOP;
   if (sepB > sepA + k_tol) { poly1 = pB; poly2 = pA; xf1 = xfB; xf2 = xfA; edge1 = edgeB; m.mtype = 2; flip = 1; }
   else { poly1 = pA; poly2 = pB; xf1 = xfA; xf2 = xfB; edge1 = edgeA; m.mtype = 1; flip = 0; }
-  Clip incident[2];
-  find_incident_edge(incident, poly1, xf1, edge1, poly2, xf2);
+  Clip inc0, inc1;
+  find_incident_edge(inc0, inc1, poly1, xf1, edge1, poly2, xf2);
   int iv1 = edge1, iv2 = edge1 + 1 < 4 ? edge1 + 1 : 0;
   V2 v11 = pv(poly1, iv1), v12 = pv(poly1, iv2);
   V2 localTangent = vsub(v12, v11);
@@ -461,23 +473,26 @@ __device__ inline void collide_polygons(DContact& m, const Poly* pA, Xf xfA, con
   float frontOffset = vdot(normal, v11);
   float sideOffset1 = -vdot(tangent, v11) + totalRadius;
   float sideOffset2 = vdot(tangent, v12) + totalRadius;
-  Clip cp1[2], cp2[2];
-  int np = clip_segment(cp1, incident, vneg(tangent), sideOffset1, iv1);
+  Clip a0, a1, b0, b1;
+  int np = clip_segment(a0, a1, inc0, inc1, vneg(tangent), sideOffset1, iv1);
   if (np < 2) return;
-  np = clip_segment(cp2, cp1, tangent, sideOffset2, iv2);
+  np = clip_segment(b0, b1, a0, a1, tangent, sideOffset2, iv2);
   if (np < 2) return;
   m.lnx = localNormal.x; m.lny = localNormal.y; m.lpx = planePoint.x; m.lpy = planePoint.y;
   int pc = 0;
+#pragma unroll
   for (int i = 0; i < 2; ++i) {
-    float separation = vdot(normal, cp2[i].v) - frontOffset;
+    const Clip& cq = i == 0 ? b0 : b1;
+    float separation = vdot(normal, cq.v) - frontOffset;
     if (separation <= totalRadius) {
-      V2 lp = xmulT(xf2, cp2[i].v);
-      uint32_t id = cp2[i].id;
+      V2 lp = xmulT(xf2, cq.v);
+      uint32_t id = cq.id;
       if (flip) {
         uint32_t ia = id & 255, ib = (id >> 8) & 255, ta = (id >> 16) & 255, tb = (id >> 24) & 255;
         id = cf_key((int)ib, (int)ia, (int)tb, (int)ta);
       }
-      m.pt[pc].lx = lp.x; m.pt[pc].ly = lp.y; m.pt[pc].id = id; m.pt[pc].ni = 0.0f; m.pt[pc].ti = 0.0f;
+      DPoint q; q.lx = lp.x; q.ly = lp.y; q.id = id; q.ni = 0.0f; q.ti = 0.0f;
+      if (pc == 0) m.pt[0] = q; else m.pt[1] = q;
       ++pc;
     }
   }
@@ -491,7 +506,9 @@ __device__ inline void world_manifold(const DContact& m, Xf xfA, Xf xfB, V2* nor
   V2 ln = V(m.lnx, m.lny), lp = V(m.lpx, m.lpy);
   if (m.mtype == 1) {
     V2 n = rmul(xfA.q, ln), planePoint = xmul(xfA, lp);
-    for (int i = 0; i < m.pointCount; ++i) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      if (i >= m.pointCount) break;
       V2 clipPoint = xmul(xfB, V(m.pt[i].lx, m.pt[i].ly));
       V2 cA = vadd(clipPoint, vmul(rA - vdot(vsub(clipPoint, planePoint), n), n));
       V2 cB = vsub(clipPoint, vmul(rB, n));
@@ -500,7 +517,9 @@ __device__ inline void world_manifold(const DContact& m, Xf xfA, Xf xfB, V2* nor
     *normal = n;
   } else {
     V2 n = rmul(xfB.q, ln), planePoint = xmul(xfB, lp);
-    for (int i = 0; i < m.pointCount; ++i) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      if (i >= m.pointCount) break;
       V2 clipPoint = xmul(xfA, V(m.pt[i].lx, m.pt[i].ly));
       V2 cB = vadd(clipPoint, vmul(rB - vdot(vsub(clipPoint, planePoint), n), n));
       V2 cA = vsub(clipPoint, vmul(rA, n));
@@ -513,8 +532,8 @@ __device__ inline void world_manifold(const DContact& m, Xf xfA, Xf xfB, V2* nor
 // b2Contact::Update
 __device__ inline void contact_update(Car& c, int ci, const LWall* W) {
   PCOUNT(14, 1); CCOUNT(c, 5, 1);
-  DContact& ct = c.ct[ci];
-  DContact old = ct;
+  DContact ct = c.ct[ci];   // register copy (one burst of loads), written back once below
+  const DContact old = ct;
   ct.flags |= CT_ENABLED;
   bool was = (ct.flags & CT_TOUCH) != 0;
   Poly pa, pb; make_box(&pa, CAR_HX, CAR_HY);
@@ -523,14 +542,16 @@ __device__ inline void contact_update(Car& c, int ci, const LWall* W) {
   Xf xfB = wall_xf(wl);
   collide_polygons(ct, &pa, c.xf, &pb, xfB);
   bool touching = ct.pointCount > 0;
-  for (int i = 0; i < ct.pointCount; ++i) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {   // warm-start impulses of the old point with the same feature id (first match)
+    if (i >= ct.pointCount) break;
     ct.pt[i].ni = 0.0f; ct.pt[i].ti = 0.0f;
-    for (int j = 0; j < old.pointCount; ++j) {
-      if (old.pt[j].id == ct.pt[i].id) { ct.pt[i].ni = old.pt[j].ni; ct.pt[i].ti = old.pt[j].ti; break; }
-    }
+    if (old.pointCount > 0 && old.pt[0].id == ct.pt[i].id) { ct.pt[i].ni = old.pt[0].ni; ct.pt[i].ti = old.pt[0].ti; }
+    else if (old.pointCount > 1 && old.pt[1].id == ct.pt[i].id) { ct.pt[i].ni = old.pt[1].ni; ct.pt[i].ti = old.pt[1].ti; }
   }
   if (touching != was) set_awake(c);
   if (touching) ct.flags |= CT_TOUCH; else ct.flags &= ~CT_TOUCH;
+  c.ct[ci] = ct;
   if (!was && touching) {
     V2 n = zero2(), pts[2];
     world_manifold(ct, c.xf, xfB, &n, pts);
@@ -841,56 +862,60 @@ __device__ inline void solve(Car& c, const WallSet& S, float dt, float dtRatio, 
 }
 
 // ------------------------------------------------------------------ GJK / TOI
+// b2Distance (GJK) with the simplex vertices and the cache indices as named values (no dynamically indexed
+// arrays: those lived in scratch memory).  Same operations in the same order as b2Simplex::ReadCache /
+// Solve2 / Solve3 / GetSearchDirection / GetWitnessPoints / WriteCache.
 struct SV { V2 wA, wB, w; float a; int iA, iB; };
-struct Simplex { SV v[3]; int count; };
-struct SCache { float metric; int count; int iA[3], iB[3]; };
+struct SCache { float metric; int count; int iA0, iA1, iA2, iB0, iB1, iB2; };
 
 __device__ __forceinline__ int support(const Poly* p, V2 d) {
   int best = 0; float bestValue = vdot(pv(p, 0), d);
   for (int i = 1; i < 4; ++i) { float value = vdot(pv(p, i), d); if (value > bestValue) { best = i; bestValue = value; } }
   return best;
 }
-__device__ inline float simplex_metric(const Simplex& s) {
-  if (s.count == 1) return 0.0f;
-  if (s.count == 2) return vlen(vsub(s.v[0].w, s.v[1].w));
-  if (s.count == 3) return vcross(vsub(s.v[1].w, s.v[0].w), vsub(s.v[2].w, s.v[0].w));
+__device__ __forceinline__ float simplex_metric(int count, const SV& v0, const SV& v1, const SV& v2) {
+  if (count == 1) return 0.0f;
+  if (count == 2) return vlen(vsub(v0.w, v1.w));
+  if (count == 3) return vcross(vsub(v1.w, v0.w), vsub(v2.w, v0.w));
   return 0.0f;
 }
+__device__ __forceinline__ void sv_set(SV& v, int ia, int ib, const Poly* pA, Xf tA, const Poly* pB, Xf tB) {
+  v.iA = ia; v.iB = ib;
+  v.wA = xmul(tA, pv(pA, ia)); v.wB = xmul(tB, pv(pB, ib));
+  v.w = vsub(v.wB, v.wA); v.a = 0.0f;
+}
 __device__ inline float gjk_distance(SCache& cache, const Poly* pA, Xf tA, const Poly* pB, Xf tB) {
-  Simplex s;
-  s.count = cache.count;
-  for (int i = 0; i < s.count; ++i) {
-    SV& v = s.v[i];
-    v.iA = cache.iA[i]; v.iB = cache.iB[i];
-    v.wA = xmul(tA, pv(pA, v.iA)); v.wB = xmul(tB, pv(pB, v.iB));
-    v.w = vsub(v.wB, v.wA); v.a = 0.0f;
+  SV v0, v1, v2;
+  v0.wA = v0.wB = v0.w = zero2(); v0.a = 0.0f; v0.iA = v0.iB = 0;
+  v2 = v1 = v0;
+  int count = cache.count;
+  if (count > 0) sv_set(v0, cache.iA0, cache.iB0, pA, tA, pB, tB);
+  if (count > 1) sv_set(v1, cache.iA1, cache.iB1, pA, tA, pB, tB);
+  if (count > 2) sv_set(v2, cache.iA2, cache.iB2, pA, tA, pB, tB);
+  if (count > 1) {
+    float metric1 = cache.metric, metric2 = simplex_metric(count, v0, v1, v2);
+    if (metric2 < 0.5f * metric1 || 2.0f * metric1 < metric2 || metric2 < FLT_EPS) count = 0;
   }
-  if (s.count > 1) {
-    float metric1 = cache.metric, metric2 = simplex_metric(s);
-    if (metric2 < 0.5f * metric1 || 2.0f * metric1 < metric2 || metric2 < FLT_EPS) s.count = 0;
+  if (count == 0) {
+    sv_set(v0, 0, 0, pA, tA, pB, tB);
+    v0.a = 1.0f;
+    count = 1;
   }
-  if (s.count == 0) {
-    SV& v = s.v[0];
-    v.iA = 0; v.iB = 0;
-    v.wA = xmul(tA, pv(pA, 0)); v.wB = xmul(tB, pv(pB, 0));
-    v.w = vsub(v.wB, v.wA); v.a = 1.0f;
-    s.count = 1;
-  }
-  int saveA[3], saveB[3], saveCount = 0, iter = 0;
+  int sA0 = 0, sA1 = 0, sA2 = 0, sB0 = 0, sB1 = 0, sB2 = 0, saveCount = 0, iter = 0;
   while (iter < 20) {
-    saveCount = s.count;
-    for (int i = 0; i < saveCount; ++i) { saveA[i] = s.v[i].iA; saveB[i] = s.v[i].iB; }
-    if (s.count == 2) {
-      V2 w1 = s.v[0].w, w2 = s.v[1].w, e12 = vsub(w2, w1);
+    saveCount = count;
+    sA0 = v0.iA; sB0 = v0.iB; sA1 = v1.iA; sB1 = v1.iB; sA2 = v2.iA; sB2 = v2.iB;
+    if (count == 2) {
+      V2 w1 = v0.w, w2 = v1.w, e12 = vsub(w2, w1);
       float d12_2 = -vdot(w1, e12);
-      if (d12_2 <= 0.0f) { s.v[0].a = 1.0f; s.count = 1; }
+      if (d12_2 <= 0.0f) { v0.a = 1.0f; count = 1; }
       else {
         float d12_1 = vdot(w2, e12);
-        if (d12_1 <= 0.0f) { s.v[1].a = 1.0f; s.count = 1; s.v[0] = s.v[1]; }
-        else { float inv = fdiv_cr(1.0f, d12_1 + d12_2); s.v[0].a = d12_1 * inv; s.v[1].a = d12_2 * inv; s.count = 2; }
+        if (d12_1 <= 0.0f) { v1.a = 1.0f; count = 1; v0 = v1; }
+        else { float inv = fdiv_cr(1.0f, d12_1 + d12_2); v0.a = d12_1 * inv; v1.a = d12_2 * inv; count = 2; }
       }
-    } else if (s.count == 3) {
-      V2 w1 = s.v[0].w, w2 = s.v[1].w, w3 = s.v[2].w;
+    } else if (count == 3) {
+      V2 w1 = v0.w, w2 = v1.w, w3 = v2.w;
       V2 e12 = vsub(w2, w1);
       float d12_1 = vdot(w2, e12), d12_2 = -vdot(w1, e12);
       V2 e13 = vsub(w3, w1);
@@ -899,53 +924,55 @@ __device__ inline float gjk_distance(SCache& cache, const Poly* pA, Xf tA, const
       float d23_1 = vdot(w3, e23), d23_2 = -vdot(w2, e23);
       float n123 = vcross(e12, e13);
       float d123_1 = n123 * vcross(w2, w3), d123_2 = n123 * vcross(w3, w1), d123_3 = n123 * vcross(w1, w2);
-      if (d12_2 <= 0.0f && d13_2 <= 0.0f) { s.v[0].a = 1.0f; s.count = 1; }
+      if (d12_2 <= 0.0f && d13_2 <= 0.0f) { v0.a = 1.0f; count = 1; }
       else if (d12_1 > 0.0f && d12_2 > 0.0f && d123_3 <= 0.0f) {
-        float inv = fdiv_cr(1.0f, d12_1 + d12_2); s.v[0].a = d12_1 * inv; s.v[1].a = d12_2 * inv; s.count = 2;
+        float inv = fdiv_cr(1.0f, d12_1 + d12_2); v0.a = d12_1 * inv; v1.a = d12_2 * inv; count = 2;
       } else if (d13_1 > 0.0f && d13_2 > 0.0f && d123_2 <= 0.0f) {
-        float inv = fdiv_cr(1.0f, d13_1 + d13_2); s.v[0].a = d13_1 * inv; s.v[2].a = d13_2 * inv; s.count = 2; s.v[1] = s.v[2];
-      } else if (d12_1 <= 0.0f && d23_2 <= 0.0f) { s.v[1].a = 1.0f; s.count = 1; s.v[0] = s.v[1]; }
-      else if (d13_1 <= 0.0f && d23_1 <= 0.0f) { s.v[2].a = 1.0f; s.count = 1; s.v[0] = s.v[2]; }
+        float inv = fdiv_cr(1.0f, d13_1 + d13_2); v0.a = d13_1 * inv; v2.a = d13_2 * inv; count = 2; v1 = v2;
+      } else if (d12_1 <= 0.0f && d23_2 <= 0.0f) { v1.a = 1.0f; count = 1; v0 = v1; }
+      else if (d13_1 <= 0.0f && d23_1 <= 0.0f) { v2.a = 1.0f; count = 1; v0 = v2; }
       else if (d23_1 > 0.0f && d23_2 > 0.0f && d123_1 <= 0.0f) {
-        float inv = fdiv_cr(1.0f, d23_1 + d23_2); s.v[1].a = d23_1 * inv; s.v[2].a = d23_2 * inv; s.count = 2; s.v[0] = s.v[2];
+        float inv = fdiv_cr(1.0f, d23_1 + d23_2); v1.a = d23_1 * inv; v2.a = d23_2 * inv; count = 2; v0 = v2;
       } else {
         float inv = fdiv_cr(1.0f, d123_1 + d123_2 + d123_3);
-        s.v[0].a = d123_1 * inv; s.v[1].a = d123_2 * inv; s.v[2].a = d123_3 * inv; s.count = 3;
+        v0.a = d123_1 * inv; v1.a = d123_2 * inv; v2.a = d123_3 * inv; count = 3;
       }
     }
-    if (s.count == 3) break;
+    if (count == 3) break;
     V2 d;
-    if (s.count == 1) d = vneg(s.v[0].w);
+    if (count == 1) d = vneg(v0.w);
     else {
-      V2 e12 = vsub(s.v[1].w, s.v[0].w);
-      float sgn = vcross(e12, vneg(s.v[0].w));
+      V2 e12 = vsub(v1.w, v0.w);
+      float sgn = vcross(e12, vneg(v0.w));
       d = sgn > 0.0f ? vcross_sv(1.0f, e12) : vcross_vs(e12, 1.0f);
     }
     if (vdot(d, d) < FLT_EPS * FLT_EPS) break;
-    SV& vx = s.v[s.count];
+    SV vx;
     vx.iA = support(pA, rmulT(tA.q, vneg(d)));
     vx.wA = xmul(tA, pv(pA, vx.iA));
     vx.iB = support(pB, rmulT(tB.q, d));
     vx.wB = xmul(tB, pv(pB, vx.iB));
     vx.w = vsub(vx.wB, vx.wA);
+    vx.a = 0.0f;
     ++iter;
-    bool dup = false;
-    for (int i = 0; i < saveCount; ++i) if (vx.iA == saveA[i] && vx.iB == saveB[i]) { dup = true; break; }
+    bool dup = (vx.iA == sA0 && vx.iB == sB0) || (saveCount > 1 && vx.iA == sA1 && vx.iB == sB1) ||
+               (saveCount > 2 && vx.iA == sA2 && vx.iB == sB2);
     if (dup) break;
-    ++s.count;
+    if (count == 1) v1 = vx; else v2 = vx;
+    ++count;
   }
   V2 wa = zero2(), wb = zero2();
-  if (s.count == 1) { wa = s.v[0].wA; wb = s.v[0].wB; }
-  else if (s.count == 2) {
-    wa = vadd(vmul(s.v[0].a, s.v[0].wA), vmul(s.v[1].a, s.v[1].wA));
-    wb = vadd(vmul(s.v[0].a, s.v[0].wB), vmul(s.v[1].a, s.v[1].wB));
-  } else if (s.count == 3) {
-    wa = vadd(vadd(vmul(s.v[0].a, s.v[0].wA), vmul(s.v[1].a, s.v[1].wA)), vmul(s.v[2].a, s.v[2].wA));
+  if (count == 1) { wa = v0.wA; wb = v0.wB; }
+  else if (count == 2) {
+    wa = vadd(vmul(v0.a, v0.wA), vmul(v1.a, v1.wA));
+    wb = vadd(vmul(v0.a, v0.wB), vmul(v1.a, v1.wB));
+  } else if (count == 3) {
+    wa = vadd(vadd(vmul(v0.a, v0.wA), vmul(v1.a, v1.wA)), vmul(v2.a, v2.wA));
     wb = wa;
   }
-  cache.metric = simplex_metric(s);
-  cache.count = s.count;
-  for (int i = 0; i < s.count; ++i) { cache.iA[i] = s.v[i].iA; cache.iB[i] = s.v[i].iB; }
+  cache.metric = simplex_metric(count, v0, v1, v2);
+  cache.count = count;
+  cache.iA0 = v0.iA; cache.iB0 = v0.iB; cache.iA1 = v1.iA; cache.iB1 = v1.iB; cache.iA2 = v2.iA; cache.iB2 = v2.iB;
   return vlen(vsub(wa, wb));
 }
 
@@ -983,28 +1010,28 @@ __device__ inline void sep_init(SepFn& f, const SCache& cache, const Poly* pA, c
   Xf xfA = sweep_xf(f.sA, t1), xfB = sweep_xf_static(f.sB, t1, qB);
   if (cache.count == 1) {
     f.type = SF_POINTS;
-    V2 pointA = xmul(xfA, pv(pA, cache.iA[0])), pointB = xmul(xfB, pv(pB, cache.iB[0]));
+    V2 pointA = xmul(xfA, pv(pA, cache.iA0)), pointB = xmul(xfB, pv(pB, cache.iB0));
     f.axis = vsub(pointB, pointA);
     vnormalize(&f.axis);
     f.lp = zero2();
-  } else if (cache.iA[0] == cache.iA[1]) {
+  } else if (cache.iA0 == cache.iA1) {
     f.type = SF_FACEB;
-    V2 lB1 = pv(pB, cache.iB[0]), lB2 = pv(pB, cache.iB[1]);
+    V2 lB1 = pv(pB, cache.iB0), lB2 = pv(pB, cache.iB1);
     f.axis = vcross_vs(vsub(lB2, lB1), 1.0f);
     vnormalize(&f.axis);
     V2 normal = rmul(xfB.q, f.axis);
     f.lp = vmul(0.5f, vadd(lB1, lB2));
-    V2 pointB = xmul(xfB, f.lp), pointA = xmul(xfA, pv(pA, cache.iA[0]));
+    V2 pointB = xmul(xfB, f.lp), pointA = xmul(xfA, pv(pA, cache.iA0));
     float s = vdot(vsub(pointA, pointB), normal);
     if (s < 0.0f) f.axis = vneg(f.axis);
   } else {
     f.type = SF_FACEA;
-    V2 lA1 = pv(pA, cache.iA[0]), lA2 = pv(pA, cache.iA[1]);
+    V2 lA1 = pv(pA, cache.iA0), lA2 = pv(pA, cache.iA1);
     f.axis = vcross_vs(vsub(lA2, lA1), 1.0f);
     vnormalize(&f.axis);
     V2 normal = rmul(xfA.q, f.axis);
     f.lp = vmul(0.5f, vadd(lA1, lA2));
-    V2 pointA = xmul(xfA, f.lp), pointB = xmul(xfB, pv(pB, cache.iB[0]));
+    V2 pointA = xmul(xfA, f.lp), pointB = xmul(xfB, pv(pB, cache.iB0));
     float s = vdot(vsub(pointB, pointA), normal);
     if (s < 0.0f) f.axis = vneg(f.axis);
   }
@@ -1057,6 +1084,7 @@ __device__ inline float time_of_impact(int* state, const Poly* pA, const Sweep& 
   float t1 = 0.0f;
   int iter = 0;
   SCache cache; cache.count = 0; cache.metric = 0.0f;
+  cache.iA0 = cache.iA1 = cache.iA2 = cache.iB0 = cache.iB1 = cache.iB2 = 0;
   for (;;) {
     Xf xfA = sweep_xf(sA, t1), xfB = sweep_xf_static(sB, t1, qB);
     float distance = gjk_distance(cache, pA, xfA, pB, xfB);
@@ -1170,7 +1198,9 @@ __device__ inline void solve_toi(Car& c, const WallSet& S, float dt, float frict
         int state;
 #ifdef NASCAR_PROFILE
         int pit[2] = {0, 0};
+        CTIME_BEGIN();
         float beta = time_of_impact(&state, &pa, sA, &pb, sB, 1.0f, pit);
+        CTIME_END(c, 10);
         CCOUNT(c, 6, pit[0]); CCOUNT(c, 7, pit[1]);
         if (state == TOI_FAILED) CCOUNT(c, 1, 1000);
 #else
@@ -1193,7 +1223,11 @@ __device__ inline void solve_toi(Car& c, const WallSet& S, float dt, float frict
       c.c = c.c0; c.a = c.a0;
       sync_transform(c);
     }
+    {
+    CTIME_BEGIN();
     contact_update(c, minC, W);
+    CTIME_END(c, 12);
+    }
     c.ct[minC].flags &= ~CT_TOI;
     ++c.ct[minC].toiCount;
     if (!(c.ct[minC].flags & CT_ENABLED) || !(c.ct[minC].flags & CT_TOUCH)) {
@@ -1205,6 +1239,8 @@ __device__ inline void solve_toi(Car& c, const WallSet& S, float dt, float frict
     set_awake(c);
     int cidx[MAX_ISLAND]; int n = 0;
     cidx[n++] = minC; c.ct[minC].flags |= CT_ISLAND;
+    {
+    CTIME_BEGIN();
     for (int i = 0; i < c.nct; ++i) {
       if (n == MAX_TOI_CONTACTS) break;
       if (n == MAX_ISLAND) {   // more touching contacts than the island buffer: flag, keep going exactly-as-far-as-possible
@@ -1218,11 +1254,21 @@ __device__ inline void solve_toi(Car& c, const WallSet& S, float dt, float frict
       c.ct[i].flags |= CT_ISLAND;
       cidx[n++] = i;
     }
+    CTIME_END(c, 12);
+    }
     float subdt = (1.0f - minAlpha) * dt;
+    {
+    CTIME_BEGIN();
     island_solve_toi(c, W, cidx, n, subdt, friction);
+    CTIME_END(c, 11);
+    }
+    {
+    CTIME_BEGIN();
     sync_fixtures(c);
     for (int i = 0; i < c.nct; ++i) c.ct[i].flags &= ~(CT_TOI | CT_ISLAND);
     find_new_contacts(c, S);
+    CTIME_END(c, 13);
+    }
   }
 }
 

@@ -90,7 +90,7 @@ def main():
         env.step(actions(k0 + k), auto_reset=True)
     CPROF_BASE = LPROF_BASE + NW * 16
     N = a.envs * a.cars
-    buf = torch.zeros(CPROF_BASE + N * 8, dtype=torch.int64, device="cuda:0")
+    buf = torch.zeros(CPROF_BASE + N * 16, dtype=torch.int64, device="cuda:0")
     L.nascar_debug_profile(ctypes.c_void_p(buf.data_ptr()))
     for s in range(a.steps):
         acts = actions(k0 + a.warmup + s)
@@ -118,15 +118,29 @@ def main():
             st, en = m[:, 14], m[:, 15]
             print(f"    realtime us: last start {(st.max() - st.min()) / 100:.1f}, median end {(np.median(en) - st.min()) / 100:.1f}, "
                   f"last end {(en.max() - st.min()) / 100:.1f}")
-        cp = b[CPROF_BASE:CPROF_BASE + N * 8].reshape(N, 8)
+        cp = b[CPROF_BASE:CPROF_BASE + N * 16].reshape(N, 16)
         if cp[:, 0].any():
             cyc = cp[:, 0]
             print(f"  per-car b2_step cycles: mean {cyc.mean():.0f}, p50 {np.percentile(cyc, 50):.0f}, "
                   f"p99 {np.percentile(cyc, 99):.0f}, p99.9 {np.percentile(cyc, 99.9):.0f}, max {cyc.max()}")
             print("  slowest waves' cars: car, wave b2 cycles, contacts at start (+1000 per FAILED TOI), TOI solved, TOI culled, "
                   "TOI events, contact updates, TOI outer iterations, root-finder iterations")
+            info = env.info_tensor().cpu().numpy().reshape(N, -1)
+            F = _lib.INFO_FIELDS
             for i in np.argsort(-cyc)[:24]:
-                print("   ", i, *cp[i, [0, 1, 2, 3, 4, 5, 6, 7]].tolist())
+                if cp[i, 1] or cp[i, 9]:
+                    print("   ", i, *cp[i, [0, 1, 2, 3, 4, 5, 6, 7]].tolist(), f"| bp full scans {cp[i, 8]}, candidates {cp[i, 9]}"
+                          f" | x {info[i, F.index('x')]:.1f} y {info[i, F.index('y')]:.1f} v ({info[i, F.index('vx')]:.1f}, "
+                          f"{info[i, F.index('vy')]:.1f}) angle {info[i, F.index('angle')]:.2f} disabled {info[i, F.index('disabled')]:.0f} n_contacts {info[i, F.index('n_contacts')]:.0f}")
+            for i in np.argsort(-cyc)[:24]:
+                if cp[i, 10:14].any():
+                    print(f"    car {i} solve_toi cycles: TOI calls {cp[i, 10]}, island solves {cp[i, 11]}, "
+                          f"event contact updates {cp[i, 12]}, event sync+broadphase {cp[i, 13]}")
+            wv = m[np.argmax(m[:, 4] - m[:, 3])]
+            print("  slowest wave's b2_step phases (cycles): collide", wv[11] - wv[3], "solve", wv[12] - wv[11],
+                  "sync+find", wv[13] - wv[12], "toi", wv[4] - wv[13])
+            print(f"  broadphase full scans per car-step {cp[:, 8].mean():.4f}, cars with a full scan {(cp[:, 8] > 0).sum()}, "
+                  f"candidates per car-step {cp[:, 9].mean():.2f}")
             it = cp[:, 7]
             print(f"  root-finder iterations per car-step: mean {it.mean():.2f}, max {it.max()}, cars > 100: {(it > 100).sum()}, "
                   f"FAILED TOIs {(cp[:, 1] // 1000).sum()}")
