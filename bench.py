@@ -130,10 +130,14 @@ def stagger_schedule(E, settle):
 
 
 class Stepper:
-    """one bench step on a BatchedCarEnv: actions from the chosen source, then the env step with auto-reset."""
+    """bench steps on a BatchedCarEnv.  Per-step path (rollout == 0): actions from the chosen source, then one env
+    step with auto-reset (nascar_policy_actions + nascar_step).  Fused path (rollout = R > 0, device action sources
+    0/1/3): R steps per nascar_rollout launch, identical results (tests/test_gpu_rollout.py)."""
 
-    def __init__(self, env, policy, seed, acts=None, gather=None):
+    def __init__(self, env, policy, seed, acts=None, gather=None, rollout=0):
         self.env, self.pol, self.seed, self.acts, self.gather = env, POLICY_ID[policy], seed, acts, gather
+        self.R = rollout if (acts is None and gather is None and self.pol != 2) else 0
+        self.traj = None
 
     def actions(self, i):
         if self.acts is not None:
@@ -146,6 +150,25 @@ class Stepper:
         if self.gather is not None:
             self.gather.push(self.env.obs, self.env.reward, self.env.car_flags, self.env.env_flags)
 
+    def run(self, first, K, trajectory=False):
+        """K steps starting at step index `first` (trajectory: per-step records of a fused launch in self.traj)"""
+        if not self.R:
+            for i in range(first, first + K):
+                self(i)
+            return
+        import torch
+        if trajectory and (self.traj is None or self.traj[0].shape[0] < K):
+            e = self.env
+            self.traj = (torch.empty(K, e.E, e.C, dtype=torch.float32, device=e.device),
+                         torch.empty(K, e.E, e.C, dtype=torch.uint8, device=e.device),
+                         torch.empty(K, e.E, dtype=torch.uint8, device=e.device))
+        k = 0
+        while k < K:
+            n = min(self.R, K - k) if not trajectory else K
+            self.env.rollout(self.pol, n, seed=self.seed, step0=first + k, auto_reset=True, trajectory=trajectory,
+                             out=self.traj if trajectory else None)
+            k += n
+
 
 def settle(env, step, n, stagger, dev):
     """bring the envs to the steady state of the workload (not timed): n closed-loop steps, env e reset at
@@ -156,6 +179,18 @@ def settle(env, step, n, stagger, dev):
     at = stagger_schedule(env.E, n) if stagger else None
     at_dev = torch.from_numpy(at).to(dev) if stagger else None
     steps_with_reset = set(int(x) for x in at[at >= 0]) if stagger else set()
+    if step.R:   # fused path: launches of up to R steps, the staggered resets applied at launch boundaries
+        k = 0
+        while k < n:
+            m = min(step.R, n - k)
+            lo, hi = k, k + m
+            if stagger:
+                sel = (at_dev >= lo) & (at_dev < hi)
+                if bool(sel.any()):
+                    env.reset(sel.to(torch.uint8))
+            step.run(k, m)
+            k += m
+        return
     for k in range(n):
         if k in steps_with_reset:
             env.reset((at_dev == k).to(torch.uint8))
@@ -172,8 +207,7 @@ def timed(step, first, K, world):
     # K steps back to back (no per-step events: each event record costs ~5 us of device time between kernels
     # on this stack, which would be charged to the throughput)
     t0 = time.perf_counter()
-    for i in range(first, first + K):
-        step(i)
+    step.run(first, K)
     if step.gather is not None:
         step.gather.wait()
     torch.cuda.synchronize()
@@ -185,10 +219,25 @@ def timed(step, first, K, world):
 def stats_pass(env, step, first, KR):
     """after the timed region, KR further steps of the same workload: HIP events on the launch stream around
     each env step (model_kernel + logic_kernel + ray_sensor_kernel; the policy kernel is outside the
-    brackets) for the roofline, and device-side tallies of what happened in those car-steps."""
+    brackets) -- or around one fused KR-step rollout launch -- for the roofline, and device-side tallies of
+    what happened in those car-steps."""
     import torch
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(KR)]
     tally = torch.zeros(7, dtype=torch.float64, device=env.device)
+    if step.R:
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        step.run(first, KR, trajectory=True)         # allocates the trajectory buffers outside the bracket
+        e0.record()
+        step.run(first + KR, KR, trajectory=True)
+        e1.record()
+        rew, cf, ef = step.traj
+        cf, ef = cf[:KR], ef[:KR]
+        tally += torch.stack([((cf & 4) != 0).sum(), ((cf & 8) != 0).sum(), ((cf & 1) != 0).sum(),
+                              ((cf & 2) != 0).sum(), ((ef & 8) != 0).sum(), ((cf & 128) != 0).sum(),
+                              torch.zeros((), device=env.device)]).double()
+        tally[6] = env.obs[..., 4].double().sum() * KR    # speed sampled at the window's last step
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) / KR, tally.tolist()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(KR)]
     for i in range(KR):
         a = step.actions(first + i)
         ev[i][0].record()
@@ -220,6 +269,9 @@ def main():
     ap.add_argument("--no-stagger", action="store_true", help="all envs start together (no staggered resets)")
     ap.add_argument("--save-state", default=None, help="write the settled state (engine arena + obs) to this file")
     ap.add_argument("--load-state", default=None, help="start from a state written by --save-state (no settle)")
+    ap.add_argument("--rollout", type=int, default=50,
+                    help="steps per fused nascar_rollout launch for the device action sources (0: per-step path, "
+                         "nascar_policy_actions + nascar_step per step)")
     ap.add_argument("--mixed", action="store_true", help="env e on track e mod 8 of the sorted bundled tracks "
                     "(BASELINE cfg5: mixed batch, divergent geometry); --track is ignored")
     ap.add_argument("--gather", action="store_true", help="gather every step's obs/reward/flags of all ranks to "
@@ -270,7 +322,7 @@ def main():
         gen = torch.Generator(device=dev)
         gen.manual_seed(1234 + rank)
         acts = torch.rand((W + K, E, C, 2), generator=gen, device=dev) * 2 - 1     # resident before timing
-    step = Stepper(env, args.policy, rank, acts, None)
+    step = Stepper(env, args.policy, rank, acts, None, args.rollout)
     t_settle = time.perf_counter()
     if args.load_state:
         blob = torch.load(args.load_state, map_location=dev, weights_only=True)
@@ -285,8 +337,9 @@ def main():
     if args.save_state:
         torch.save({"state": env.get_state().cpu(), "obs": env.obs.cpu(), "step": base}, args.save_state)
     step.gather = gather
-    for i in range(base, base + W):
-        step(i)
+    if gather is not None:
+        step.R = 0
+    step.run(base, W)
     elapsed = timed(step, base + W, K, world)
     KR = min(K, 50)
     kern_ms, tally = stats_pass(env, step, base + W + K, KR)
@@ -326,11 +379,13 @@ def main():
         "config": {"workload": f"{track_name} {C}-car: {E} envs x {C} cars per GPU, {POLICY_TEXT[args.policy]}"
                                f"{settle_txt}, auto-reset",
                    "envs_per_gpu": E, "cars_per_env": C, "policy": args.policy,
+                   "launch": f"fused rollout, {step.R} steps per launch" if step.R else "per-step kernels",
                    "track": "mixed (env e: track e mod 8)" if args.mixed else os.path.basename(tpath),
                    "parallelism": f"dp{world} (env shards" + (", RCCL gather of obs/reward/flags to rank 0 per step)" if gather else ", no collective)")},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": tnote,
-                     "kernel": "model_kernel + logic_kernel + ray_sensor_kernel (one env step)", "kernel_ms": kern_ms,
+                     "kernel": (f"rollout_kernel ({step.R} fused env steps per launch; per-step time)" if step.R else
+                                "model_kernel + logic_kernel + ray_sensor_kernel (one env step)"), "kernel_ms": kern_ms,
                      "algo_bytes_per_car_step": ALGO_BYTES_PER_CAR_STEP},
         "workload_stats": wstats,
         "engine_errors": int(tally[5]),
@@ -345,8 +400,7 @@ def main():
         gen.manual_seed(1234 + rank)
         acts2 = torch.rand((W + K, E, C, 2), generator=gen, device=dev) * 2 - 1
         s2 = Stepper(env2, "uniform", rank, acts2, None)
-        for i in range(W):
-            s2(i)
+        s2.run(0, W)
         el2 = reduce_max([timed(s2, W, K, world)], dev)[0]
         out["uniform_from_reset"] = {"value": throughput(world, E, C, K, el2), "ms_per_step": el2 / K * 1e3,
                                      "note": "secondary: uniform actions from reset (cars stay on the start "

@@ -67,6 +67,19 @@ int nascar_reset(NascarHandle* h, const uint8_t* env_mask, float* obs, void* str
 int nascar_step(NascarHandle* h, const void* actions, int32_t discrete, float* obs, float* reward,
                 uint8_t* car_flags, uint8_t* env_flags, int32_t auto_reset, float* terminal_obs, void* stream);
 
+/* Fused multi-step rollout: `steps` x (device action source on the current obs + CarEnv.step), i.e. the loop
+ * of game/control drivers / learn/genetic_trainer.py:225-283 evaluation rollouts (actions from a policy on the
+ * previous observation, src/car_env.py:678-803 per step), in one launch.  Identical results to `steps` calls of
+ * nascar_policy_actions(policy, seed, step0 + k) + nascar_step(auto_reset).
+ *   policy:  0 uniform, 1 BaseController._fallback_control, 3 noisy rule driver (policy 1 with 15 % of the
+ *            car-steps uniform) -- see nascar_policy_actions
+ *   obs:     [E*C*38] float32, in: the current observation, out: the last step's
+ *   traj != 0: reward [steps][E*C], car_flags [steps][E*C], env_flags [steps][E] (per-step records);
+ *   traj == 0: reward [E*C], car_flags [E*C], env_flags [E] hold the last step's values.
+ * car_flags / env_flags may be NULL.  No terminal observations (auto-reset obs overwrite the final ones). */
+int nascar_rollout(NascarHandle* h, int32_t policy, uint64_t seed, int64_t step0, int32_t steps, float* obs,
+                   float* reward, uint8_t* car_flags, uint8_t* env_flags, int32_t auto_reset, int32_t traj, void* stream);
+
 /* Info builder (src/car_env.py:1160-1227, src/lap_timer.py:354-372): per-car float64 [E*C*N_INFO]
  * (field order: nascargymnasium_amd/_lib.py INFO_FIELDS) written to a device buffer. */
 int nascar_get_info(NascarHandle* h, double* info, void* stream);
@@ -80,7 +93,8 @@ int nascar_set_state(NascarHandle* h, const void* src_device, void* stream);
  *   policy 0: counter-based uniform U[-1,1]^2 (key = seed, car, step)
  *   policy 1: BaseController._fallback_control (game/control/base_controller.py:39-103) from obs
  *   policy 2: the SAC actor loaded with nascar_set_actor, deterministic (SACController.control,
- *             game/control/sac_control_class.py:80-115) from obs */
+ *             game/control/sac_control_class.py:80-115) from obs
+ *   policy 3: policy 1 with its action replaced by policy 0's draw on 15 % of the car-steps (counter hash) */
 int nascar_policy_actions(NascarHandle* h, int32_t policy, uint64_t seed, int64_t step, const float* obs,
                           float* actions, void* stream);
 

@@ -73,6 +73,8 @@ def lib():
     L.nascar_reset.restype = ctypes.c_int
     L.nascar_step.argtypes = [vp, vp, i32, vp, vp, vp, vp, i32, vp, vp]
     L.nascar_step.restype = ctypes.c_int
+    L.nascar_rollout.argtypes = [vp, i32, u64, i64, i32, vp, vp, vp, vp, i32, i32, vp]
+    L.nascar_rollout.restype = ctypes.c_int
     L.nascar_get_info.argtypes = [vp, vp, vp]
     L.nascar_get_info.restype = ctypes.c_int
     L.nascar_state_bytes.argtypes = [vp]
@@ -97,7 +99,7 @@ def lib():
 
 
 EXPORTED = ["nascar_create", "nascar_destroy", "nascar_last_error", "nascar_add_track", "nascar_set_env_tracks",
-            "nascar_reset", "nascar_step", "nascar_get_info", "nascar_state_bytes", "nascar_get_state",
+            "nascar_reset", "nascar_step", "nascar_rollout", "nascar_get_info", "nascar_state_bytes", "nascar_get_state",
             "nascar_set_state", "nascar_policy_actions", "nascar_set_actor", "nascar_actor_forward",
             "nascar_debug_sincosf", "nascar_debug_sensors"]
 

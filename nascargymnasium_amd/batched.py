@@ -123,6 +123,30 @@ class BatchedCarEnv:
                                           _ptr(self.car_flags), _ptr(self.env_flags), int(auto_reset),
                                           _ptr(self.terminal_obs) if terminal_obs else None, _stream()))
 
+    def rollout(self, policy: int, steps: int, seed: int = 0, step0: int = 0, auto_reset: bool = True,
+                trajectory: bool = False, out=None):
+        """`steps` env steps in one fused launch, actions from device action source `policy` (0 uniform, 1 rule
+        driver, 3 noisy rule driver) on the previous observation; equals `steps` x (policy_actions(policy, seed,
+        step0 + k) + step(..., auto_reset)).  Returns (obs, reward, car_flags, env_flags): the last step's, or with
+        trajectory=True the per-step records [steps, E, C] / [steps, E] (obs is always the last step's)."""
+        steps = int(steps)
+        if trajectory and out is not None:      # caller-owned per-step buffers (at least `steps` records)
+            rew, cf, ef = out
+            if rew.shape[0] < steps or cf.shape[0] < steps or ef.shape[0] < steps:
+                raise ValueError("trajectory buffers hold fewer than `steps` records")
+        elif trajectory:
+            rew = torch.empty(steps, self.E, self.C, dtype=torch.float32, device=self.device)
+            cf = torch.empty(steps, self.E, self.C, dtype=torch.uint8, device=self.device)
+            ef = torch.empty(steps, self.E, dtype=torch.uint8, device=self.device)
+        else:
+            rew, cf, ef = self.reward, self.car_flags, self.env_flags
+        with torch.cuda.device(self.device):
+            _lib.check(self.L.nascar_rollout(self.h, int(policy), int(seed), int(step0), steps, _ptr(self.obs), _ptr(rew),
+                                             _ptr(cf), _ptr(ef), int(auto_reset), int(trajectory), _stream()))
+        if trajectory and steps > 0:
+            self.reward.copy_(rew[steps - 1]); self.car_flags.copy_(cf[steps - 1]); self.env_flags.copy_(ef[steps - 1])
+        return self.obs, rew, cf, ef
+
     def info_tensor(self) -> torch.Tensor:
         """per-car info [E, C, N_INFO] float64 (fields: _lib.INFO_FIELDS)."""
         with torch.cuda.device(self.device):

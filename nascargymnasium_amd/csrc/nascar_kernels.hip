@@ -94,6 +94,7 @@ struct Params {
   float4* pose;        // [2][N] sensor hand-off: (x, y, angle, mode) -- see sensor_kernel
   double2* pose_cs;    // [2][N] cos, sin of (double)angle for the ray end points (computed once per car)
   const double2* ray_cs;   // [16] cos, sin of the ray offsets radians(22.5 i) (nascar_rays.h)
+  double* ctl;         // [N][4] rule-driver state of the device action sources (policy_car)
   // block map shortcuts (prepare()): map_identity = blk_env[s] is s (< E) or -1, one_track >= 0 = every
   // block's track; they spare each kernel's first dependent load
   int map_identity, one_track;
@@ -1216,33 +1217,19 @@ __device__ __forceinline__ void quad_transpose(const float v[4], float o[4], int
 #define RSENSOR_WPE 6   // 4 lanes per car at 6 waves/SIMD: 41.5 us (8 lanes 53.7, 2 lanes 44.3; 16 lanes 62.4)
 #endif
 #define RAY_LPC 4     // lanes per car; each lane walks the lists of rays r, r + 4, r + 8, r + 12
-__global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(RSENSOR_WPE)))
-ray_sensor_kernel(Params P, float* obs, float* terminal_obs, int passes) {
-  constexpr int CPW = BLOCK / RAY_LPC, RPL = 16 / RAY_LPC;
-  constexpr int SUB = (SBLOCK + CPW - 1) / CPW;   // sensor workgroups per step-kernel workgroup
-  const int b = blockIdx.x / SUB, sub = blockIdx.x - b * SUB;
-  const int t = threadIdx.x, lc = t / RAY_LPC, r = t - lc * RAY_LPC;
-  const int C = P.C;
-  const int slot = sub * CPW + lc;
-  const int el = slot / C, car = slot - el * C;
-  const int env = blk_env_of(P, el, b * P.epb + el);
-  const TrackDev& T = P.tracks[blk_track_of(P, b)];
-  {
-    float4* s_w = (float4*)smem;
-    const int nw2 = 2 * T.nwall;
-    for (int k = t; k < nw2; k += BLOCK) s_w[k] = T.swall[k];
-    __syncthreads();
-  }
-  if (env < 0) return;
+// The 4-lane work of car n, lane r (rays r, r + 4, r + 8, r + 12) in ray_sensor_kernel / rollout_kernel: both
+// passes, the beam-list walks against the wall image sw (LDS), the quad transpose and the obs stores.
+// All 4 lanes of a car are consecutive lanes of one quad and call this together.
+__device__ __forceinline__ void ray_lane(const Params& P, const TrackDev& T, const float4* __restrict__ sw, int n, int r,
+                                         float* obs, float* terminal_obs, int passes) {
+  constexpr int RPL = 16 / RAY_LPC;
   // pose loads after the staging barrier: issuing them (and pass A's cos/sin) before it, or the beam-cell
   // lookup too, measured 2.5 / 9 us slower (registers held across the staging)
-  const int n = env * C + car;
   int mode = 0;
   float4 pa = make_float4(0.f, 0.f, 0.f, 0.f), pb = pa;
   if (passes & 1) { pa = P.pose[n]; mode = __float_as_int(pa.w) & (PM_A_OBS | PM_A_TERM); }
   if (passes & 2) { pb = P.pose[P.N + n]; mode |= __float_as_int(pb.w) & PM_B_OBS; }
   const BeamGrid G = T.beam;
-  const float4* __restrict__ sw = (const float4*)smem;   // the track's wall image staged per workgroup
 #pragma unroll 1
   for (int pass = 0; pass < 2; ++pass) {
     const bool active = pass == 0 ? (mode & (PM_A_OBS | PM_A_TERM)) != 0 : (mode & PM_B_OBS) != 0;
@@ -1311,6 +1298,100 @@ ray_sensor_kernel(Params P, float* obs, float* terminal_obs, int passes) {
   }
 }
 
+__global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(RSENSOR_WPE)))
+ray_sensor_kernel(Params P, float* obs, float* terminal_obs, int passes) {
+  constexpr int CPW = BLOCK / RAY_LPC;
+  constexpr int SUB = (SBLOCK + CPW - 1) / CPW;   // sensor workgroups per step-kernel workgroup
+  const int b = blockIdx.x / SUB, sub = blockIdx.x - b * SUB;
+  const int t = threadIdx.x, lc = t / RAY_LPC, r = t - lc * RAY_LPC;
+  const int C = P.C;
+  const int slot = sub * CPW + lc;
+  const int el = slot / C, car = slot - el * C;
+  const int env = blk_env_of(P, el, b * P.epb + el);
+  const TrackDev& T = P.tracks[blk_track_of(P, b)];
+  {
+    float4* s_w = (float4*)smem;
+    const int nw2 = 2 * T.nwall;
+    for (int k = t; k < nw2; k += BLOCK) s_w[k] = T.swall[k];
+    __syncthreads();
+  }
+  if (env < 0) return;
+  ray_lane(P, T, (const float4*)smem, env * C + car, r, obs, terminal_obs, passes);
+}
+
+__device__ __forceinline__ uint32_t mix32(uint64_t x) {   // splitmix64 finaliser
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  x ^= x >> 31;
+  return (uint32_t)(x >> 32);
+}
+// Noisy rule driver (policy 3): with probability NOISE_P16 / 65536 per car-step the driver's action is
+// replaced by the uniform draw of policy 0 (the driver state still advances), as gen_golden.py's
+// "rule_noisy" mode does with a host RNG; cars of one env therefore leave the common start trajectory.
+#define NOISE_P16 9830u   // 0.15 * 65536
+// device action sources 0, 1, 3 for car n from its current observation row (policy 2, the SAC actor, is
+// actor_kernel): writes (throttle_brake, steering) to a0, a1
+__device__ __forceinline__ void policy_car(int policy, uint64_t seed, int64_t step, int n, const float* obs, double* ctl,
+                                           float& a0, float& a1) {
+  const uint64_t key = (seed * 0x100000001B3ull) ^ ((uint64_t)n << 24) ^ (uint64_t)step * 0x9E3779B1ull;
+  const float u0 = (float)(mix32(key) >> 8) * (2.0f / 16777216.0f) - 1.0f;
+  const float u1 = (float)(mix32(key ^ 0xABCDEF12345ull) >> 8) * (2.0f / 16777216.0f) - 1.0f;
+  if (policy == 0) { a0 = u0; a1 = u1; return; }
+  // BaseController._fallback_control (game/control/base_controller.py:39-103); state per car in ctl[4*n..]:
+  // throttle_brake is a Python float (float64 += 0.1, *= 0.5, clamps); steering, speed_limit and
+  // last_forward hold numpy float32 values (NEP 50: float32 op python scalar stays float32).
+  const float* o = obs + (size_t)n * 38;
+  double* s = ctl + 4 * (size_t)n;   // throttle_brake, steering, last_forward, speed_limit
+  const float fwd = o[22], spd = o[4];
+  float steer = (float)s[1], last = (float)s[2], lim = (float)s[3];
+  double tb = s[0];
+  if (last >= fwd) lim = fwd;
+  if (last < fwd) lim = 1.0f;
+  if (spd < lim * 0.95f) tb += 0.1;
+  if (spd > lim * 1.05f) tb -= 0.1;
+  const float r = o[22 + 15], l = o[22 + 1];
+  if (r > l) steer = 1.0f - (l / r);
+  else if (l > r) steer = (1.0f - (r / l)) * -1.0f;
+  else steer *= 0.9f;
+  if (fabsf(steer) > 0.25f) tb *= 0.5;
+  tb = tb > 1.0 ? 1.0 : tb;  tb = tb < -1.0 ? -1.0 : tb;            // max(min(tb, 1), -1)
+  steer = steer > 1.0f ? 1.0f : steer;  steer = steer < -1.0f ? -1.0f : steer;
+  s[0] = tb; s[1] = steer; s[2] = fwd; s[3] = lim;
+  if (policy == 3 && (mix32(key ^ 0x5DEECE66Dull) >> 16) < NOISE_P16) { a0 = u0; a1 = u1; }
+  else { a0 = (float)tb; a1 = steer; }
+}
+__global__ void policy_kernel(int N, int policy, uint64_t seed, int64_t step, const float* obs, float* act, double* ctl) {
+  const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= N) return;
+  float a0, a1;
+  policy_car(policy, seed, step, n, obs, ctl, a0, a1);
+  act[2 * n] = a0; act[2 * n + 1] = a1;
+}
+
+
+
+// CarEnv action -> CarPhysics.step for one car whose physics state is loaded in c (src/car_env.py:733-740,
+// src/car_physics.py:341-384): BaseEnv._convert_to_internal_action of (tb, st), Car.update_physics, the
+// Box2D step; writes the model / body state back and the sensor pass-A pose.
+__device__ __forceinline__ void model_car(const Params& P, Car& c, int n, const TrackDev& T, float tb, float st, int want_term) {
+  const WallSet S{T.walls, T.nwall, T.bp, T.sn};
+  float a0, a1, a2 = st;
+  if (tb >= 0) { a0 = tb; a1 = 0.0f; } else { a0 = 0.0f; a1 = -tb; }
+  if (c.disabled) { a0 = 0.0f; a1 = 0.0f; a2 = 0.0f; }
+  c.thr_in = pymax(0.0, pymin(1.0, (double)a0));
+  c.brk_in = pymax(0.0, pymin(1.0, (double)a1));
+  c.str_in = pymax(-1.0, pymin(1.0, (double)a2));
+  car_update_physics(P, c, n, T);
+  car_store_model(P, n, c);
+  asm volatile("" ::: "memory");   // keep the model write-back ahead of the Box2D step (register pressure)
+  PROF(3);
+  b2_step(c, S, P.dt_f, P.friction);
+  PROF(4);
+  car_store_body(P, n, c);
+  set_pose(P, n, c, PM_A_OBS | (want_term ? PM_A_TERM : 0));   // sensor pass A
+}
+
 // The env step as two launches: model_kernel (actions -> Car.update_physics -> Box2D step, one lane
 // per car; its TOI code holds it at one wave per SIMD) hands the body / listener state to logic_kernel
 // (banking, disable logic, lap timer, rewards, termination, obs, auto-reset) through the state arrays.
@@ -1348,72 +1429,60 @@ __global__ void __launch_bounds__(SBLOCK) __attribute__((amdgpu_waves_per_eu(MOD
   T.segs = s_segs;
   PROF(1);
   if (env < 0) return;
-  const WallSet S{T.walls, T.nwall, T.bp, T.sn};
   PROF(2);
-  float a0, a1, a2 = st;
-  if (tb >= 0) { a0 = tb; a1 = 0.0f; } else { a0 = 0.0f; a1 = -tb; }
-  if (c.disabled) { a0 = 0.0f; a1 = 0.0f; a2 = 0.0f; }
-  c.thr_in = pymax(0.0, pymin(1.0, (double)a0));
-  c.brk_in = pymax(0.0, pymin(1.0, (double)a1));
-  c.str_in = pymax(-1.0, pymin(1.0, (double)a2));
-  car_update_physics(P, c, n, T);
-  car_store_model(P, n, c);
-  asm volatile("" ::: "memory");   // keep the model write-back ahead of the Box2D step (register pressure)
-  PROF(3);
-  b2_step(c, S, P.dt_f, P.friction);
-  PROF(4);
-  car_store_body(P, n, c);
-  set_pose(P, n, c, PM_A_OBS | (want_term ? PM_A_TERM : 0));   // sensor pass A
+  model_car(P, c, n, T, tb, st, want_term);
   PROF(5);
   PROF_RT(15);
 }
 
-__global__ void __launch_bounds__(SBLOCK) logic_kernel(Params P, float* obs, float* reward, uint8_t* car_flags,
-                                                      uint8_t* env_flags, int auto_reset, float* terminal_obs) {
-  __shared__ int s_laps_old[SBLOCK], s_dis_old[SBLOCK], s_laps_new[SBLOCK], s_dis_new[SBLOCK], s_lapdone[SBLOCK];
-  __shared__ int s_dis_final[SBLOCK], s_below[SBLOCK];
-  __shared__ int s_envdone[SBLOCK];
-  const int tid = threadIdx.x, C = P.C;
-  const int el = tid / C, car = tid - el * C;
-  const int slot = blockIdx.x * P.epb + el;
-  const int env = blk_env_of(P, el, slot);
-  const int n = env >= 0 ? env * C + car : 0;
-  LPROF(0);
-  __shared__ DSeg s_segs[MAX_SEG];
-  __shared__ double s_prefix[MAX_SEG];
-  __shared__ float s_obs[SBLOCK * 22];
-  __shared__ int s_rowbase[SBLOCK];
-  __shared__ float4 s_sg[MAX_SEG];
-  __shared__ float s_rll[MAX_SEG];
-  Car c;
-  double sim = 0.0;
-  int pend_in = 0, reason_in = 0;   // env state read by the env passes (car 0's lane), fetched up front
-  if (env >= 0) {   // state loads issued before the segment staging barrier (independent round trips)
+// logic_kernel's shared memory: env reductions and the coalesced obs[:, 0:22] row store
+struct LogicLDS {
+  int laps_old[SBLOCK], dis_old[SBLOCK], laps_new[SBLOCK], dis_new[SBLOCK], lapdone[SBLOCK];
+  int dis_final[SBLOCK], below[SBLOCK], envdone[SBLOCK];
+  float obs[SBLOCK * 22];
+  int rowbase[SBLOCK];
+};
+// the block's track segments in LDS (f64 segments, chord prefix sums, f32 chord screens)
+struct TrackLDS { DSeg segs[MAX_SEG]; double prefix[MAX_SEG]; float4 sg[MAX_SEG]; float rll[MAX_SEG]; };
+__device__ __forceinline__ void stage_track_lds(const TrackDev& T, TrackLDS& TL, int tid) {
+  if (tid < T.nseg) {
+    const DSeg sg = T.segs[tid];
+    TL.segs[tid] = sg; TL.prefix[tid] = T.prefix[tid];
+    const double dx = sg.ex - sg.sx, dy = sg.ey - sg.sy, ll = dx * dx + dy * dy;
+    TL.sg[tid] = make_float4((float)sg.sx, (float)sg.sy, (float)dx, (float)dy);
+    TL.rll[tid] = ll < 1e-6 ? 0.0f : (float)(1.0 / ll);
+  }
+}
+// logic state of car n (body from model_kernel, lap timer / bookkeeping, tyres) and its env's time / pending /
+// reason words (read by car 0's lane in the env passes)
+__device__ __forceinline__ void logic_load(const Params& P, int env, int car, int n, Car& c, double& sim, int& pend_in,
+                                           int& reason_in) {
+  sim = 0.0; pend_in = 0; reason_in = 0;
+  if (env >= 0) {
     car_load_body(P, n, c);
     car_load_logic(P, n, c);
     car_reload_tyres(P, n, c);
     if (car == 0) { pend_in = P.env_i32[E_PENDING * P.E + env]; reason_in = P.env_i32[E_REASON * P.E + env]; }
     sim = P.env_time[env];
   }
-  TrackDev T = P.tracks[blk_track_of(P, blockIdx.x)];
-  if (tid < T.nseg) {
-    const DSeg sg = T.segs[tid];
-    s_segs[tid] = sg; s_prefix[tid] = T.prefix[tid];
-    const double dx = sg.ex - sg.sx, dy = sg.ey - sg.sy, ll = dx * dx + dy * dy;
-    s_sg[tid] = make_float4((float)sg.sx, (float)sg.sy, (float)dx, (float)dy);
-    s_rll[tid] = ll < 1e-6 ? 0.0f : (float)(1.0 / ll);
-  }
-  __syncthreads();
-  T.segs = s_segs; T.prefix = s_prefix;
-  const ChordScreen CS{s_sg, s_rll, T.nseg};
+}
+// the rest of the env step for one block (every thread calls it; it holds block barriers): banking, impulse /
+// stuck / backward disable, lap timer, env pass 1, obs[0:22], rewards, env pass 2 (termination), auto-reset
+// (sensor pass-B pose), state write-back, coalesced obs rows.  T.segs / T.prefix point at TL.
+__device__ __forceinline__ void logic_run(const Params& P, const TrackDev& T, const TrackLDS& TL, LogicLDS& L, int tid,
+                                          int el, int car, int env, int n, Car& c, double sim, int pend_in, int reason_in,
+                                          float* obs, float* reward, uint8_t* car_flags, uint8_t* env_flags, int auto_reset,
+                                          float* terminal_obs) {
+  const int C = P.C;
+  const ChordScreen CS{TL.sg, TL.rll, T.nseg};
   float cut = INFINITY;
   const int nw = T.nwall;
   const WallSet S{T.walls, nw, T.bp, T.sn};
   bool lapdone = false;
   if (env >= 0) {
-    s_dis_old[tid] = c.disabled;
+    L.dis_old[tid] = c.disabled;
     LPROF(1);
-    s_laps_old[tid] = c.lt_laps;   // the lap count does not change before lap_update
+    L.laps_old[tid] = c.lt_laps;   // the lap count does not change before lap_update
     cut = screen_cut(CS, c.xf.p.x, c.xf.p.y);   // the body position is final for this step
     c.bank = T.has_banking ? banking_at_screened(T, CS, cut, c.xf.p.x, c.xf.p.y) : 0.0;
     if (!c.disabled) {   // _run_single_physics_step (src/car_env.py:582-638)
@@ -1426,7 +1495,7 @@ __global__ void __launch_bounds__(SBLOCK) logic_kernel(Params P, float* obs, flo
       else { c.stuck_dur = 0.0; c.has_stuck_start = 0; }
     }
     lapdone = lap_update(T, CS, c, c.xf.p.x, c.xf.p.y, sim);
-    s_laps_new[tid] = c.lt_laps; s_dis_new[tid] = c.disabled; s_lapdone[tid] = lapdone;
+    L.laps_new[tid] = c.lt_laps; L.dis_new[tid] = c.disabled; L.lapdone[tid] = lapdone;
   }
   LPROF(2);
   __syncthreads();
@@ -1438,11 +1507,11 @@ __global__ void __launch_bounds__(SBLOCK) logic_kernel(Params P, float* obs, flo
     if (P.reset_on_lap) {
       const int b = tid;
       for (int i = 0; i < C; ++i) {
-        if (!s_lapdone[b + i]) continue;
+        if (!L.lapdone[b + i]) continue;
         bool any = false, all = true;
         for (int j = 0; j < C; ++j) {
-          int dis = j <= i ? s_dis_new[b + j] : s_dis_old[b + j];
-          int laps = j <= i ? s_laps_new[b + j] : s_laps_old[b + j];
+          int dis = j <= i ? L.dis_new[b + j] : L.dis_old[b + j];
+          int laps = j <= i ? L.laps_new[b + j] : L.laps_old[b + j];
           if (dis) continue;
           any = true;
           if (laps < 1) all = false;
@@ -1507,8 +1576,8 @@ __global__ void __launch_bounds__(SBLOCK) logic_kernel(Params P, float* obs, flo
       if (!c.disabled) c.prev_back = c.back;
       rew = (float)r;
     }
-    s_dis_final[tid] = c.disabled;
-    s_below[tid] = (!c.disabled && c.cum_reward < -250.0f) ? 1 : 0;
+    L.dis_final[tid] = c.disabled;
+    L.below[tid] = (!c.disabled && c.cum_reward < -250.0f) ? 1 : 0;
   }
   LPROF(5);
   __syncthreads();
@@ -1517,7 +1586,7 @@ __global__ void __launch_bounds__(SBLOCK) logic_kernel(Params P, float* obs, flo
     const double st = sim + P.dt_d;   // env_time is written only here
     P.env_time[env] = st;
     int ndis = 0, active = 0, below = 0, term = 0, trunc = 0, reason = reason_in;
-    for (int j = 0; j < C; ++j) { ndis += s_dis_final[tid + j]; if (!s_dis_final[tid + j]) { active++; below += s_below[tid + j]; } }
+    for (int j = 0; j < C; ++j) { ndis += L.dis_final[tid + j]; if (!L.dis_final[tid + j]) { active++; below += L.below[tid + j]; } }
     if (ndis >= C) { term = 1; reason = 1; }
     else if (active > 0 && below == active) { term = 1; reason = 2; }
     else if (P.reset_on_lap && st > 60.0) { term = 1; reason = 3; }
@@ -1527,7 +1596,7 @@ __global__ void __launch_bounds__(SBLOCK) logic_kernel(Params P, float* obs, flo
     P.env_i32[E_TERMINATED * P.E + env] = term;
     P.env_i32[E_TRUNCATED * P.E + env] = trunc;
     int done = term | trunc;
-    s_envdone[el] = done;
+    L.envdone[el] = done;
     if (env_flags) env_flags[env] = (uint8_t)((term ? EF_TERMINATED : 0) | (trunc ? EF_TRUNCATED : 0) |
                                               ((auto_reset && done) ? EF_RESET : 0) | ((reason & 7) << 4));
   }
@@ -1543,7 +1612,7 @@ __global__ void __launch_bounds__(SBLOCK) logic_kernel(Params P, float* obs, flo
     c.just_disabled = 0;
     reward[n] = rew;
     if (car_flags) car_flags[n] = flags;
-    const bool reset_now = auto_reset && s_envdone[el];
+    const bool reset_now = auto_reset && L.envdone[el];
     LPROF(6);
     if (terminal_obs) { float* t = terminal_obs + (size_t)n * 38; for (int i = 0; i < 22; ++i) t[i] = o[i]; }
     // sensor pass B: the reset pose of every auto-reset car (its pass-B values overwrite the pass-A
@@ -1555,7 +1624,7 @@ __global__ void __launch_bounds__(SBLOCK) logic_kernel(Params P, float* obs, flo
     } else {
       P.pose[P.N + n] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
-    for (int i = 0; i < 22; ++i) s_obs[tid * 22 + i] = o[i];
+    for (int i = 0; i < 22; ++i) L.obs[tid * 22 + i] = o[i];
     if (reset_now) car_store(P, n, c);    // car_reset rewrote every field
     else car_store_logic(P, n, c);
     LPROF(7);
@@ -1565,17 +1634,130 @@ __global__ void __launch_bounds__(SBLOCK) logic_kernel(Params P, float* obs, flo
       P.env_i32[E_TERMINATED * P.E + env] = 0; P.env_i32[E_TRUNCATED * P.E + env] = 0;
     }
   }
-  s_rowbase[tid] = env >= 0 ? n * 38 : -1;
+  L.rowbase[tid] = env >= 0 ? n * 38 : -1;
   __syncthreads();
   // obs[:, 0:22] rows of this workgroup, written 22 consecutive floats per row by consecutive lanes
 #pragma unroll
   for (int k = 0; k < 22; ++k) {   // unrolled: the 22 LDS reads are issued back to back
     const int i = tid + k * SBLOCK;
     const int row = i / 22, col = i - row * 22;
-    const int base = s_rowbase[row];
-    if (base >= 0) obs[(size_t)base + col] = s_obs[i];
+    const int base = L.rowbase[row];
+    if (base >= 0) obs[(size_t)base + col] = L.obs[i];
   }
-  LPROF(8);
+  LPROF(8);}
+
+__global__ void __launch_bounds__(SBLOCK) logic_kernel(Params P, float* obs, float* reward, uint8_t* car_flags,
+                                                      uint8_t* env_flags, int auto_reset, float* terminal_obs) {
+  __shared__ LogicLDS L;
+  __shared__ TrackLDS TL;
+  const int tid = threadIdx.x, C = P.C;
+  const int el = tid / C, car = tid - el * C;
+  const int slot = blockIdx.x * P.epb + el;
+  const int env = blk_env_of(P, el, slot);
+  const int n = env >= 0 ? env * C + car : 0;
+  LPROF(0);
+  Car c;
+  double sim;
+  int pend_in, reason_in;
+  logic_load(P, env, car, n, c, sim, pend_in, reason_in);   // state loads issued before the staging barrier
+  TrackDev T = P.tracks[blk_track_of(P, blockIdx.x)];
+  stage_track_lds(T, TL, tid);
+  __syncthreads();
+  T.segs = TL.segs; T.prefix = TL.prefix;
+  logic_run(P, T, TL, L, tid, el, car, env, n, c, sim, pend_in, reason_in, obs, reward, car_flags, env_flags, auto_reset,
+            terminal_obs);
+}
+
+// Fused multi-step rollout (nascar_rollout): K env steps of each block's envs in one launch, the actions
+// from a device action source (policy 0 / 1 / 3, policy_car) on the previous step's observation.  Per step
+// a block runs policy + model (one lane per car), logic (one lane per car, env passes in LDS) and the
+// sensors (4 lanes per car in RAY_LPC rounds of the block's threads), with block barriers between the
+// phases; the track's segments and sensor wall image are staged in LDS once per launch.  A car with a long
+// Box2D chain (TOI events, contact islands) delays only its own block, which the other blocks do not wait
+// for: in the per-step path every step waits for the slowest car of the whole batch.  Same device code as
+// model_kernel / logic_kernel / ray_sensor_kernel, so the results equal K x (nascar_policy_actions +
+// nascar_step with auto-reset) bit for bit (tests/test_gpu_rollout.py).
+// Each phase is an out-of-line function: inlined into one loop, the three phases' loop-invariant addresses
+// and live ranges spilled ~700 VGPRs; as calls each phase is allocated like its own kernel (the loop keeps
+// only a few values live across them).  Params are read through a constant-address-space pointer (scalar
+// loads) from the kernel argument.
+typedef const __attribute__((address_space(4))) Params* ParamsK;
+__shared__ TrackLDS g_ro_track;    // rollout_kernel: the block's track segments
+__shared__ LogicLDS g_ro_logic;    // rollout_kernel: logic_run's env reductions / obs rows
+
+struct RoSlot { int tid, el, car, env, n; };
+__device__ __forceinline__ RoSlot ro_slot(const Params& P) {
+  RoSlot r;
+  r.tid = threadIdx.x;
+  r.el = r.tid / P.C; r.car = r.tid - r.el * P.C;
+  r.env = blk_env_of(P, r.el, blockIdx.x * P.epb + r.el);
+  r.n = r.env >= 0 ? r.env * P.C + r.car : 0;
+  return r;
+}
+__device__ __forceinline__ TrackDev ro_track(const Params& P) {
+  TrackDev T = P.tracks[blk_track_of(P, blockIdx.x)];
+  T.segs = g_ro_track.segs; T.prefix = g_ro_track.prefix;
+  return T;
+}
+static __device__ __attribute__((noinline)) void ro_model_phase(ParamsK Pk, int policy, uint64_t seed, int64_t step,
+                                                                const float* obs) {
+  const Params& P = *(const Params*)Pk;
+  const RoSlot s = ro_slot(P);
+  if (s.env < 0) return;
+  const TrackDev T = ro_track(P);
+  Car c;
+  car_load_phys(P, s.n, c);
+  c.pid = s.n;
+  float tb, st;
+  policy_car(policy, seed, step, s.n, obs, P.ctl, tb, st);
+  model_car(P, c, s.n, T, tb, st, 0);
+}
+static __device__ __attribute__((noinline)) void ro_logic_phase(ParamsK Pk, float* obs, float* reward, uint8_t* car_flags,
+                                                                uint8_t* env_flags, int auto_reset) {
+  const Params& P = *(const Params*)Pk;
+  const RoSlot s = ro_slot(P);
+  const TrackDev T = ro_track(P);
+  Car c;
+  double sim;
+  int pend_in, reason_in;
+  logic_load(P, s.env, s.car, s.n, c, sim, pend_in, reason_in);
+  logic_run(P, T, g_ro_track, g_ro_logic, s.tid, s.el, s.car, s.env, s.n, c, sim, pend_in, reason_in, obs, reward,
+            car_flags, env_flags, auto_reset, nullptr);
+}
+static __device__ __attribute__((noinline)) void ro_sensor_phase(ParamsK Pk, float* obs, int passes) {
+  const Params& P = *(const Params*)Pk;
+  const TrackDev T = ro_track(P);
+  const int C = P.C;
+#pragma unroll 1
+  for (int q = 0; q < RAY_LPC; ++q) {   // SBLOCK car slots x RAY_LPC lanes: RAY_LPC rounds of the block
+    const int task = threadIdx.x + q * SBLOCK, lc = task / RAY_LPC, r = task - lc * RAY_LPC;
+    const int el = lc / C, car = lc - el * C;
+    const int env = blk_env_of(P, el, blockIdx.x * P.epb + el);
+    if (env >= 0) ray_lane(P, T, (const float4*)smem, env * C + car, r, obs, nullptr, passes);
+  }
+}
+__global__ void __launch_bounds__(SBLOCK) __attribute__((amdgpu_waves_per_eu(MODEL_WPE)))
+rollout_kernel(Params P, int K, int policy, uint64_t seed, int64_t step0, float* obs, float* reward, uint8_t* car_flags,
+               uint8_t* env_flags, int auto_reset, int traj) {
+  ParamsK Pk = (ParamsK)&P;
+  {
+    const TrackDev T = P.tracks[blk_track_of(P, blockIdx.x)];
+    stage_track_lds(T, g_ro_track, threadIdx.x);
+    float4* s_w = (float4*)smem;   // [2 * nwall] sensor wall image
+    for (int k = threadIdx.x; k < 2 * T.nwall; k += SBLOCK) s_w[k] = T.swall[k];
+  }
+  __syncthreads();
+#pragma unroll 1
+  for (int k = 0; k < K; ++k) {
+    const size_t ko = traj ? (size_t)k : 0;
+    ro_model_phase(Pk, policy, seed, step0 + k, obs);
+    __syncthreads();
+    ro_logic_phase(Pk, obs, reward + ko * P.N, car_flags ? car_flags + ko * P.N : nullptr,
+                   env_flags ? env_flags + ko * P.E : nullptr, auto_reset);
+    __syncthreads();
+    ro_sensor_phase(Pk, obs, auto_reset ? 3 : 1);
+    __syncthreads();
+  }
 }
 
 __global__ void __launch_bounds__(SBLOCK) reset_kernel(Params P, const uint8_t* mask, float* obs) {
@@ -1632,55 +1814,6 @@ __global__ void __launch_bounds__(SBLOCK) info_kernel(Params P, double* info) {
 }
 
 // ------------------------------------------------------------------ synthetic action sources (bench)
-__device__ __forceinline__ uint32_t mix32(uint64_t x) {   // splitmix64 finaliser
-  x += 0x9E3779B97F4A7C15ull;
-  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
-  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
-  x ^= x >> 31;
-  return (uint32_t)(x >> 32);
-}
-// Noisy rule driver (policy 3): with probability NOISE_P16 / 65536 per car-step the driver's action is
-// replaced by the uniform draw of policy 0 (the driver state still advances), as gen_golden.py's
-// "rule_noisy" mode does with a host RNG; cars of one env therefore leave the common start trajectory.
-#define NOISE_P16 9830u   // 0.15 * 65536
-__global__ void policy_kernel(int N, int policy, uint64_t seed, int64_t step, const float* obs, float* act, double* ctl) {
-  const int n = blockIdx.x * blockDim.x + threadIdx.x;
-  if (n >= N) return;
-  const uint64_t key = (seed * 0x100000001B3ull) ^ ((uint64_t)n << 24) ^ (uint64_t)step * 0x9E3779B1ull;
-  const float u0 = (float)(mix32(key) >> 8) * (2.0f / 16777216.0f) - 1.0f;
-  const float u1 = (float)(mix32(key ^ 0xABCDEF12345ull) >> 8) * (2.0f / 16777216.0f) - 1.0f;
-  if (policy == 0) {
-    act[2 * n] = u0;
-    act[2 * n + 1] = u1;
-    return;
-  }
-  // BaseController._fallback_control (game/control/base_controller.py:39-103); state per car in ctl[4*n..]:
-  // throttle_brake is a Python float (float64 += 0.1, *= 0.5, clamps); steering, speed_limit and
-  // last_forward hold numpy float32 values (NEP 50: float32 op python scalar stays float32).
-  const float* o = obs + (size_t)n * 38;
-  double* s = ctl + 4 * (size_t)n;   // throttle_brake, steering, last_forward, speed_limit
-  const float fwd = o[22], spd = o[4];
-  float steer = (float)s[1], last = (float)s[2], lim = (float)s[3];
-  double tb = s[0];
-  if (last >= fwd) lim = fwd;
-  if (last < fwd) lim = 1.0f;
-  if (spd < lim * 0.95f) tb += 0.1;
-  if (spd > lim * 1.05f) tb -= 0.1;
-  const float r = o[22 + 15], l = o[22 + 1];
-  if (r > l) steer = 1.0f - (l / r);
-  else if (l > r) steer = (1.0f - (r / l)) * -1.0f;
-  else steer *= 0.9f;
-  if (fabsf(steer) > 0.25f) tb *= 0.5;
-  tb = tb > 1.0 ? 1.0 : tb;  tb = tb < -1.0 ? -1.0 : tb;            // max(min(tb, 1), -1)
-  steer = steer > 1.0f ? 1.0f : steer;  steer = steer < -1.0f ? -1.0f : steer;
-  s[0] = tb; s[1] = steer; s[2] = fwd; s[3] = lim;
-  if (policy == 3 && (mix32(key ^ 0x5DEECE66Dull) >> 16) < NOISE_P16) {
-    act[2 * n] = u0; act[2 * n + 1] = u1;
-  } else {
-    act[2 * n] = (float)tb; act[2 * n + 1] = steer;
-  }
-}
-
 // =================================================================== host side / C ABI
 static thread_local std::string g_err;
 static int fail(const char* fmt, ...) {
@@ -2185,7 +2318,7 @@ static Params make_params(NascarHandle* h) {
   P.act_n = (float*)(a + h->off_n); P.env_time = (double*)(a + h->off_time); P.env_i32 = (int*)(a + h->off_ei32);
   P.blk_track = h->d_blk_track; P.blk_env = h->d_blk_env; P.tracks = h->d_tracks;
   P.map_identity = h->map_identity; P.one_track = h->one_track;
-  P.pose = h->d_pose; P.pose_cs = h->d_pose_cs; P.ray_cs = h->d_ray_cs;
+  P.pose = h->d_pose; P.pose_cs = h->d_pose_cs; P.ray_cs = h->d_ray_cs; P.ctl = h->d_ctl;
   return P;
 }
 
@@ -2242,6 +2375,22 @@ extern "C" int nascar_step(NascarHandle* h, const void* actions, int32_t discret
                      env_flags, auto_reset, terminal_obs);
   HIPCHK(hipGetLastError());
   launch_sensors(h, P, obs, terminal_obs, auto_reset ? 3 : 1, stream);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+extern "C" int nascar_rollout(NascarHandle* h, int32_t policy, uint64_t seed, int64_t step0, int32_t steps, float* obs,
+                              float* reward, uint8_t* car_flags, uint8_t* env_flags, int32_t auto_reset, int32_t traj,
+                              void* stream) {
+  if (!h || !obs || !reward) return fail("null argument");
+  if (policy != 0 && policy != 1 && policy != 3) return fail("rollout policy must be 0, 1 or 3 (got %d)", policy);
+  if (steps < 0) return fail("steps must be >= 0");
+  if (steps == 0) return 0;
+  if (prepare(h)) return -1;
+  Params P = make_params(h);
+  const size_t lds = h->max_sensor_lds;   // >= 2 float4 per wall of the largest track
+  hipLaunchKernelGGL(rollout_kernel, dim3(h->nblocks), dim3(SBLOCK), lds, (hipStream_t)stream, P, steps, policy, seed,
+                     step0, obs, reward, car_flags, env_flags, auto_reset, traj);
   HIPCHK(hipGetLastError());
   return 0;
 }
