@@ -62,10 +62,15 @@ __device__ unsigned long long* g_prof = nullptr;
 #define CPROF_BASE (LPROF_BASE + 65536 * 16)
 #define CCOUNT(c, slot, v) do { if (g_prof) g_prof[CPROF_BASE + (size_t)(c).pid * 16 + (slot)] += (unsigned long long)(v); } while (0)
 #define CTIME_BEGIN() const unsigned long long _ct0 = __builtin_amdgcn_s_memtime()
+// rollout_kernel per-wave phase cycles summed over its steps: region after the per-car counters (N <= 2^20)
+#define RPROF_BASE (CPROF_BASE + (size_t)(1 << 20) * 16)
+#define RPROF_ADD(slot, v) do { if (g_prof && (threadIdx.x & 63) == 0) \
+    g_prof[RPROF_BASE + ((size_t)blockIdx.x * (SBLOCK / 64) + threadIdx.x / 64) * 4 + (slot)] += (v); } while (0)
 #define CTIME_END(c, slot) CCOUNT(c, slot, __builtin_amdgcn_s_memtime() - _ct0)
 #else
 #define CCOUNT(c, slot, v) do { } while (0)
 #define CTIME_BEGIN() do { } while (0)
+#define RPROF_ADD(slot, v) do { } while (0)
 #define CTIME_END(c, slot) do { } while (0)
 #define PROF(ph) do { } while (0)
 #define PROFS(ph) do { } while (0)

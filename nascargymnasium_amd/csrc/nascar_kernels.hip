@@ -1679,8 +1679,9 @@ __global__ void __launch_bounds__(SBLOCK) logic_kernel(Params P, float* obs, flo
 // nascar_step with auto-reset) bit for bit (tests/test_gpu_rollout.py).
 // Each phase is an out-of-line function: inlined into one loop, the three phases' loop-invariant addresses
 // and live ranges spilled ~700 VGPRs; as calls each phase is allocated like its own kernel (the loop keeps
-// only a few values live across them).  Params are read through a constant-address-space pointer (scalar
-// loads) from the kernel argument.
+// only a few values live across them).  Params are read from a device copy (nascar_rollout uploads it)
+// through a constant-address-space pointer, so the phases use scalar loads.  (The address of a by-value
+// kernel argument must not be used for that: clang copies an address-taken argument to private memory.)
 typedef const __attribute__((address_space(4))) Params* ParamsK;
 __shared__ TrackLDS g_ro_track;    // rollout_kernel: the block's track segments
 __shared__ LogicLDS g_ro_logic;    // rollout_kernel: logic_run's env reductions / obs rows
@@ -1737,9 +1738,10 @@ static __device__ __attribute__((noinline)) void ro_sensor_phase(ParamsK Pk, flo
   }
 }
 __global__ void __launch_bounds__(SBLOCK) __attribute__((amdgpu_waves_per_eu(MODEL_WPE)))
-rollout_kernel(Params P, int K, int policy, uint64_t seed, int64_t step0, float* obs, float* reward, uint8_t* car_flags,
-               uint8_t* env_flags, int auto_reset, int traj) {
-  ParamsK Pk = (ParamsK)&P;
+rollout_kernel(const Params* __restrict__ Pg, int K, int policy, uint64_t seed, int64_t step0, float* obs, float* reward,
+               uint8_t* car_flags, uint8_t* env_flags, int auto_reset, int traj) {
+  ParamsK Pk = (ParamsK)Pg;   // global -> constant address space (same addresses)
+  const Params& P = *Pg;
   {
     const TrackDev T = P.tracks[blk_track_of(P, blockIdx.x)];
     stage_track_lds(T, g_ro_track, threadIdx.x);
@@ -1750,13 +1752,26 @@ rollout_kernel(Params P, int K, int policy, uint64_t seed, int64_t step0, float*
 #pragma unroll 1
   for (int k = 0; k < K; ++k) {
     const size_t ko = traj ? (size_t)k : 0;
+#ifdef NASCAR_PROFILE
+    const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+#endif
     ro_model_phase(Pk, policy, seed, step0 + k, obs);
     __syncthreads();
+#ifdef NASCAR_PROFILE
+    const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+#endif
     ro_logic_phase(Pk, obs, reward + ko * P.N, car_flags ? car_flags + ko * P.N : nullptr,
                    env_flags ? env_flags + ko * P.E : nullptr, auto_reset);
     __syncthreads();
+#ifdef NASCAR_PROFILE
+    const unsigned long long t2 = __builtin_amdgcn_s_memtime();
+#endif
     ro_sensor_phase(Pk, obs, auto_reset ? 3 : 1);
     __syncthreads();
+#ifdef NASCAR_PROFILE
+    const unsigned long long t3 = __builtin_amdgcn_s_memtime();
+    RPROF_ADD(0, t1 - t0); RPROF_ADD(1, t2 - t1); RPROF_ADD(2, t3 - t2); RPROF_ADD(3, 1);
+#endif
   }
 }
 
@@ -2099,6 +2114,8 @@ struct NascarHandle {
   double2* d_pose_cs = nullptr;
   double2* d_ray_cs = nullptr;
   void* d_actor = nullptr;   // SAC actor weights (nascar_set_actor), one allocation
+  void* d_params = nullptr;  // device copy of the launch Params (rollout_kernel) and the host image last uploaded
+  Params params_up; bool params_valid = false;
   ActorDev actor{};
   size_t max_lds = 0, max_sensor_lds = 0, max_sensor_groups_lds = 0;
   bool dirty_tracks = true;
@@ -2147,7 +2164,7 @@ extern "C" int nascar_create(const NascarConfig* cfg, NascarHandle** out) {
 
 extern "C" void nascar_destroy(NascarHandle* h) {
   if (!h) return;
-  hipFree(h->arena); hipFree(h->d_pose); hipFree(h->d_pose_cs); hipFree(h->d_ray_cs); hipFree(h->d_actor);
+  hipFree(h->arena); hipFree(h->d_pose); hipFree(h->d_pose_cs); hipFree(h->d_ray_cs); hipFree(h->d_actor); hipFree(h->d_params);
   for (auto& t : h->tracks) {
     hipFree(t.d_walls); hipFree(t.d_segs); hipFree(t.d_prefix);
     hipFree(t.bp.d_start); hipFree(t.bp.d_idx); hipFree(t.bp.d_box); hipFree(t.sn.d_start); hipFree(t.sn.d_idx); hipFree(t.d_groups); hipFree(t.d_swall);
@@ -2388,9 +2405,17 @@ extern "C" int nascar_rollout(NascarHandle* h, int32_t policy, uint64_t seed, in
   if (steps == 0) return 0;
   if (prepare(h)) return -1;
   Params P = make_params(h);
+  if (!h->d_params) {
+    HIPCHK(hipMalloc(&h->d_params, sizeof(Params)));
+    memset(&h->params_up, 0, sizeof(Params));
+  }
+  if (!h->params_valid || memcmp(&h->params_up, &P, sizeof(Params)) != 0) {   // stream-ordered upload when changed
+    h->params_up = P; h->params_valid = true;
+    HIPCHK(hipMemcpyAsync(h->d_params, &h->params_up, sizeof(Params), hipMemcpyHostToDevice, (hipStream_t)stream));
+  }
   const size_t lds = h->max_sensor_lds;   // >= 2 float4 per wall of the largest track
-  hipLaunchKernelGGL(rollout_kernel, dim3(h->nblocks), dim3(SBLOCK), lds, (hipStream_t)stream, P, steps, policy, seed,
-                     step0, obs, reward, car_flags, env_flags, auto_reset, traj);
+  hipLaunchKernelGGL(rollout_kernel, dim3(h->nblocks), dim3(SBLOCK), lds, (hipStream_t)stream, (const Params*)h->d_params,
+                     steps, policy, seed, step0, obs, reward, car_flags, env_flags, auto_reset, traj);
   HIPCHK(hipGetLastError());
   return 0;
 }

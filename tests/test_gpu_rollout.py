@@ -12,10 +12,10 @@ pytestmark = pytest.mark.gpu
 torch = pytest.importorskip("torch")
 
 
-def _engine(tracks, E, C):
+def _engine(tracks, E, C, reset_on_lap=False):
     from nascargymnasium_amd.batched import BatchedCarEnv
     files = [os.path.join(TRACKS, tracks[e % len(tracks)]) for e in range(E)]
-    return BatchedCarEnv(E, C, files, device="cuda:0")
+    return BatchedCarEnv(E, C, files, reset_on_lap=reset_on_lap, device="cuda:0")
 
 
 def _per_step(env, policy, seed, step0, K):
@@ -28,15 +28,17 @@ def _per_step(env, policy, seed, step0, K):
 
 
 @pytest.mark.parametrize("tracks,E,C,policy,warm,K", [
-    (["daytona.track"], 48, 10, 3, 600, 900),          # the bench workload: noisy driver, contacts, laps
-    (["martinsville.track"], 32, 4, 0, 0, 800),        # uniform: crashes, stuck cars, all-disabled resets
-    (["talladega.track", "michigan.track", "nascar2.track", "trioval.track"], 40, 3, 1, 200, 700),   # mixed tracks
+    (["daytona.track"], 48, 10, 3, 600, 900),          # the bench workload: noisy driver, contacts
+    (["daytona.track"], 16, 2, 1, 0, 400),             # rule driver from reset
+    (["martinsville.track"], 32, 4, 0, 3500, 300),     # uniform, reset_on_lap: the t > 60 s termination + auto-reset
+    (["talladega.track", "michigan.track", "nascar2.track", "trioval.track"], 40, 3, 3, 900, 600),   # mixed tracks
 ])
 def test_rollout_equals_per_step(tracks, E, C, policy, warm, K):
-    a, b = _engine(tracks, E, C), _engine(tracks, E, C)
+    rol = policy == 0
+    a, b = _engine(tracks, E, C, rol), _engine(tracks, E, C, rol)
     a.reset()
-    for k in range(warm):                       # leave the reset state first (cars spread, contacts active)
-        a.launch_step(a.policy_actions(policy, seed=5, step=k), auto_reset=True)
+    if warm:                                    # leave the reset state first (cars spread, contacts active)
+        a.rollout(policy, warm, seed=5, step0=0, auto_reset=True)
     b.set_state(a.get_state())
     b.obs.copy_(a.obs)
     R, CF, EF = _per_step(a, policy, 5, warm, K)
@@ -50,9 +52,10 @@ def test_rollout_equals_per_step(tracks, E, C, policy, warm, K):
     assert torch.equal(a.get_state(), b.get_state())
     n_contact = int(((CF & 4) != 0).sum())
     n_reset = int(((EF & 8) != 0).sum())
-    assert n_contact > 0
     if policy == 0:
-        assert n_reset > 0
+        assert n_reset > 0          # reset_on_lap: envs terminate once t > 60 s (step 3601) and auto-reset
+    if policy == 3:
+        assert n_contact > 0
     a.close(); b.close()
 
 

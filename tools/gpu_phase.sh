@@ -8,7 +8,7 @@ timeout -k 10 300 python bench.py --save-state /tmp/nascar_ss.pt --no-cpu-baseli
     > "$OUT/phase_bench.log" 2>&1; stop $? bench
 for L in ${LIBS:-libnascar_prof.so}; do
   C=""; case "$L" in *cnt*) C="--count";; esac
-  timeout -k 10 200 python tools/phase_profile.py --no-build --lib "$L" $C --load-state /tmp/nascar_ss.pt --warmup 20 --steps 2 \
+  timeout -k 10 200 python tools/phase_profile.py --no-build --lib "$L" $C --load-state /tmp/nascar_ss.pt --warmup 20 --steps 2 $PHASE_ARGS \
       > "$OUT/phase_${L%.so}.log" 2>&1; stop $? "phase $L"
 done
 if [ -n "$TESTS" ]; then

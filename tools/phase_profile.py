@@ -57,6 +57,8 @@ def main():
     ap.add_argument("--load-state", default=None, help="start from a bench.py --save-state file (steady state); "
                     "actions then come from the device noisy rule driver (policy 3) instead of uniform draws")
     ap.add_argument("--define", action="append", default=[], help="extra -D for the profile build")
+    ap.add_argument("--rollout", type=int, default=0, help="also profile one fused rollout launch of this many steps "
+                    "(per-wave phase cycles per step: model, logic, sensors, each up to its block barrier)")
     ap.add_argument("--count", action="store_true", help="library built with -DNASCAR_PROFILE_COUNT (sensor event "
                     "counters; the atomics distort that build's sensor timings)")
     a = ap.parse_args()
@@ -90,7 +92,8 @@ def main():
         env.step(actions(k0 + k), auto_reset=True)
     CPROF_BASE = LPROF_BASE + NW * 16
     N = a.envs * a.cars
-    buf = torch.zeros(CPROF_BASE + N * 16, dtype=torch.int64, device="cuda:0")
+    RPROF_BASE = CPROF_BASE + (1 << 20) * 16
+    buf = torch.zeros(RPROF_BASE + 65536 * 4, dtype=torch.int64, device="cuda:0")
     L.nascar_debug_profile(ctypes.c_void_p(buf.data_ptr()))
     for s in range(a.steps):
         acts = actions(k0 + a.warmup + s)
@@ -171,6 +174,23 @@ def main():
         if cb[0]:
             print(f"ray_sensor_kernel: rays {cb[0]}, fallback rays {cb[1]} ({100 * cb[1] / cb[0]:.2f}%), "
                   f"list entries per ray {cb[3] / max(1, cb[0] - cb[1]):.2f}, walked {cb[2] / max(1, cb[0] - cb[1]):.2f}")
+    if a.rollout:
+        import time
+        buf.zero_()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        env.rollout(3 if a.load_state else 0, a.rollout, seed=0, step0=k0 + a.warmup + a.steps)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        r = buf[RPROF_BASE:RPROF_BASE + 65536 * 4].cpu().numpy().reshape(-1, 4)
+        r = r[r[:, 3] > 0].astype(np.float64)
+        per = r[:, :3] / r[:, 3:4]
+        tot = per.sum(1)
+        print(f"rollout_kernel: {a.rollout} steps in {dt * 1e3:.1f} ms ({dt / a.rollout * 1e6:.1f} us/step incl. launch), "
+              f"waves {len(r)}; cycles per step per wave: total mean {tot.mean():.0f} (max wave {tot.max():.0f})")
+        for k, name in enumerate(["policy + model (+ barrier)", "logic (+ barrier)", "sensors (+ barrier)"]):
+            print(f"  {name:28s} mean {per[:, k].mean():9.0f}  p90 {np.percentile(per[:, k], 90):9.0f}  "
+                  f"max {per[:, k].max():9.0f}")
     L.nascar_debug_profile(ctypes.c_void_p(0))
     env.close()
 
