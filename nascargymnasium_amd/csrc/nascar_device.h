@@ -364,7 +364,6 @@ __device__ inline void find_new_contacts(Car& c, const WallSet& S) {
     const float cx = 0.5f * (c.fat.hi.x + c.fat.lo.x), cy = 0.5f * (c.fat.hi.y + c.fat.lo.y);
     if (hx <= S.bp.reach - 0.05f && hy <= S.bp.reach - 0.05f && grid_list(S.bp, cx, cy, beg, end)) list = S.bp.idx;
     else { beg = 0; end = S.nw; CCOUNT(c, 8, 1); }
-    CCOUNT(c, 9, end - beg);
   }
 #if BP_BATCH > 0
   if (list && S.bp.box) {
@@ -591,8 +590,10 @@ struct VC {
 };
 struct BodyState { V2 c; float a; V2 v; float w; };
 
-__device__ inline void cs_init(VC* vc, int n, const Car& c, const int* cidx, const LWall* W, bool warm, float dtRatio) {
-  for (int i = 0; i < n; ++i) {
+template <int NMAX> __device__ __forceinline__ void cs_init(VC* vc, int n, const Car& c, const int* cidx, const LWall* W, bool warm, float dtRatio) {
+#pragma unroll (NMAX <= 2 ? NMAX : 1)   // registers for small islands; the general bound stays a loop
+  for (int i = 0; i < NMAX; ++i) {
+    if (i >= n) break;
     const DContact& ct = c.ct[cidx[i]];
     VC& v = vc[i];
     v.ci = cidx[i];
@@ -606,17 +607,20 @@ __device__ inline void cs_init(VC* vc, int n, const Car& c, const int* cidx, con
       v.p[j].rA = v.p[j].rB = zero2(); v.p[j].nm = v.p[j].tm = v.p[j].vb = 0.0f;
       v.lps[j] = zero2();
     }
-    for (int j = 0; j < ct.pointCount; ++j) {
+    for (int j = 0; j < 2; ++j) {
+      if (j >= ct.pointCount) break;
       if (warm) { v.p[j].ni = dtRatio * ct.pt[j].ni; v.p[j].ti = dtRatio * ct.pt[j].ti; }
       v.lps[j] = V(ct.pt[j].lx, ct.pt[j].ly);
     }
   }
 }
 
-__device__ inline void cs_init_velocity(VC* vc, int n, const Car& c, const BodyState& A) {
+template <int NMAX> __device__ __forceinline__ void cs_init_velocity(VC* vc, int n, const Car& c, const BodyState& A) {
   const float mA = CAR_INV_MASS, iA = CAR_INV_I, mB = 0.0f, iB = 0.0f;
   const float friction_unused = 0.0f; (void)friction_unused;
-  for (int i = 0; i < n; ++i) {
+#pragma unroll (NMAX <= 2 ? NMAX : 1)   // registers for small islands; the general bound stays a loop
+  for (int i = 0; i < NMAX; ++i) {
+    if (i >= n) break;
     VC& v = vc[i];
     const DContact& m = c.ct[v.ci];
     V2 cA = A.c; float aA = A.a; V2 vA = A.v; float wA = A.w;
@@ -628,7 +632,8 @@ __device__ inline void cs_init_velocity(VC* vc, int n, const Car& c, const BodyS
     V2 normal = zero2(), pts[2];
     world_manifold(m, xfA, xfB, &normal, pts);
     v.normal = normal;
-    for (int j = 0; j < v.pointCount; ++j) {
+    for (int j = 0; j < 2; ++j) {
+      if (j >= v.pointCount) break;
       VCP& p = v.p[j];
       p.rA = vsub(pts[j], cA); p.rB = vsub(pts[j], cB);
       float rnA = vcross(p.rA, v.normal), rnB = vcross(p.rB, v.normal);
@@ -662,13 +667,16 @@ __device__ inline void cs_init_velocity(VC* vc, int n, const Car& c, const BodyS
   }
 }
 
-__device__ inline void cs_warm_start(VC* vc, int n, BodyState& A) {
+template <int NMAX> __device__ __forceinline__ void cs_warm_start(VC* vc, int n, BodyState& A) {
   const float mA = CAR_INV_MASS, iA = CAR_INV_I, mB = 0.0f, iB = 0.0f;
-  for (int i = 0; i < n; ++i) {
+#pragma unroll (NMAX <= 2 ? NMAX : 1)   // registers for small islands; the general bound stays a loop
+  for (int i = 0; i < NMAX; ++i) {
+    if (i >= n) break;
     VC& v = vc[i];
     V2 vA = A.v; float wA = A.w; V2 vB = v.vB; float wB = v.wB;
     V2 normal = v.normal, tangent = vcross_vs(normal, 1.0f);
-    for (int j = 0; j < v.pointCount; ++j) {
+    for (int j = 0; j < 2; ++j) {
+      if (j >= v.pointCount) break;
       VCP& p = v.p[j];
       V2 P = vadd(vmul(p.ni, normal), vmul(p.ti, tangent));
       wA -= iA * vcross(p.rA, P);
@@ -684,13 +692,16 @@ __device__ __forceinline__ V2 rel_vel(V2 vA, float wA, V2 vB, float wB, const VC
   return vsub(vsub(vadd(vB, vcross_sv(wB, p.rB)), vA), vcross_sv(wA, p.rA));
 }
 
-__device__ inline void cs_solve_velocity(VC* vc, int n, BodyState& A, float friction) {
+template <int NMAX> __device__ __forceinline__ void cs_solve_velocity(VC* vc, int n, BodyState& A, float friction) {
   const float mA = CAR_INV_MASS, iA = CAR_INV_I, mB = 0.0f, iB = 0.0f;
-  for (int i = 0; i < n; ++i) {
+#pragma unroll (NMAX <= 2 ? NMAX : 1)   // registers for small islands; the general bound stays a loop
+  for (int i = 0; i < NMAX; ++i) {
+    if (i >= n) break;
     VC& v = vc[i];
     V2 vA = A.v; float wA = A.w; V2 vB = v.vB; float wB = v.wB;
     V2 normal = v.normal, tangent = vcross_vs(normal, 1.0f);
-    for (int j = 0; j < v.pointCount; ++j) {
+    for (int j = 0; j < 2; ++j) {
+      if (j >= v.pointCount) break;
       VCP& p = v.p[j];
       V2 dv = rel_vel(vA, wA, vB, wB, p);
       float vt = vdot(dv, tangent) - 0.0f;
@@ -754,20 +765,26 @@ __device__ inline void cs_solve_velocity(VC* vc, int n, BodyState& A, float fric
   }
 }
 
-__device__ inline void cs_store(const VC* vc, int n, Car& c) {
-  for (int i = 0; i < n; ++i) {
+template <int NMAX> __device__ __forceinline__ void cs_store(const VC* vc, int n, Car& c) {
+#pragma unroll (NMAX <= 2 ? NMAX : 1)   // registers for small islands; the general bound stays a loop
+  for (int i = 0; i < NMAX; ++i) {
+    if (i >= n) break;
     DContact& m = c.ct[vc[i].ci];
-    for (int j = 0; j < vc[i].pointCount; ++j) { m.pt[j].ni = vc[i].p[j].ni; m.pt[j].ti = vc[i].p[j].ti; }
+    for (int j = 0; j < 2; ++j) {
+      if (j >= vc[i].pointCount) break; m.pt[j].ni = vc[i].p[j].ni; m.pt[j].ti = vc[i].p[j].ti; }
   }
 }
 
-__device__ inline int cs_solve_position(VC* vc, int n, BodyState& A, int toi) {
+template <int NMAX> __device__ __forceinline__ int cs_solve_position(VC* vc, int n, BodyState& A, int toi) {
   float minSep = 0.0f;
   const float mA = CAR_INV_MASS, iA = CAR_INV_I, mB = 0.0f, iB = 0.0f;
-  for (int i = 0; i < n; ++i) {
+#pragma unroll (NMAX <= 2 ? NMAX : 1)   // registers for small islands; the general bound stays a loop
+  for (int i = 0; i < NMAX; ++i) {
+    if (i >= n) break;
     VC& v = vc[i];
     V2 cA = A.c; float aA = A.a; V2 cB = v.cB; float aB = v.aB;
-    for (int j = 0; j < v.pcount; ++j) {
+    for (int j = 0; j < 2; ++j) {
+      if (j >= v.pcount) break;
       Xf xfA, xfB;
       xfA.q = rot_set(aA); xfB.q = rot_set(aB);
       xfA.p = vsub(cA, rmul(xfA.q, zero2()));
@@ -797,8 +814,12 @@ __device__ inline int cs_solve_position(VC* vc, int n, BodyState& A, int toi) {
   return toi ? (minSep >= -1.5f * LINEAR_SLOP) : (minSep >= -3.0f * LINEAR_SLOP);
 }
 
-__device__ inline void report(Car& c, const VC* vc, int n) {
-  for (int i = 0; i < n; ++i) lis_post(c, vc[i].pointCount, vc[i].p[0].ni, vc[i].p[1].ni);
+template <int NMAX> __device__ __forceinline__ void report(Car& c, const VC* vc, int n) {
+#pragma unroll (NMAX <= 2 ? NMAX : 1)   // registers for small islands; the general bound stays a loop
+  for (int i = 0; i < NMAX; ++i) {
+    if (i >= n) break;
+    lis_post(c, vc[i].pointCount, vc[i].p[0].ni, vc[i].p[1].ni);
+  }
 }
 
 __device__ inline void integrate_positions(BodyState& A, float h) {
@@ -818,17 +839,17 @@ __device__ inline void integrate_positions(BodyState& A, float h) {
   A.c = cc; A.a = a; A.v = v; A.w = w;
 }
 
-// b2World::Solve (single dynamic body island)
-__device__ inline void solve(Car& c, const WallSet& S, float dt, float dtRatio, float friction) {
-  const LWall* W = S.W;
-  if (!c.awake) return;
-  int cidx[MAX_ISLAND]; int n = 0;
-  for (int i = 0; i < c.nct; ++i) {
-    int fl = c.ct[i].flags;
-    if (!(fl & CT_ENABLED) || !(fl & CT_TOUCH)) continue;
-    if (n == MAX_ISLAND) { c.overflow = 2; break; }
-    cidx[n++] = i;
-  }
+// island contact list: cidx[n] = i without a dynamically indexed store (selects keep cidx in registers)
+__device__ __forceinline__ void island_push(int cidx[MAX_ISLAND], int& n, int i) {
+#pragma unroll
+  for (int j = 0; j < MAX_ISLAND; ++j) cidx[j] = j == n ? i : cidx[j];
+  ++n;
+}
+// the island solve of b2World::Solve for n touching contacts; NMAX >= n contact constraints in registers (the
+// common islands of 1-2 contacts; a larger bound would sit in scratch memory)
+template <int NMAX>
+__device__ __forceinline__ int solve_island(Car& c, const LWall* W, const int* cidx, int n, float dt, float dtRatio,
+                                            float friction) {
   float h = dt;
   BodyState A;
   c.c0 = c.c; c.a0 = c.a;
@@ -839,18 +860,35 @@ __device__ inline void solve(Car& c, const WallSet& S, float dt, float dtRatio, 
     wv += h * CAR_INV_I * c.torque;
     A.c = c.c; A.a = c.a; A.v = v; A.w = wv;
   }
-  VC vc[MAX_ISLAND];
-  cs_init(vc, n, c, cidx, W, true, dtRatio);
-  cs_init_velocity(vc, n, c, A);
-  cs_warm_start(vc, n, A);
-  for (int it = 0; it < 6; ++it) cs_solve_velocity(vc, n, A, friction);
-  cs_store(vc, n, c);
+  VC vc[NMAX];
+  cs_init<NMAX>(vc, n, c, cidx, W, true, dtRatio);
+  cs_init_velocity<NMAX>(vc, n, c, A);
+  cs_warm_start<NMAX>(vc, n, A);
+  for (int it = 0; it < 6; ++it) cs_solve_velocity<NMAX>(vc, n, A, friction);
+  cs_store<NMAX>(vc, n, c);
   integrate_positions(A, h);
   int positionSolved = 0;
-  for (int it = 0; it < 4; ++it) { if (cs_solve_position(vc, n, A, 0)) { positionSolved = 1; break; } }
+  for (int it = 0; it < 4; ++it) { if (cs_solve_position<NMAX>(vc, n, A, 0)) { positionSolved = 1; break; } }
   c.c = A.c; c.a = A.a; c.v = A.v; c.w = A.w;
   sync_transform(c);
-  report(c, vc, n);
+  report<NMAX>(c, vc, n);
+  return positionSolved;
+}
+
+// b2World::Solve (single dynamic body island)
+__device__ inline void solve(Car& c, const WallSet& S, float dt, float dtRatio, float friction) {
+  const LWall* W = S.W;
+  if (!c.awake) return;
+  int cidx[MAX_ISLAND] = {0, 0, 0, 0, 0, 0, 0, 0}; int n = 0;
+  for (int i = 0; i < c.nct; ++i) {
+    int fl = c.ct[i].flags;
+    if (!(fl & CT_ENABLED) || !(fl & CT_TOUCH)) continue;
+    if (n == MAX_ISLAND) { c.overflow = 2; break; }
+    island_push(cidx, n, i);
+  }
+  const float h = dt;
+  const int positionSolved = n <= 2 ? solve_island<2>(c, W, cidx, n, dt, dtRatio, friction)
+                                    : solve_island<MAX_ISLAND>(c, W, cidx, n, dt, dtRatio, friction);
   {
     float minSleepTime = FLT_BIG;
     const float linTolSqr = LINEAR_SLEEP_TOL * LINEAR_SLEEP_TOL;
@@ -1077,7 +1115,7 @@ __device__ inline float sep_eval(const SepFn& f, const Poly* pA, const Poly* pB,
 }
 enum { TOI_UNKNOWN, TOI_FAILED, TOI_OVERLAPPED, TOI_TOUCHING, TOI_SEPARATED };
 __device__ inline float time_of_impact(int* state, const Poly* pA, const Sweep& sweepA, const Poly* pB, const Sweep& sweepB, float tMax,
-                                      int* prof_iters = nullptr) {
+                                      int* prof_iters = nullptr, unsigned long long* prof_cyc = nullptr) {
   *state = TOI_UNKNOWN;
   float out_t = tMax;
   Sweep sA = sweepA, sB = sweepB;
@@ -1091,8 +1129,15 @@ __device__ inline float time_of_impact(int* state, const Poly* pA, const Sweep& 
   SCache cache; cache.count = 0; cache.metric = 0.0f;
   cache.iA0 = cache.iA1 = cache.iA2 = cache.iB0 = cache.iB1 = cache.iB2 = 0;
   for (;;) {
+#ifdef NASCAR_PROFILE
+    const unsigned long long tg0 = __builtin_amdgcn_s_memtime();
+#endif
     Xf xfA = sweep_xf(sA, t1), xfB = sweep_xf_static(sB, t1, qB);
     float distance = gjk_distance(cache, pA, xfA, pB, xfB);
+#ifdef NASCAR_PROFILE
+    if (prof_cyc) prof_cyc[0] += __builtin_amdgcn_s_memtime() - tg0;
+    const unsigned long long ts0 = __builtin_amdgcn_s_memtime();
+#endif
     if (distance <= 0.0f) { *state = TOI_OVERLAPPED; out_t = 0.0f; break; }
     if (distance < target + tolerance) { *state = TOI_TOUCHING; out_t = t1; break; }
     SepFn fcn;
@@ -1129,6 +1174,7 @@ __device__ inline float time_of_impact(int* state, const Poly* pA, const Sweep& 
     ++iter;
 #ifdef NASCAR_PROFILE
     if (prof_iters) ++prof_iters[0];
+    if (prof_cyc) prof_cyc[1] += __builtin_amdgcn_s_memtime() - ts0;
 #endif
     if (done) break;
     if (iter == 20) { *state = TOI_FAILED; out_t = t1; break; }
@@ -1136,18 +1182,23 @@ __device__ inline float time_of_impact(int* state, const Poly* pA, const Sweep& 
   return out_t;
 }
 
-__device__ inline void island_solve_toi(Car& c, const LWall* W, const int* cidx, int n, float subdt, float friction) {
+template <int NMAX>
+__device__ __forceinline__ void island_solve_toi_n(Car& c, const LWall* W, const int* cidx, int n, float subdt, float friction) {
   BodyState A; A.c = c.c; A.a = c.a; A.v = c.v; A.w = c.w;
-  VC vc[MAX_ISLAND];
-  cs_init(vc, n, c, cidx, W, false, 1.0f);
-  for (int it = 0; it < 20; ++it) { if (cs_solve_position(vc, n, A, 1)) break; }
+  VC vc[NMAX];
+  cs_init<NMAX>(vc, n, c, cidx, W, false, 1.0f);
+  for (int it = 0; it < 20; ++it) { if (cs_solve_position<NMAX>(vc, n, A, 1)) break; }
   c.c0 = A.c; c.a0 = A.a;
-  cs_init_velocity(vc, n, c, A);
-  for (int it = 0; it < 6; ++it) cs_solve_velocity(vc, n, A, friction);
+  cs_init_velocity<NMAX>(vc, n, c, A);
+  for (int it = 0; it < 6; ++it) cs_solve_velocity<NMAX>(vc, n, A, friction);
   integrate_positions(A, subdt);
   c.c = A.c; c.a = A.a; c.v = A.v; c.w = A.w;
   sync_transform(c);
-  report(c, vc, n);
+  report<NMAX>(c, vc, n);
+}
+__device__ inline void island_solve_toi(Car& c, const LWall* W, const int* cidx, int n, float subdt, float friction) {
+  if (n <= 2) island_solve_toi_n<2>(c, W, cidx, n, subdt, friction);
+  else island_solve_toi_n<MAX_ISLAND>(c, W, cidx, n, subdt, friction);
 }
 
 // Exact shortcut for b2TimeOfImpact on a (car, static wall) pair.  The root finder can only report
@@ -1203,9 +1254,23 @@ __device__ inline void solve_toi(Car& c, const WallSet& S, float dt, float frict
         int state;
 #ifdef NASCAR_PROFILE
         int pit[2] = {0, 0};
+        unsigned long long pcy[2] = {0, 0};
         CTIME_BEGIN();
-        float beta = time_of_impact(&state, &pa, sA, &pb, sB, 1.0f, pit);
+        float beta = time_of_impact(&state, &pa, sA, &pb, sB, 1.0f, pit, pcy);
         CTIME_END(c, 10);
+        CCOUNT(c, 14, pcy[0]); CCOUNT(c, 15, pcy[1]);
+#ifdef NASCAR_PROFILE_TOI
+        {   // isolated single-lane latency of the same call (first lane of the active set only), 4 repeats
+          const unsigned long long act = __ballot(1);
+          if ((int)__lane_id() == __ffsll((long long)act) - 1) {
+            const unsigned long long ti0 = __builtin_amdgcn_s_memtime();
+            float acc = 0.0f;
+            for (int rep = 0; rep < 4; ++rep) { int st2; acc += time_of_impact(&st2, &pa, sA, &pb, sB, 1.0f); }
+            const unsigned long long ti1 = __builtin_amdgcn_s_memtime();
+            CCOUNT(c, 13, (ti1 - ti0) / 4 + (acc == 123.0f ? 1 : 0)); CCOUNT(c, 9, 1);
+          }
+        }
+#endif
         CCOUNT(c, 6, pit[0]); CCOUNT(c, 7, pit[1]);
         if (state == TOI_FAILED) CCOUNT(c, 1, 1000);
 #else
@@ -1242,8 +1307,8 @@ __device__ inline void solve_toi(Car& c, const WallSet& S, float dt, float frict
       continue;
     }
     set_awake(c);
-    int cidx[MAX_ISLAND]; int n = 0;
-    cidx[n++] = minC; c.ct[minC].flags |= CT_ISLAND;
+    int cidx[MAX_ISLAND] = {0, 0, 0, 0, 0, 0, 0, 0}; int n = 0;
+    island_push(cidx, n, minC); c.ct[minC].flags |= CT_ISLAND;
     {
     CTIME_BEGIN();
     for (int i = 0; i < c.nct; ++i) {
@@ -1257,7 +1322,7 @@ __device__ inline void solve_toi(Car& c, const WallSet& S, float dt, float frict
       if (!(c.ct[i].flags & CT_ENABLED)) continue;
       if (!(c.ct[i].flags & CT_TOUCH)) continue;
       c.ct[i].flags |= CT_ISLAND;
-      cidx[n++] = i;
+      island_push(cidx, n, i);
     }
     CTIME_END(c, 12);
     }
@@ -1267,13 +1332,9 @@ __device__ inline void solve_toi(Car& c, const WallSet& S, float dt, float frict
     island_solve_toi(c, W, cidx, n, subdt, friction);
     CTIME_END(c, 11);
     }
-    {
-    CTIME_BEGIN();
     sync_fixtures(c);
     for (int i = 0; i < c.nct; ++i) c.ct[i].flags &= ~(CT_TOI | CT_ISLAND);
     find_new_contacts(c, S);
-    CTIME_END(c, 13);
-    }
   }
 }
 

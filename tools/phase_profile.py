@@ -137,13 +137,16 @@ def main():
                           f"{info[i, F.index('vy')]:.1f}) angle {info[i, F.index('angle')]:.2f} disabled {info[i, F.index('disabled')]:.0f} n_contacts {info[i, F.index('n_contacts')]:.0f}")
             for i in np.argsort(-cyc)[:24]:
                 if cp[i, 10:14].any():
-                    print(f"    car {i} solve_toi cycles: TOI calls {cp[i, 10]}, island solves {cp[i, 11]}, "
-                          f"event contact updates {cp[i, 12]}, event sync+broadphase {cp[i, 13]}")
+                    iso = f", isolated single-lane TOI {cp[i, 13] / cp[i, 9]:.0f} cycles/call" if cp[i, 9] else ""
+                    print(f"    car {i} solve_toi cycles: TOI calls {cp[i, 10]} (GJK {cp[i, 14]}, separation fn {cp[i, 15]}), "
+                          f"island solves {cp[i, 11]}, event contact updates {cp[i, 12]}{iso}")
+            m9 = cp[:, 9] > 0
+            if m9.any():
+                print(f"  isolated single-lane TOI: {cp[m9, 13].sum() / cp[m9, 9].sum():.0f} cycles/call over {cp[m9, 9].sum()} calls")
             wv = m[np.argmax(m[:, 4] - m[:, 3])]
             print("  slowest wave's b2_step phases (cycles): collide", wv[11] - wv[3], "solve", wv[12] - wv[11],
                   "sync+find", wv[13] - wv[12], "toi", wv[4] - wv[13])
-            print(f"  broadphase full scans per car-step {cp[:, 8].mean():.4f}, cars with a full scan {(cp[:, 8] > 0).sum()}, "
-                  f"candidates per car-step {cp[:, 9].mean():.2f}")
+            print(f"  broadphase full scans per car-step {cp[:, 8].mean():.4f}, cars with a full scan {(cp[:, 8] > 0).sum()}")
             it = cp[:, 7]
             print(f"  root-finder iterations per car-step: mean {it.mean():.2f}, max {it.max()}, cars > 100: {(it > 100).sum()}, "
                   f"FAILED TOIs {(cp[:, 1] // 1000).sum()}")
