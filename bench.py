@@ -269,7 +269,7 @@ def main():
     ap.add_argument("--no-stagger", action="store_true", help="all envs start together (no staggered resets)")
     ap.add_argument("--save-state", default=None, help="write the settled state (engine arena + obs) to this file")
     ap.add_argument("--load-state", default=None, help="start from a state written by --save-state (no settle)")
-    ap.add_argument("--rollout", type=int, default=50,
+    ap.add_argument("--rollout", type=int, default=0,
                     help="steps per fused nascar_rollout launch for the device action sources (0: per-step path, "
                          "nascar_policy_actions + nascar_step per step)")
     ap.add_argument("--mixed", action="store_true", help="env e on track e mod 8 of the sorted bundled tracks "

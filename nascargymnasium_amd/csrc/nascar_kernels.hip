@@ -1217,6 +1217,40 @@ __device__ __forceinline__ void quad_transpose(const float v[4], float o[4], int
 #define RSENSOR_WPE 6   // 4 lanes per car at 6 waves/SIMD: 41.5 us (8 lanes 53.7, 2 lanes 44.3; 16 lanes 62.4)
 #endif
 #define RAY_LPC 4     // lanes per car; each lane walks the lists of rays r, r + 4, r + 8, r + 12
+// One ray's walk of its beam list (list index li, head record h = G.head[li]): the first BEAM_HEAD entries from
+// the head, the rest of the list only when all of them were walked; stops at the first entry whose distance
+// bound lies beyond the best hit.  Returns the best b2PolygonShape::RayCast fraction (2 = no hit).
+__device__ __forceinline__ float ray_walk(const BeamGrid& G, const float4* __restrict__ sw, int li, uint4 h, V2 p1, V2 p2,
+                                          float dx, float dy) {
+  float bi = 2.0f;
+  const uint32_t hv[BEAM_HEAD] = {h.x, h.y, h.z, h.w};
+  bool more = true;
+#pragma unroll
+  for (int k = 0; k < BEAM_HEAD; ++k) {
+    const uint32_t v = hv[k];
+    if ((float)(v >> 16) * 0.01f > bi * 250.0f * 1.00001f + 0.01f) { more = false; break; }
+    const int j = (int)(v & 0xFFFFu);
+    PCOUNT(10, 1);
+    bi = wall_cast(sw[2 * j], sw[2 * j + 1], p1, p2.x, p2.y, dx, dy, bi);
+  }
+  if (more) {
+    const uint32_t s0 = G.start[li] + BEAM_HEAD, e0 = G.start[li + 1];
+    for (uint32_t k = s0; k < e0; ++k) {
+      const uint32_t v = G.ent[k];
+      if ((float)(v >> 16) * 0.01f > bi * 250.0f * 1.00001f + 0.01f) break;
+      const int j = (int)(v & 0xFFFFu);
+      PCOUNT(10, 1);
+      bi = wall_cast(sw[2 * j], sw[2 * j + 1], p1, p2.x, p2.y, dx, dy, bi);
+    }
+  }
+  return bi;
+}
+__device__ __forceinline__ int beam_slot0(double ang) {   // list slot of ray 0's direction bin (see ray_lane)
+  double u = ang * (BEAM_NB / (2.0 * PI_D));
+  u -= BEAM_NB * floor(u * (1.0 / BEAM_NB));
+  return beam_slot(min(BEAM_NB - 1, max(0, (int)u)));
+}
+
 // The 4-lane work of car n, lane r (rays r, r + 4, r + 8, r + 12) in ray_sensor_kernel / rollout_kernel: both
 // passes, the beam-list walks against the wall image sw (LDS), the quad transpose and the obs stores.
 // All 4 lanes of a car are consecutive lanes of one quad and call this together.
@@ -1260,28 +1294,7 @@ __device__ __forceinline__ void ray_lane(const Params& P, const TrackDev& T, con
       float bi = 2.0f;
       if (base >= 0) {
         const int sl = slot_of(i);
-        // the list's first BEAM_HEAD entries in one load; the rest of the list only when all were walked
-        const uint4 h = G.head[base + sl];
-        const uint32_t hv[BEAM_HEAD] = {h.x, h.y, h.z, h.w};
-        bool more = true;
-#pragma unroll
-        for (int k = 0; k < BEAM_HEAD; ++k) {
-          const uint32_t v = hv[k];
-          if ((float)(v >> 16) * 0.01f > bi * 250.0f * 1.00001f + 0.01f) { more = false; break; }
-          const int j = (int)(v & 0xFFFFu);
-          PCOUNT(10, 1);
-          bi = wall_cast(sw[2 * j], sw[2 * j + 1], p1, p2.x, p2.y, dx, dy, bi);
-        }
-        if (more) {
-          const uint32_t s0 = G.start[base + sl] + BEAM_HEAD, e0 = G.start[base + sl + 1];
-          for (uint32_t k = s0; k < e0; ++k) {
-            const uint32_t v = G.ent[k];
-            if ((float)(v >> 16) * 0.01f > bi * 250.0f * 1.00001f + 0.01f) break;
-            const int j = (int)(v & 0xFFFFu);
-            PCOUNT(10, 1);
-            bi = wall_cast(sw[2 * j], sw[2 * j + 1], p1, p2.x, p2.y, dx, dy, bi);
-          }
-        }
+        bi = ray_walk(G, sw, base + sl, G.head[base + sl], p1, p2, dx, dy);
       } else {
         PCOUNT(9, 1);
         bi = ray_fallback(T, p1, p2.x, p2.y, dx, dy, ps.z, i);
@@ -1298,6 +1311,85 @@ __device__ __forceinline__ void ray_lane(const Params& P, const TrackDev& T, con
   }
 }
 
+// rollout_kernel's sensor phase for one block: thread t owns lane r = t % 4 of the cars in slots t / 4 + 32 j
+// (j = 0..3, RAY_LPC rounds of ray_lane's mapping).  At the fused kernel's low occupancy the dependent loads
+// of a lane (pose -> beam cell -> list heads) are not hidden by other waves, so they are issued for all four
+// cars and all 16 of the thread's rays at once before any list is walked.  Pass B (auto-reset cars) goes
+// through ray_lane per car.  Same walks and results as ray_lane.
+__device__ __forceinline__ void ray_block_batched(const Params& P, const TrackDev& T, const float4* __restrict__ sw,
+                                                  float* obs, int passes) {
+  static_assert(RAY_LPC == 4 && SBLOCK / RAY_LPC == 32, "batched sensor mapping");
+  constexpr int NJ = 4, RPL = 4;
+  const int t = threadIdx.x, r = t & 3, C = P.C;
+  const BeamGrid G = T.beam;
+  int n[NJ], base[NJ], slot0[NJ];
+  bool ok[NJ];
+  float4 pa[NJ];
+  double2 cs[NJ];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int lc = (t >> 2) + 32 * j, el = lc / C, car = lc - el * C;
+    const int env = blk_env_of(P, el, blockIdx.x * P.epb + el);
+    ok[j] = env >= 0;
+    n[j] = ok[j] ? env * C + car : 0;
+  }
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    pa[j] = ok[j] ? P.pose[n[j]] : make_float4(0.f, 0.f, 0.f, 0.f);
+    cs[j] = ok[j] ? P.pose_cs[n[j]] : make_double2(1.0, 0.0);
+  }
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    ok[j] = ok[j] && (__float_as_int(pa[j].w) & PM_A_OBS) != 0;
+    base[j] = ok[j] ? beam_cell_base(G, pa[j].x, pa[j].y) : -1;
+    slot0[j] = beam_slot0((double)pa[j].z);
+  }
+  V2 p2[NJ][RPL];
+  uint4 hd[NJ][RPL];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+#pragma unroll
+    for (int q = 0; q < RPL; ++q) {
+      double dxd, dyd;
+      p2[j][q] = ray_end(P, pa[j].x, pa[j].y, pa[j].z, cs[j].x, cs[j].y, r + RAY_LPC * q, dxd, dyd);
+      const int sl = (slot0[j] & ~15) | ((slot0[j] - (r + RAY_LPC * q)) & 15);
+      hd[j][q] = base[j] >= 0 ? G.head[base[j] + sl] : make_uint4(0, 0, 0, 0);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    if (!ok[j]) continue;                    // uniform over the car's quad
+    const V2 p1 = V(pa[j].x, pa[j].y);
+    float v[RPL] = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll 1
+    for (int q = 0; q < RPL; ++q) {
+      const int i = r + RAY_LPC * q;
+      const V2 e = q == 0 ? p2[j][0] : q == 1 ? p2[j][1] : q == 2 ? p2[j][2] : p2[j][3];
+      const float dx = (e.x - p1.x) * 0.004f, dy = (e.y - p1.y) * 0.004f;   // cull only
+      float bi;
+      if (base[j] >= 0) {
+        const uint4 h = q == 0 ? hd[j][0] : q == 1 ? hd[j][1] : q == 2 ? hd[j][2] : hd[j][3];
+        const int sl = (slot0[j] & ~15) | ((slot0[j] - i) & 15);
+        bi = ray_walk(G, sw, base[j] + sl, h, p1, e, dx, dy);
+      } else {
+        bi = ray_fallback(T, p1, e.x, e.y, dx, dy, pa[j].z, i);
+      }
+      put4(v, q, sensor_value(bi));
+    }
+    float o[4];
+    quad_transpose(v, o, r);
+    const size_t at = (size_t)n[j] * 38 + 22 + 4 * r;
+    *(float2*)(obs + at) = make_float2(o[0], o[1]); *(float2*)(obs + at + 2) = make_float2(o[2], o[3]);
+  }
+  if (passes & 2) {
+#pragma unroll 1
+    for (int j = 0; j < NJ; ++j) {
+      const int lc = (t >> 2) + 32 * j, el = lc / C, car = lc - el * C;
+      const int env = blk_env_of(P, el, blockIdx.x * P.epb + el);
+      if (env >= 0) ray_lane(P, T, sw, env * C + car, r, obs, nullptr, 2);
+    }
+  }
+}
 __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(RSENSOR_WPE)))
 ray_sensor_kernel(Params P, float* obs, float* terminal_obs, int passes) {
   constexpr int CPW = BLOCK / RAY_LPC;
@@ -1728,14 +1820,7 @@ static __device__ __attribute__((noinline)) void ro_logic_phase(ParamsK Pk, floa
 static __device__ __attribute__((noinline)) void ro_sensor_phase(ParamsK Pk, float* obs, int passes) {
   const Params& P = *(const Params*)Pk;
   const TrackDev T = ro_track(P);
-  const int C = P.C;
-#pragma unroll 1
-  for (int q = 0; q < RAY_LPC; ++q) {   // SBLOCK car slots x RAY_LPC lanes: RAY_LPC rounds of the block
-    const int task = threadIdx.x + q * SBLOCK, lc = task / RAY_LPC, r = task - lc * RAY_LPC;
-    const int el = lc / C, car = lc - el * C;
-    const int env = blk_env_of(P, el, blockIdx.x * P.epb + el);
-    if (env >= 0) ray_lane(P, T, (const float4*)smem, env * C + car, r, obs, nullptr, passes);
-  }
+  ray_block_batched(P, T, (const float4*)smem, obs, passes);
 }
 __global__ void __launch_bounds__(SBLOCK) __attribute__((amdgpu_waves_per_eu(MODEL_WPE)))
 rollout_kernel(const Params* __restrict__ Pg, int K, int policy, uint64_t seed, int64_t step0, float* obs, float* reward,
