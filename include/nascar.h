@@ -47,7 +47,9 @@ const char* nascar_last_error(void);
  * are derived on the host here.  Returns the track id (>= 0). */
 int nascar_add_track(NascarHandle* h, const double* segments, int32_t nseg, double total_length,
                      const double* walls, int32_t nwall);
-/* per-env track ids (host array of E ints); envs are grouped per track into workgroups. */
+/* per-env track ids (host array of E ints); envs are grouped per track into workgroups.  A changed id takes
+ * effect at that env's next nascar_reset (fresh physics worlds on the new track, as CarEnv.reset recreates
+ * CarPhysics, src/car_env.py:375-394); until then the env keeps stepping on its old track. */
 int nascar_set_env_tracks(NascarHandle* h, const int32_t* env_track);
 
 /* CarEnv.reset (src/car_env.py:316-535) for the envs whose env_mask[e] != 0 (device uint8[E];
@@ -83,6 +85,12 @@ int nascar_rollout(NascarHandle* h, int32_t policy, uint64_t seed, int64_t step0
 /* Info builder (src/car_env.py:1160-1227, src/lap_timer.py:354-372): per-car float64 [E*C*N_INFO]
  * (field order: nascargymnasium_amd/_lib.py INFO_FIELDS) written to a device buffer. */
 int nascar_get_info(NascarHandle* h, double* info, void* stream);
+
+/* Car.velocity_history for Car.validate_performance (src/car.py:173, 384-386, 1060-1098): enable != 0 keeps
+ * every car's speed after each step in a 600-sample window on the device (VH_RING x N float32, outside the
+ * state arena, so snapshots do not carry it) and nascar_get_info reports perf_count / perf_max_speed /
+ * perf_first_fast; 0 frees it (the info fields then read -1 / 0 / -1).  Off by default. */
+int nascar_set_perf_history(NascarHandle* h, int32_t enable, void* stream);
 
 /* Raw state snapshot / restore (checkpointing and state-injection parity tests). */
 int64_t nascar_state_bytes(NascarHandle* h);

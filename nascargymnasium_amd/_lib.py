@@ -15,8 +15,9 @@ CSRC = os.path.join(HERE, "csrc")
 INFO_FIELDS = ["x", "y", "vx", "vy", "angle", "omega", "speed", "lap_count", "last_lap_time", "best_lap_time",
                "is_timing", "current_lap_time", "total_distance_traveled", "has_crossed_startline", "disabled",
                "cumulative_reward", "cumulative_impact_force", "on_track", "engine_rpm", "simulation_time",
-               "n_contacts", "error", "track_progress"]
+               "n_contacts", "error", "track_progress", "perf_count", "perf_max_speed", "perf_first_fast"]
 N_INFO = len(INFO_FIELDS)
+INFO_INDEX = {f: i for i, f in enumerate(INFO_FIELDS)}
 OBS_DIM = 38
 
 # car flag bits / env flag bits (csrc/nascar_layout.h)
@@ -75,6 +76,8 @@ def lib():
     L.nascar_step.restype = ctypes.c_int
     L.nascar_rollout.argtypes = [vp, i32, u64, i64, i32, vp, vp, vp, vp, i32, i32, vp]
     L.nascar_rollout.restype = ctypes.c_int
+    L.nascar_set_perf_history.argtypes = [vp, i32, vp]
+    L.nascar_set_perf_history.restype = ctypes.c_int
     L.nascar_get_info.argtypes = [vp, vp, vp]
     L.nascar_get_info.restype = ctypes.c_int
     L.nascar_state_bytes.argtypes = [vp]
@@ -99,7 +102,7 @@ def lib():
 
 
 EXPORTED = ["nascar_create", "nascar_destroy", "nascar_last_error", "nascar_add_track", "nascar_set_env_tracks",
-            "nascar_reset", "nascar_step", "nascar_rollout", "nascar_get_info", "nascar_state_bytes", "nascar_get_state",
+            "nascar_reset", "nascar_step", "nascar_rollout", "nascar_get_info", "nascar_set_perf_history", "nascar_state_bytes", "nascar_get_state",
             "nascar_set_state", "nascar_policy_actions", "nascar_set_actor", "nascar_actor_forward",
             "nascar_debug_sincosf", "nascar_debug_sensors"]
 

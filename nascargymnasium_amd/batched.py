@@ -33,7 +33,7 @@ class BatchedCarEnv:
 
     def __init__(self, num_envs: int, num_cars: int = 1, track_file: Union[str, Sequence[str]] = "daytona",
                  reset_on_lap: bool = False, device: Union[str, int, torch.device] = "cuda",
-                 start_position=None, start_angle: float = 0.0):
+                 start_position=None, start_angle: float = 0.0, perf_history: bool = False):
         if not torch.cuda.is_available():
             raise RuntimeError("BatchedCarEnv needs a HIP device (torch.cuda.is_available() is False); "
                                "the product path has no CPU fallback")
@@ -68,6 +68,15 @@ class BatchedCarEnv:
         self.terminal_obs = torch.zeros_like(self.obs)
         self._info = torch.zeros(self.E, self.C, _lib.N_INFO, dtype=torch.float64, device=dev)
         self._actions = torch.zeros(self.E, self.C, 2, dtype=torch.float32, device=dev)
+        if perf_history:
+            self.set_perf_history(True)
+
+    def set_perf_history(self, enable: bool = True):
+        """Keep Car.velocity_history on the device so the info's `performance` dict is Car.validate_performance
+        (src/car.py:1060-1098); a 640-sample float32 ring per car, one 4-byte store per car-step.  The window starts
+        at the next reset of each env."""
+        with torch.cuda.device(self.device):
+            _lib.check(self.L.nascar_set_perf_history(self.h, int(bool(enable)), _stream()))
 
     def _add_track(self, path: str) -> int:
         """Load a .track file into the handle (TrackLoader + _create_track_walls tables); returns its id."""
@@ -85,8 +94,10 @@ class BatchedCarEnv:
         return tid
 
     def set_env_tracks(self, files: Sequence[str]):
-        """Per-env track (name or path) for the next reset of each env; new tracks are loaded on demand.
-        The start pose is the handle's (every bundled track starts its GRID at (0, 0), heading 0)."""
+        """Per-env track (name or path), applied by the next reset of each env (fresh worlds on the new track, as
+        CarEnv.reset rebuilds CarPhysics, src/car_env.py:375-394); until then an env steps on its old track.  New
+        tracks are loaded on demand.  The start pose is the handle's (every bundled track starts its GRID at (0, 0),
+        heading 0)."""
         if isinstance(files, str):
             files = [files] * self.E
         if len(files) != self.E:

@@ -77,61 +77,89 @@ class BaseEnv(Env):
             raise ValueError(f"Invalid discrete action: {action}") from None
 
 
-class _LazyInfo(dict):
-    """The reference's info dict (src/car_env.py:1160-1227), built from the device info
-    tensor on first access (the reference builds it eagerly every step)."""
+# src/constants/environment.py:19-26
+MIN_REALISTIC_FPS, MAX_REALISTIC_FPS = 5.0, 300.0
+PERFORMANCE_VALIDATION_MIN_SAMPLES = 10
+PERFORMANCE_SPEED_TOLERANCE, PERFORMANCE_TIME_TOLERANCE = 0.95, 1.1
 
-    def __init__(self, builder):
-        super().__init__()
-        self._builder = builder
-        self._built = False
+_SIM_T = [0.0]
 
-    def _build(self):
-        if not self._built:
-            self._built = True
-            super().update(self._builder())
 
-    def __getitem__(self, k):
-        self._build()
-        return super().__getitem__(k)
+def _sim_time(k: int) -> float:
+    """the float64 time after k steps of 1/60 s, summed one step at a time as CarEnv/CarPhysics/
+    validate_performance do (src/car_env.py:573, src/car.py:1085-1086)"""
+    while len(_SIM_T) <= k:
+        _SIM_T.append(_SIM_T[-1] + DT)
+    return _SIM_T[k]
 
-    def get(self, k, d=None):
-        self._build()
-        return super().get(k, d)
 
-    def __contains__(self, k):
-        self._build()
-        return super().__contains__(k)
+def validate_performance(count: int, max_speed: float, first_fast: int) -> dict:
+    """Car.validate_performance (src/car.py:1060-1098) from the device's window summary: count = samples in
+    velocity_history (-1: history not kept), max_speed = their maximum, first_fast = index of the first sample
+    >= CAR_TARGET_100KMH_MS (-1: none)."""
+    res = {"max_speed_ms": CAR_MAX_SPEED_MS, "target_100kmh_ms": CAR_TARGET_100KMH_MS,
+           "target_acceleration_time": CAR_ACCELERATION_0_100_KMH, "current_max_speed": 0.0,
+           "estimated_0_100_time": 0.0, "performance_valid": False}
+    if count > PERFORMANCE_VALIDATION_MIN_SAMPLES:
+        res["current_max_speed"] = max_speed
+        if first_fast >= 0:
+            res["estimated_0_100_time"] = _sim_time(first_fast + 1)
+        speed_ok = max_speed >= CAR_MAX_SPEED_MS * PERFORMANCE_SPEED_TOLERANCE
+        est = res["estimated_0_100_time"]
+        accel_ok = est <= CAR_ACCELERATION_0_100_KMH * PERFORMANCE_TIME_TOLERANCE if est > 0 else False
+        res["performance_valid"] = speed_ok and accel_ok
+    return res
 
-    def __iter__(self):
-        self._build()
-        return super().__iter__()
 
-    def __len__(self):
-        self._build()
-        return super().__len__()
+def physics_stats(k: int, bodies: int) -> dict:
+    """CarPhysics.get_performance_stats (src/car_physics.py:573-592) after k steps since the reset: the world's
+    simulation_time is the env time before its last step, average_fps is updated every 60 steps
+    (src/car_physics.py:374-385) and clamped to [MIN_REALISTIC_FPS, MAX_REALISTIC_FPS]."""
+    fps = 60.0
+    if k >= 60:
+        m = 60 * (k // 60)
+        elapsed = _sim_time(m - 1) - (_sim_time(m - 61) if m > 60 else 0.0)
+        fps = 60 / elapsed if elapsed > 0 else 60.0
+    return {"physics_steps": k, "simulation_time": _sim_time(k - 1) if k > 0 else 0.0,
+            "average_fps": max(MIN_REALISTIC_FPS, min(fps, MAX_REALISTIC_FPS)), "bodies_in_world": bodies}
 
-    def keys(self):
-        self._build()
-        return super().keys()
 
-    def items(self):
-        self._build()
-        return super().items()
-
-    def values(self):
-        self._build()
-        return super().values()
-
-    def __repr__(self):
-        self._build()
-        return super().__repr__()
-
-    def __eq__(self, other):
-        self._build()
-        return dict(self) == other
-
-    __hash__ = None
+def build_info(info_np, num_cars: int, followed: int, reason, bodies: int) -> dict:
+    """CarEnv._get_multi_info (src/car_env.py:1160-1227) as a plain dict from one env's host copy of the device
+    info rows ([C, N_INFO] float64, fields _lib.INFO_FIELDS)."""
+    F = _lib.INFO_INDEX
+    cars = []
+    for i in range(num_cars):
+        r = info_np[i]
+        speed = float(r[F["speed"]])
+        last = None if np.isnan(r[F["last_lap_time"]]) else float(r[F["last_lap_time"]])
+        best = None if np.isnan(r[F["best_lap_time"]]) else float(r[F["best_lap_time"]])
+        timing = bool(r[F["is_timing"]])
+        cur = float(r[F["current_lap_time"]])
+        cars.append({
+            "car_index": i,
+            "disabled": bool(r[F["disabled"]]),
+            "car_position": (float(r[F["x"]]), float(r[F["y"]])),
+            "car_speed_kmh": speed * 3.6,
+            "car_speed_ms": speed,
+            "on_track": bool(r[F["on_track"]]),
+            "performance": validate_performance(int(r[F["perf_count"]]), float(r[F["perf_max_speed"]]),
+                                                int(r[F["perf_first_fast"]])),
+            "lap_timing": {   # LapTimer.get_timing_info (src/lap_timer.py:354-372)
+                "current_lap_time": cur, "last_lap_time": last, "best_lap_time": best,
+                "lap_count": int(r[F["lap_count"]]), "is_timing": timing,
+                "has_crossed_startline": bool(r[F["has_crossed_startline"]]),
+                "total_distance_traveled": float(r[F["total_distance_traveled"]]),
+                "formatted_current": _format_time(cur if timing else None),
+                "formatted_last": _format_time(last), "formatted_best": _format_time(best)},
+            "cumulative_reward": float(r[F["cumulative_reward"]]),
+            "cumulative_impact_force": float(r[F["cumulative_impact_force"]]),
+        })
+    sim = float(info_np[0, F["simulation_time"]])
+    k = int(round(sim / DT))
+    physics = [{**physics_stats(k, bodies), **c["performance"]} for c in cars]
+    return {"simulation_time": sim, "num_cars": num_cars, "followed_car_index": followed,
+            "termination_reason": reason, "cars": cars, "physics": physics}
 
 
 def _format_time(t: Optional[float]) -> str:
@@ -184,7 +212,7 @@ class CarEnv(BaseEnv):
         self._torch = torch
         self._engine = BatchedCarEnv(1, num_cars, track_path(self.track_file), reset_on_lap=reset_on_lap,
                                      device=device if device is not None else "cuda",
-                                     start_position=self.start_position, start_angle=start_angle)
+                                     start_position=self.start_position, start_angle=start_angle, perf_history=True)
         self._ready = False
         self.cars = []
         self.disabled_cars = set()
@@ -228,7 +256,7 @@ class CarEnv(BaseEnv):
             self.track = load_track(track_path(self.track_file))
             self._engine.set_env_tracks([track_path(self.track_file)])
         obs = self._engine.reset()[0].cpu().numpy()
-        self._info_cache = None
+        self._info_cache = self._engine.info_tensor()[0].cpu().numpy()
         self._ready = True
         self.cars = list(range(self.num_cars))
         self.disabled_cars = set()
@@ -236,7 +264,7 @@ class CarEnv(BaseEnv):
         self.termination_reason = None
         self.simulation_time = 0.0
         self._cumulative_rewards = [0.0] * self.num_cars
-        info = self._make_info()
+        info = self._make_info(self._info_cache)
         return (obs[0], info) if self.num_cars == 1 else (obs, info)
 
     def step(self, action):
@@ -255,13 +283,19 @@ class CarEnv(BaseEnv):
             dev_a = torch.from_numpy(np.ascontiguousarray(a)).view(1, C, 2)
         self.last_action = np.array(internal[0], dtype=np.float32)
         self.elapsed_time = time.time() - self.start_time
-        obs_t, rew_t, term_t, trunc_t = self._engine.step(dev_a.to(self._engine.device))
-        # one device->host transfer of everything the caller sees this step
-        info_t = self._engine.info_tensor()
-        obs, rew = obs_t[0].cpu().numpy(), rew_t[0].cpu().numpy()
-        terminated, truncated = bool(term_t[0].item()), bool(trunc_t[0].item())
-        reason = int(self._engine.termination_reason()[0].item())
-        info_np = info_t[0].cpu().numpy()
+        eng = self._engine
+        eng.step(dev_a.to(eng.device))
+        # one device->host transfer of everything the caller sees this step: obs, reward (float32, exact in
+        # float64), the env flag byte and the info rows, packed on the device
+        info_t = eng.info_tensor()
+        packed = torch.cat([eng.obs[0].reshape(-1).double(), eng.reward[0].double(), eng.env_flags[:1].double(),
+                            info_t[0].reshape(-1)]).cpu().numpy()
+        obs = packed[:C * 38].astype(np.float32).reshape(C, 38)
+        rew = packed[C * 38:C * 39].astype(np.float32)
+        ef = int(packed[C * 39])
+        terminated, truncated = bool(ef & _lib.EF_TERMINATED), bool(ef & _lib.EF_TRUNCATED)
+        reason = (ef >> 4) & 7
+        info_np = packed[C * 39 + 1:].reshape(C, _lib.N_INFO)
         F = _lib.INFO_FIELDS
         self.simulation_time = float(info_np[0, F.index("simulation_time")])
         self.disabled_cars = {i for i in range(C) if info_np[i, F.index("disabled")] != 0}
@@ -313,48 +347,10 @@ class CarEnv(BaseEnv):
         return out
 
     # ------------------------------------------------------------------ info (src/car_env.py:1160-1227)
-    def _make_info(self, info_np=None):
-        def build():
-            nonlocal info_np
-            if info_np is None:
-                info_np = self._engine.info_tensor()[0].cpu().numpy()
-            F = {f: i for i, f in enumerate(_lib.INFO_FIELDS)}
-            cars = []
-            for i in range(self.num_cars):
-                r = info_np[i]
-                speed = float(r[F["speed"]])
-                last = None if np.isnan(r[F["last_lap_time"]]) else float(r[F["last_lap_time"]])
-                best = None if np.isnan(r[F["best_lap_time"]]) else float(r[F["best_lap_time"]])
-                timing = bool(r[F["is_timing"]])
-                cur = float(r[F["current_lap_time"]])
-                cars.append({
-                    "car_index": i,
-                    "disabled": bool(r[F["disabled"]]),
-                    "car_position": (float(r[F["x"]]), float(r[F["y"]])),
-                    "car_speed_kmh": speed * 3.6,
-                    "car_speed_ms": speed,
-                    "on_track": bool(r[F["on_track"]]),
-                    "performance": {   # src/car.py:1060-1098 (velocity history is not kept on the device)
-                        "max_speed_ms": CAR_MAX_SPEED_MS, "target_100kmh_ms": CAR_TARGET_100KMH_MS,
-                        "target_acceleration_time": CAR_ACCELERATION_0_100_KMH, "current_max_speed": 0.0,
-                        "estimated_0_100_time": 0.0, "performance_valid": False},
-                    "lap_timing": {   # LapTimer.get_timing_info (src/lap_timer.py:354-372)
-                        "current_lap_time": cur, "last_lap_time": last, "best_lap_time": best,
-                        "lap_count": int(r[F["lap_count"]]), "is_timing": timing,
-                        "has_crossed_startline": bool(r[F["has_crossed_startline"]]),
-                        "total_distance_traveled": float(r[F["total_distance_traveled"]]),
-                        "formatted_current": _format_time(cur if timing else None),
-                        "formatted_last": _format_time(last), "formatted_best": _format_time(best)},
-                    "cumulative_reward": float(r[F["cumulative_reward"]]),
-                    "cumulative_impact_force": float(r[F["cumulative_impact_force"]]),
-                })
-            sim = float(info_np[0, F["simulation_time"]])
-            physics = [{"physics_steps": int(round(sim / DT)), "simulation_time": sim, "average_fps": 60.0,
-                        "bodies_in_world": 1 + self._nwalls(),
-                        **c["performance"]} for c in cars]
-            return {"simulation_time": sim, "num_cars": self.num_cars, "followed_car_index": self.followed_car_index,
-                    "termination_reason": self.termination_reason, "cars": cars, "physics": physics}
-        return _LazyInfo(build)
+    def _make_info(self, info_np) -> dict:
+        """the step's / reset's info dict, built eagerly from the host copy fetched with the step (picklable,
+        as SubprocVecEnv workers need; later steps do not change it)"""
+        return build_info(info_np, self.num_cars, self.followed_car_index, self.termination_reason, 1 + self._nwalls())
 
     def _nwalls(self) -> int:
         from .track import build_walls

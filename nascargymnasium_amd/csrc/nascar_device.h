@@ -589,9 +589,12 @@ struct VC {
   V2 ln, lp, lps[2]; int pcount, type, ci;
 };
 struct BodyState { V2 c; float a; V2 v; float w; };
+// unroll count of the per-contact loops below: full for islands of <= 2 contacts (register-resident), else a loop
+#define UNROLL_SMALL NUNR<NMAX>::v
+template <int NMAX> struct NUNR { static constexpr int v = NMAX <= 2 ? NMAX : 1; };
 
 template <int NMAX> __device__ __forceinline__ void cs_init(VC* vc, int n, const Car& c, const int* cidx, const LWall* W, bool warm, float dtRatio) {
-#pragma unroll (NMAX <= 2 ? NMAX : 1)   // registers for small islands; the general bound stays a loop
+#pragma unroll UNROLL_SMALL   // registers for small islands; the general bound stays a loop
   for (int i = 0; i < NMAX; ++i) {
     if (i >= n) break;
     const DContact& ct = c.ct[cidx[i]];
@@ -618,7 +621,7 @@ template <int NMAX> __device__ __forceinline__ void cs_init(VC* vc, int n, const
 template <int NMAX> __device__ __forceinline__ void cs_init_velocity(VC* vc, int n, const Car& c, const BodyState& A) {
   const float mA = CAR_INV_MASS, iA = CAR_INV_I, mB = 0.0f, iB = 0.0f;
   const float friction_unused = 0.0f; (void)friction_unused;
-#pragma unroll (NMAX <= 2 ? NMAX : 1)   // registers for small islands; the general bound stays a loop
+#pragma unroll UNROLL_SMALL   // registers for small islands; the general bound stays a loop
   for (int i = 0; i < NMAX; ++i) {
     if (i >= n) break;
     VC& v = vc[i];
@@ -669,7 +672,7 @@ template <int NMAX> __device__ __forceinline__ void cs_init_velocity(VC* vc, int
 
 template <int NMAX> __device__ __forceinline__ void cs_warm_start(VC* vc, int n, BodyState& A) {
   const float mA = CAR_INV_MASS, iA = CAR_INV_I, mB = 0.0f, iB = 0.0f;
-#pragma unroll (NMAX <= 2 ? NMAX : 1)   // registers for small islands; the general bound stays a loop
+#pragma unroll UNROLL_SMALL   // registers for small islands; the general bound stays a loop
   for (int i = 0; i < NMAX; ++i) {
     if (i >= n) break;
     VC& v = vc[i];
@@ -694,7 +697,7 @@ __device__ __forceinline__ V2 rel_vel(V2 vA, float wA, V2 vB, float wB, const VC
 
 template <int NMAX> __device__ __forceinline__ void cs_solve_velocity(VC* vc, int n, BodyState& A, float friction) {
   const float mA = CAR_INV_MASS, iA = CAR_INV_I, mB = 0.0f, iB = 0.0f;
-#pragma unroll (NMAX <= 2 ? NMAX : 1)   // registers for small islands; the general bound stays a loop
+#pragma unroll UNROLL_SMALL   // registers for small islands; the general bound stays a loop
   for (int i = 0; i < NMAX; ++i) {
     if (i >= n) break;
     VC& v = vc[i];
@@ -766,7 +769,7 @@ template <int NMAX> __device__ __forceinline__ void cs_solve_velocity(VC* vc, in
 }
 
 template <int NMAX> __device__ __forceinline__ void cs_store(const VC* vc, int n, Car& c) {
-#pragma unroll (NMAX <= 2 ? NMAX : 1)   // registers for small islands; the general bound stays a loop
+#pragma unroll UNROLL_SMALL   // registers for small islands; the general bound stays a loop
   for (int i = 0; i < NMAX; ++i) {
     if (i >= n) break;
     DContact& m = c.ct[vc[i].ci];
@@ -778,7 +781,7 @@ template <int NMAX> __device__ __forceinline__ void cs_store(const VC* vc, int n
 template <int NMAX> __device__ __forceinline__ int cs_solve_position(VC* vc, int n, BodyState& A, int toi) {
   float minSep = 0.0f;
   const float mA = CAR_INV_MASS, iA = CAR_INV_I, mB = 0.0f, iB = 0.0f;
-#pragma unroll (NMAX <= 2 ? NMAX : 1)   // registers for small islands; the general bound stays a loop
+#pragma unroll UNROLL_SMALL   // registers for small islands; the general bound stays a loop
   for (int i = 0; i < NMAX; ++i) {
     if (i >= n) break;
     VC& v = vc[i];
@@ -815,7 +818,7 @@ template <int NMAX> __device__ __forceinline__ int cs_solve_position(VC* vc, int
 }
 
 template <int NMAX> __device__ __forceinline__ void report(Car& c, const VC* vc, int n) {
-#pragma unroll (NMAX <= 2 ? NMAX : 1)   // registers for small islands; the general bound stays a loop
+#pragma unroll UNROLL_SMALL   // registers for small islands; the general bound stays a loop
   for (int i = 0; i < NMAX; ++i) {
     if (i >= n) break;
     lis_post(c, vc[i].pointCount, vc[i].p[0].ni, vc[i].p[1].ni);
@@ -1210,18 +1213,37 @@ __device__ inline void island_solve_toi(Car& c, const LWall* W, const int* cidx,
 // is a lower bound of their distance there.  If that bound minus the motion exceeds target + tol by a
 // 1 cm rounding margin, the swept car never comes that close and TOI would return SEPARATED or FAILED:
 // alpha = 1 without running it (identical result, verified by every GPU-vs-oracle test).
-#define TOI_CULL_DIST (0.005f + 0.00125f + 0.01f)
+//
+// The bound is a separating-axis one per fixed world axis u (the wall's two axes and the car's two axes at
+// the end pose, each oriented from the wall toward the car): the gap along u at sweep parameter beta is
+//   gap_u(beta) >= gap_u(end) - max(0, u . (c - c0)) - |a - a0| * R_car
+// because u . c(beta) = u . c - (1 - beta) u . (c - c0) (linear sweep) and the rotation moves every car
+// point by at most |a - a0| * R_car.  A car sliding along or approaching a wall therefore keeps its end
+// pose gap (only motion AWAY from the wall along u widens the interval); distance(beta) >= gap_u(beta).
+// Box gaps are exact: gap_u = |u . d| - e_car(u) - e_wall(u) with e(u) = hx |u . x| + hy |u . y|.
+// The rounding margin (3 mm) is ~25 ulps of the largest track coordinates (|x| < 1500 m, ulp 1.2e-4).
+#define TOI_CULL_DIST (0.005f + 0.00125f + 0.003f)
+__device__ __forceinline__ float toi_gap_bound(V2 u, V2 d, V2 dc, V2 cx, V2 cy, V2 wx, V2 wy, float whx, float why) {
+  const float s = vdot(u, d);
+  const float gap = fabsf(s) - (CAR_HX * fabsf(vdot(u, cx)) + CAR_HY * fabsf(vdot(u, cy)))
+                             - (whx * fabsf(vdot(u, wx)) + why * fabsf(vdot(u, wy)));
+  const float away = s >= 0.0f ? vdot(u, dc) : -vdot(u, dc);   // motion toward +gap during the sweep
+  return gap - fmaxb(0.0f, away);
+}
 __device__ __forceinline__ bool toi_far(const Car& c, const Poly* pa, const LWall& wl) {
 #ifdef NASCAR_NO_TOI_CULL   // A/B and verification builds only
   return false;
 #endif
+  (void)pa;
   const float R_CAR = 2.80389f;   // > sqrt(CAR_HX^2 + CAR_HY^2) = 2.80323
-  const float motion = vlen(vsub(c.c, c.c0)) + fabsf(c.a - c.a0) * R_CAR;
-  Poly pb; make_box(&pb, wl.hx, wl.hy);
-  const Xf xfB = wall_xf(wl);
-  int e;
-  const float sep = fmaxb(find_max_separation(&e, pa, c.xf, &pb, xfB), find_max_separation(&e, &pb, xfB, pa, c.xf));
-  return sep - motion > TOI_CULL_DIST;
+  const V2 cx = V(c.xf.q.c, c.xf.q.s), cy = V(-c.xf.q.s, c.xf.q.c);
+  const V2 wx = V(wl.qc, wl.qs), wy = V(-wl.qs, wl.qc);
+  const V2 d = vsub(c.xf.p, V(wl.px, wl.py)), dc = vsub(c.c, c.c0);
+  float b = toi_gap_bound(wx, d, dc, cx, cy, wx, wy, wl.hx, wl.hy);
+  b = fmaxb(b, toi_gap_bound(wy, d, dc, cx, cy, wx, wy, wl.hx, wl.hy));
+  b = fmaxb(b, toi_gap_bound(cx, d, dc, cx, cy, wx, wy, wl.hx, wl.hy));
+  b = fmaxb(b, toi_gap_bound(cy, d, dc, cx, cy, wx, wy, wl.hx, wl.hy));
+  return b - fabsf(c.a - c.a0) * R_CAR > TOI_CULL_DIST;
 }
 
 // b2World::SolveTOI
@@ -1244,6 +1266,16 @@ __device__ inline void solve_toi(Car& c, const WallSet& S, float dt, float frict
         const LWall& wl = W[ct.wall];
         if (toi_far(c, &pa, wl)) {
           PCOUNT(13, 1); CCOUNT(c, 3, 1);
+#ifdef NASCAR_TOI_CULL_CHECK   // verification build: run the culled TOI anyway, count TOUCHING outcomes
+          {
+            Poly pb; make_box(&pb, wl.hx, wl.hy);
+            Sweep sA; sA.c0 = c.c0; sA.c = c.c; sA.a0 = c.a0; sA.a = c.a; sA.alpha0 = c.alpha0;
+            Sweep sB; sB.c0 = V(wl.px, wl.py); sB.c = sB.c0; sB.a0 = wl.ang; sB.a = wl.ang; sB.alpha0 = 0.0f;
+            int st; (void)time_of_impact(&st, &pa, sA, &pb, sB, 1.0f);
+            PCOUNT(16, 1);
+            if (st == TOI_TOUCHING) PCOUNT(17, 1);
+          }
+#endif
           ct.toi = 1.0f; ct.flags |= CT_TOI;
           continue;   // alpha = 1: never below minAlpha
         }

@@ -95,6 +95,7 @@ struct Params {
   double2* pose_cs;    // [2][N] cos, sin of (double)angle for the ray end points (computed once per car)
   const double2* ray_cs;   // [16] cos, sin of the ray offsets radians(22.5 i) (nascar_rays.h)
   double* ctl;         // [N][4] rule-driver state of the device action sources (policy_car)
+  float* vhist;        // [VH_RING][N] speed history for validate_performance, or null (nascar_set_perf_history)
   // block map shortcuts (prepare()): map_identity = blk_env[s] is s (< E) or -1, one_track >= 0 = every
   // block's track; they spare each kernel's first dependent load
   int map_identity, one_track;
@@ -1554,7 +1555,10 @@ __device__ __forceinline__ void logic_load(const Params& P, int env, int car, in
     car_load_body(P, n, c);
     car_load_logic(P, n, c);
     car_reload_tyres(P, n, c);
-    if (car == 0) { pend_in = P.env_i32[E_PENDING * P.E + env]; reason_in = P.env_i32[E_REASON * P.E + env]; }
+    if (car == 0) {   // reason_in bit 8: the env was never reset (E_CREATED == 0)
+      pend_in = P.env_i32[E_PENDING * P.E + env];
+      reason_in = P.env_i32[E_REASON * P.E + env] | (P.env_i32[E_CREATED * P.E + env] == 0 ? 0x100 : 0);
+    }
     sim = P.env_time[env];
   }
 }
@@ -1677,7 +1681,7 @@ __device__ __forceinline__ void logic_run(const Params& P, const TrackDev& T, co
   if (env >= 0 && car == 0) {
     const double st = sim + P.dt_d;   // env_time is written only here
     P.env_time[env] = st;
-    int ndis = 0, active = 0, below = 0, term = 0, trunc = 0, reason = reason_in;
+    int ndis = 0, active = 0, below = 0, term = 0, trunc = 0, reason = reason_in & 0xFF;
     for (int j = 0; j < C; ++j) { ndis += L.dis_final[tid + j]; if (!L.dis_final[tid + j]) { active++; below += L.below[tid + j]; } }
     if (ndis >= C) { term = 1; reason = 1; }
     else if (active > 0 && below == active) { term = 1; reason = 2; }
@@ -1688,7 +1692,9 @@ __device__ __forceinline__ void logic_run(const Params& P, const TrackDev& T, co
     P.env_i32[E_TERMINATED * P.E + env] = term;
     P.env_i32[E_TRUNCATED * P.E + env] = trunc;
     int done = term | trunc;
-    L.envdone[el] = done;
+    // bit 1: the env was never reset (E_CREATED == 0): an auto-reset builds it fresh worlds (read here, before
+    // the barrier, because car 0 sets E_CREATED after its own reset below)
+    L.envdone[el] = done | ((reason_in & 0x100) ? 2 : 0);
     if (env_flags) env_flags[env] = (uint8_t)((term ? EF_TERMINATED : 0) | (trunc ? EF_TRUNCATED : 0) |
                                               ((auto_reset && done) ? EF_RESET : 0) | ((reason & 7) << 4));
   }
@@ -1702,15 +1708,20 @@ __device__ __forceinline__ void logic_run(const Params& P, const TrackDev& T, co
     uint8_t flags = (uint8_t)((c.disabled ? CF_DISABLED : 0) | (c.just_disabled ? CF_JUST_DISABLED : 0) |
                               (collided ? CF_COLLISION : 0) | (lapdone ? CF_LAP : 0) | (c.overflow ? CF_ERROR : 0));
     c.just_disabled = 0;
+    if (P.vhist) {   // Car.update_physics appends |v| at the start of the next step (src/car.py:384-386)
+      const int k = (int)rint((sim + P.dt_d) * 60.0);
+      P.vhist[(size_t)(k % VH_RING) * P.N + n] = vlen(c.v);
+    }
     reward[n] = rew;
     if (car_flags) car_flags[n] = flags;
-    const bool reset_now = auto_reset && L.envdone[el];
+    const bool reset_now = auto_reset && (L.envdone[el] & 1);
     LPROF(6);
     if (terminal_obs) { float* t = terminal_obs + (size_t)n * 38; for (int i = 0; i < 22; ++i) t[i] = o[i]; }
     // sensor pass B: the reset pose of every auto-reset car (its pass-B values overwrite the pass-A
     // ones in obs); cleared for every other car
     if (reset_now) {
-      car_reset(P, c, n, false, S, T);
+      // an env never reset before (E_CREATED == 0) gets fresh worlds, as in reset_kernel
+      car_reset(P, c, n, (L.envdone[el] & 2) != 0, S, T);
       car_obs(c, o);
       set_pose(P, (size_t)P.N + n, c, PM_B_OBS);
     } else {
@@ -1722,6 +1733,7 @@ __device__ __forceinline__ void logic_run(const Params& P, const TrackDev& T, co
     LPROF(7);
     if (reset_now && car == 0) {
       P.env_time[env] = 0.0;
+      P.env_i32[E_CREATED * P.E + env] = 1;
       P.env_i32[E_PENDING * P.E + env] = 0; P.env_i32[E_REASON * P.E + env] = 0;
       P.env_i32[E_TERMINATED * P.E + env] = 0; P.env_i32[E_TRUNCATED * P.E + env] = 0;
     }
@@ -1911,6 +1923,22 @@ __global__ void __launch_bounds__(SBLOCK) info_kernel(Params P, double* info) {
   // CarEnv._calculate_track_progress of the current position (src/car_env.py:1544-1611): the reward pass
   // stores it every step for every car that is not disabled (and reset_car for the start pose)
   o[INFO_PROGRESS] = c.prog_hist;
+  // Car.validate_performance inputs (src/car.py:1060-1098): the last min(k, 600) speeds (sample j = the speed
+  // after j steps; sample 0, after the reset, is 0), their maximum and the position of the first one
+  // >= CAR_TARGET_100KMH_MS in the window; the host turns them into the reference's dict (car_env.py)
+  if (P.vhist) {
+    const int k = (int)rint(P.env_time[env] * 60.0);
+    const int cnt = k < VH_SIZE ? k : VH_SIZE, j0 = k - cnt;
+    float mx = 0.0f; int first = -1;
+    for (int j = j0; j < k; ++j) {
+      const float v = j == 0 ? 0.0f : P.vhist[(size_t)(j % VH_RING) * P.N + n];
+      if (j == j0 || v > mx) mx = v;
+      if (first < 0 && (double)v >= 100.0 * 0.277778) first = j - j0;
+    }
+    o[INFO_PERF_COUNT] = cnt; o[INFO_PERF_MAX] = cnt ? (double)mx : 0.0; o[INFO_PERF_FIRST] = first;
+  } else {
+    o[INFO_PERF_COUNT] = -1.0; o[INFO_PERF_MAX] = 0.0; o[INFO_PERF_FIRST] = -1.0;
+  }
 }
 
 // ------------------------------------------------------------------ synthetic action sources (bench)
@@ -2194,6 +2222,8 @@ struct NascarHandle {
   int* d_blk_track = nullptr; int* d_blk_env = nullptr; int nblocks = 0;
   int map_identity = 0, one_track = -1;   // Params shortcuts of the block map (prepare)
   std::vector<int> env_track;
+  std::vector<int> pending_track;   // nascar_set_env_tracks, applied per env by its next nascar_reset
+  float* d_vhist = nullptr;  // [VH_RING][N] speed history (nascar_set_perf_history), outside the snapshot arena
   double* d_ctl = nullptr;   // rule-driver state for nascar_policy_actions (inside the arena: snapshots keep it)
   float4* d_pose = nullptr;  // [2][N] step/reset -> sensor_kernel hand-off
   double2* d_pose_cs = nullptr;
@@ -2249,6 +2279,7 @@ extern "C" int nascar_create(const NascarConfig* cfg, NascarHandle** out) {
 
 extern "C" void nascar_destroy(NascarHandle* h) {
   if (!h) return;
+  hipFree(h->d_vhist);
   hipFree(h->arena); hipFree(h->d_pose); hipFree(h->d_pose_cs); hipFree(h->d_ray_cs); hipFree(h->d_actor); hipFree(h->d_params);
   for (auto& t : h->tracks) {
     hipFree(t.d_walls); hipFree(t.d_segs); hipFree(t.d_prefix);
@@ -2356,14 +2387,35 @@ extern "C" int nascar_set_env_tracks(NascarHandle* h, const int32_t* env_track) 
   if (!h || !env_track) return fail("null argument");
   for (int e = 0; e < h->E; ++e)
     if (env_track[e] < 0 || env_track[e] >= (int)h->tracks.size()) return fail("env %d: bad track id %d", e, env_track[e]);
-  // an env whose track changes gets fresh physics worlds at its next reset
-  // (CarEnv.reset recreates CarPhysics on a track change, src/car_env.py:375-394)
-  char* created = (char*)h->arena + h->off_ei32 + sizeof(int) * (size_t)E_CREATED * h->E;
-  for (int e = 0; e < h->E; ++e) {
-    if (h->env_track[e] != env_track[e]) HIPCHK(hipMemset(created + sizeof(int) * e, 0, sizeof(int)));
-    h->env_track[e] = env_track[e];
+  // recorded only: an env moves to its new track at its next nascar_reset, with fresh physics worlds (CarEnv.reset
+  // recreates CarPhysics on a track change, src/car_env.py:375-394); until then it keeps stepping on its old track
+  // (its Box2D contacts hold wall indices of that track)
+  h->pending_track.assign(env_track, env_track + h->E);
+  return 0;
+}
+
+// nascar_reset's half of a track change: envs with a pending track that this reset covers switch now (E_CREATED
+// cleared on the stream, so reset_kernel builds them fresh worlds); the block map is rebuilt by prepare()
+static int apply_pending_tracks(NascarHandle* h, const uint8_t* env_mask, void* stream) {
+  if (h->pending_track.empty()) return 0;
+  bool any = false;
+  for (int e = 0; e < h->E && !any; ++e) any = h->pending_track[e] != h->env_track[e];
+  if (!any) { h->pending_track.clear(); return 0; }
+  std::vector<uint8_t> mask(h->E, 1);
+  if (env_mask) {   // device mask: one small synchronous copy, only when a track change is pending
+    HIPCHK(hipMemcpyAsync(mask.data(), env_mask, h->E, hipMemcpyDeviceToHost, (hipStream_t)stream));
+    HIPCHK(hipStreamSynchronize((hipStream_t)stream));
   }
-  h->dirty_tracks = true;
+  int* created = (int*)((char*)h->arena + h->off_ei32) + (size_t)E_CREATED * h->E;
+  bool left = false;
+  for (int e = 0; e < h->E; ++e) {
+    if (h->pending_track[e] == h->env_track[e]) continue;
+    if (!mask[e]) { left = true; continue; }
+    h->env_track[e] = h->pending_track[e];
+    HIPCHK(hipMemsetAsync(created + e, 0, sizeof(int), (hipStream_t)stream));
+    h->dirty_tracks = true;
+  }
+  if (!left) h->pending_track.clear();
   return 0;
 }
 
@@ -2421,6 +2473,7 @@ static Params make_params(NascarHandle* h) {
   P.blk_track = h->d_blk_track; P.blk_env = h->d_blk_env; P.tracks = h->d_tracks;
   P.map_identity = h->map_identity; P.one_track = h->one_track;
   P.pose = h->d_pose; P.pose_cs = h->d_pose_cs; P.ray_cs = h->d_ray_cs; P.ctl = h->d_ctl;
+  P.vhist = h->d_vhist;
   return P;
 }
 
@@ -2453,6 +2506,7 @@ static void launch_sensors(NascarHandle* h, const Params& P, float* obs, float* 
 
 extern "C" int nascar_reset(NascarHandle* h, const uint8_t* env_mask, float* obs, void* stream) {
   if (!h || !obs) return fail("null argument");
+  if (apply_pending_tracks(h, env_mask, stream)) return -1;
   if (prepare(h)) return -1;
   Params P = make_params(h);
   hipLaunchKernelGGL(reset_kernel, dim3(h->nblocks), dim3(SBLOCK), 0, (hipStream_t)stream, P, env_mask, obs);
@@ -2511,6 +2565,16 @@ extern "C" int nascar_get_info(NascarHandle* h, double* info, void* stream) {
   Params P = make_params(h);
   hipLaunchKernelGGL(info_kernel, dim3(h->nblocks), dim3(SBLOCK), 0, (hipStream_t)stream, P, info);
   HIPCHK(hipGetLastError());
+  return 0;
+}
+
+extern "C" int nascar_set_perf_history(NascarHandle* h, int32_t enable, void* stream) {
+  if (!h) return fail("null argument");
+  if (!enable) { if (h->d_vhist) { HIPCHK(hipStreamSynchronize((hipStream_t)stream)); hipFree(h->d_vhist); h->d_vhist = nullptr; } return 0; }
+  if (h->d_vhist) return 0;
+  const size_t bytes = sizeof(float) * (size_t)VH_RING * h->N;
+  HIPCHK(hipMalloc(&h->d_vhist, bytes));
+  HIPCHK(hipMemsetAsync(h->d_vhist, 0, bytes, (hipStream_t)stream));
   return 0;
 }
 

@@ -58,8 +58,16 @@ enum { E_CREATED, E_PENDING, E_REASON, E_TERMINATED, E_TRUNCATED, N_EI32 };
 enum {
   INFO_X, INFO_Y, INFO_VX, INFO_VY, INFO_ANGLE, INFO_OMEGA, INFO_SPEED, INFO_LAP_COUNT, INFO_LAST_LAP,
   INFO_BEST_LAP, INFO_IS_TIMING, INFO_CUR_LAP_TIME, INFO_LAP_DIST, INFO_HAS_CROSSED, INFO_DISABLED,
-  INFO_CUM_REWARD, INFO_CUM_IMPACT, INFO_ON_TRACK, INFO_RPM, INFO_SIM_TIME, INFO_NCT, INFO_ERROR, INFO_PROGRESS, N_INFO
+  INFO_CUM_REWARD, INFO_CUM_IMPACT, INFO_ON_TRACK, INFO_RPM, INFO_SIM_TIME, INFO_NCT, INFO_ERROR, INFO_PROGRESS,
+  INFO_PERF_COUNT, INFO_PERF_MAX, INFO_PERF_FIRST, N_INFO
 };
+
+// Car.velocity_history (src/car.py:173, 384-386; deque(maxlen=VELOCITY_HISTORY_SIZE = 600)) for
+// Car.validate_performance (src/car.py:1060-1098): per car, the body speed after each step, ring slot
+// (steps since reset) % VH_RING, layout [VH_RING][N] float32 (b2Vec2::Length is float32).  Optional
+// (nascar_set_perf_history); VH_RING > 600 so a step's write never lands in the window it is read with.
+#define VH_SIZE 600
+#define VH_RING 640
 
 // car flag bits (nascar_step car_flags output)
 enum { CF_DISABLED = 1, CF_JUST_DISABLED = 2, CF_COLLISION = 4, CF_LAP = 8, CF_ERROR = 128 };

@@ -47,7 +47,7 @@ class ObsGather:
         buf[n * (OBS_DIM + 2):n * (OBS_DIM + 2) + e].copy_(env_flags.reshape(-1))
 
     def _gather(self, buf):
-        if self.world == 1:
+        if not dist.is_initialized():
             self.recv[0].copy_(buf)
             return
         parts = list(self.recv.unbind(0)) if self.rank == self.dst else None

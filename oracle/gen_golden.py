@@ -426,6 +426,13 @@ def car_info_row(ci):
             g(ci.get("on_track")), g(ci.get("disabled")), g(ci.get("cumulative_reward")), g(ci.get("cumulative_impact_force"))]
 
 
+PERF_KEYS = ["current_max_speed", "estimated_0_100_time", "performance_valid"]   # Car.validate_performance
+
+
+def perf_row(p):
+    return [float(p.get(k, np.nan)) for k in PERF_KEYS]
+
+
 REASONS = {None: 0, "all_cars_disabled": 1, "time_limit": 3, "truncated": 4}
 
 
@@ -488,7 +495,8 @@ def run_scenario(ref, name, track, C, steps, policy, reset_on_lap=False, reset_a
         obs, info = env.reset()
     rng = np.random.default_rng(seed)
     drivers = [RuleDriver(ref) for _ in range(C)]
-    rec = {k: [] for k in ["actions", "obs", "rewards", "terminated", "truncated", "reason", "sim_time", "info", "reset"]}
+    rec = {k: [] for k in ["actions", "obs", "rewards", "terminated", "truncated", "reason", "sim_time", "info", "reset",
+                           "perf", "physics"]}
     obs = obs.reshape(C, 38)
     rec["obs0"] = obs.copy()
     for k in range(steps):
@@ -519,6 +527,9 @@ def run_scenario(ref, name, track, C, steps, policy, reset_on_lap=False, reset_a
         rec["reason"].append(reason_code(env.termination_reason))
         rec["sim_time"].append(info["simulation_time"])
         rec["info"].append([car_info_row(ci) for ci in info["cars"]])
+        rec["perf"].append([perf_row(ci.get("performance", {})) for ci in info["cars"]])
+        rec["physics"].append([[float(p["physics_steps"]), float(p["simulation_time"]), float(p["average_fps"]),
+                                float(p["bodies_in_world"])] for p in info["physics"]])
     sys.path.remove(ref)
     n = len(rec["obs"])
     keep = np.arange(n) if n <= 4000 else np.unique(np.r_[np.arange(0, n, 50), np.arange(n - 20, n)])
@@ -529,7 +540,8 @@ def run_scenario(ref, name, track, C, steps, policy, reset_on_lap=False, reset_a
                rewards=np.array(rec["rewards"], np.float32), terminated=np.array(rec["terminated"]),
                truncated=np.array(rec["truncated"]), reason=np.array(rec["reason"], np.int32),
                sim_time=np.array(rec["sim_time"]), info=np.array(rec["info"], np.float64)[keep],
-               reset=np.array(rec["reset"]), obs0=rec["obs0"])
+               reset=np.array(rec["reset"]), obs0=rec["obs0"],
+               perf=np.array(rec["perf"], np.float64)[keep], physics=np.array(rec["physics"], np.float64)[keep])
     return out
 
 

@@ -71,7 +71,8 @@ def _gather_worker(rank, world, port, q):
         g.push(obs, rew, cf, ef)
         r = g.received()
         if r is not None:
-            got.append({k: v.clone() for k, v in r.items()})
+            # numpy copies: tensors in an mp queue travel by shared-memory handle, which dies with this process
+            got.append({k: v.numpy().copy() for k, v in r.items()})
     q.put((rank, got))
     dist.destroy_process_group()
 
@@ -93,7 +94,7 @@ def test_obs_gather_world2():
     for step, r in enumerate(res[0]):
         assert r["obs"].shape == (2, 3, 2, 38)
         for rank in range(2):
-            assert torch.equal(r["obs"][rank], torch.full((3, 2, 38), 100.0 * rank + step) + torch.arange(38.0))
-            assert torch.equal(r["reward"][rank], torch.full((3, 2), -0.05 * (rank + 1) + step))
-            assert torch.equal(r["car_flags"][rank], torch.full((3, 2), 4 * rank + step, dtype=torch.uint8))
+            assert torch.equal(torch.from_numpy(r["obs"][rank]), torch.full((3, 2, 38), 100.0 * rank + step) + torch.arange(38.0))
+            assert torch.equal(torch.from_numpy(r["reward"][rank]), torch.full((3, 2), -0.05 * (rank + 1) + step))
+            assert torch.equal(torch.from_numpy(r["car_flags"][rank]), torch.full((3, 2), 4 * rank + step, dtype=torch.uint8))
             assert r["env_flags"][rank].tolist() == [rank, step, 8 + rank]

@@ -43,11 +43,22 @@ def _replay_carenv(name, steps=None):
         assert np.array_equal(np.atleast_1d(rew), d["rewards"][k]), k
         if keep is None or k in keep:
             assert np.array_equal(obs.reshape(C, 38), d["obs"][j]), k
+            if "perf" in d:   # Car.validate_performance and CarPhysics.get_performance_stats, exact
+                for i, c in enumerate(info["cars"]):
+                    p = c["performance"]
+                    got = [p["current_max_speed"], p["estimated_0_100_time"], float(p["performance_valid"])]
+                    assert got == d["perf"][j, i].tolist(), (k, i, got, d["perf"][j, i])
+                    ph = info["physics"][i]
+                    got = [float(ph["physics_steps"]), ph["simulation_time"], ph["average_fps"], float(ph["bodies_in_world"])]
+                    assert got == d["physics"][j, i].tolist(), (k, i, got, d["physics"][j, i])
             j += 1
         lap = [c["lap_timing"]["lap_count"] for c in info["cars"]]
         assert lap == d["info"][k, :, 0].astype(int).tolist(), k
         assert [c["disabled"] for c in info["cars"]] == (d["info"][k, :, 8] != 0).tolist(), k
         assert env.disabled_cars == {i for i in range(C) if d["info"][k, i, 8] != 0}
+        if k == 5:   # SubprocVecEnv workers pickle every step's info
+            import pickle
+            assert pickle.loads(pickle.dumps(info)) == info
     env.close()
 
 

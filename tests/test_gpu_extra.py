@@ -1,0 +1,109 @@
+"""GPU tests for the boundary's less common paths: the RCCL obs gather (cfg4 single-learner layout), a
+mixed-track launch against the oracle per env (cfg5 shape), and track changes that wait for the env's reset."""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+from golden_replay import TRACKS
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+
+
+def _actions(rng, E, C, k):
+    a = rng.uniform(-1, 1, (E, C, 2)).astype(np.float32)
+    a[: E // 2, :, 0] = np.abs(a[: E // 2, :, 0])          # half the envs mostly throttle -> wall impacts
+    a[:, :, 1] *= 0.5 if k % 50 < 25 else 1.0
+    return a
+
+
+def test_obs_gather_rccl_world1():
+    """ObsGather over RCCL (torch.distributed "nccl", world size 1, side stream): the gathered record of every
+    step equals the env's own outputs bit for bit."""
+    import torch.distributed as dist
+    from nascargymnasium_amd.batched import BatchedCarEnv
+    from nascargymnasium_amd.gather import ObsGather
+    s = socket.socket(); s.bind(("127.0.0.1", 0)); port = s.getsockname()[1]; s.close()
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
+    try:
+        E, C = 64, 4
+        env = BatchedCarEnv(E, C, os.path.join(TRACKS, "daytona.track"), device="cuda:0")
+        g = ObsGather(E, C, env.device)
+        env.reset()
+        for k in range(40):
+            env.launch_step(env.policy_actions(3, seed=1, step=k).clone(), auto_reset=True)
+            g.push(env.obs, env.reward, env.car_flags, env.env_flags)
+            g.wait()
+            r = g.received()
+            assert torch.equal(r["obs"][0], env.obs) and torch.equal(r["reward"][0], env.reward)
+            assert torch.equal(r["car_flags"][0], env.car_flags) and torch.equal(r["env_flags"][0], env.env_flags)
+        env.close()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_mixed_tracks_vs_oracle():
+    """cfg5 shape: 256 envs, env e on track e mod 8, one launch; every env equals the oracle on its own track
+    (obs, rewards, disabled flags, done flags) every step."""
+    from nascargymnasium_amd.batched import BatchedCarEnv
+    from oracle_lib import OracleEnv
+    tracks = sorted(f for f in os.listdir(TRACKS) if f.endswith(".track"))
+    E, C, S = 256, 2, 400
+    env = BatchedCarEnv(E, C, [os.path.join(TRACKS, tracks[e % 8]) for e in range(E)], device="cuda:0")
+    groups = [[e for e in range(E) if e % 8 == t] for t in range(8)]
+    orcs = [OracleEnv(os.path.join(TRACKS, tracks[t]), len(groups[t]), C) for t in range(8)]
+    g = env.reset().cpu().numpy()
+    for t in range(8):
+        assert np.array_equal(g[groups[t]], orcs[t].reset()[0]), tracks[t]
+    rng = np.random.default_rng(11)
+    contacts = 0
+    for k in range(S):
+        a = _actions(rng, E, C, k)
+        env.step(torch.from_numpy(a).cuda(), auto_reset=False)
+        go, gr = env.obs.cpu().numpy(), env.reward.cpu().numpy()
+        gcf, gef = env.car_flags.cpu().numpy(), env.env_flags.cpu().numpy()
+        contacts += int((gcf & 4).astype(bool).sum())
+        for t in range(8):
+            oo, orw, ocf, oef = orcs[t].step(a[groups[t]])
+            assert np.array_equal(go[groups[t]], oo), (k, tracks[t])
+            assert np.array_equal(gr[groups[t]], orw), (k, tracks[t])
+            assert np.array_equal(gcf[groups[t]] & 1, ocf & 1), (k, tracks[t])
+            assert np.array_equal(gef[groups[t]] & 3 != 0, (oef[:, 0] != 0) | (oef[:, 1] != 0)), (k, tracks[t])
+    assert contacts > 0
+    env.close()
+
+
+def test_track_change_waits_for_reset():
+    """nascar_set_env_tracks takes effect at the env's next reset: until then the env keeps stepping on its old
+    track (its contacts hold that track's wall indices), the reset builds fresh worlds on the new one, and
+    auto-reset afterwards stays on it.  talladega (732 walls) -> martinsville (fewer walls)."""
+    from nascargymnasium_amd.batched import BatchedCarEnv
+    E, C = 12, 3
+    tal, mar = os.path.join(TRACKS, "talladega.track"), os.path.join(TRACKS, "martinsville.track")
+    env = BatchedCarEnv(E, C, tal, device="cuda:0")
+    twin = BatchedCarEnv(E, C, tal, device="cuda:0")
+    fresh = BatchedCarEnv(E, C, mar, device="cuda:0")
+    env.reset(); twin.reset()
+    rng = np.random.default_rng(3)
+    for k in range(400):    # drive into the walls: contact lists fill up
+        a = torch.from_numpy(_actions(rng, E, C, k)).cuda()
+        env.step(a); twin.step(a)
+    assert int(env.info_tensor()[..., env_field("n_contacts")].sum()) > 0
+    env.set_env_tracks([mar] * E)
+    for k in range(100):    # no reset yet: still talladega
+        a = torch.from_numpy(_actions(rng, E, C, k)).cuda()
+        assert torch.equal(env.step(a, auto_reset=True)[0], twin.step(a, auto_reset=True)[0]), k
+    o = env.reset().clone()
+    assert torch.equal(o, fresh.reset())
+    for k in range(700):    # idle half the time -> stuck disables -> auto-resets on the new track
+        a = torch.from_numpy(_actions(rng, E, C, k) * (k % 200 < 100)).cuda()
+        assert torch.equal(env.step(a, auto_reset=True)[0], fresh.step(a, auto_reset=True)[0]), k
+    for x in (env, twin, fresh):
+        x.close()
+
+
+def env_field(name):
+    from nascargymnasium_amd import _lib
+    return _lib.INFO_FIELDS.index(name)

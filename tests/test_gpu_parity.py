@@ -60,12 +60,14 @@ def test_golden_trace_gpu(name):
     d = load(name)
     C = int(d["C"]); E = 4
     env = _env(str(d["track"]), E, C, bool(d["reset_on_lap"]))
+    env.set_perf_history(True)
     obs0 = env.reset().cpu().numpy()
     for e in range(E):
         assert np.array_equal(obs0[e], d["obs0"]), "reset obs"
     keep = set(d["obs_steps"].tolist()) if "obs_steps" in d else None
     fidx = [_lib.INFO_FIELDS.index(f) for _, f in INFO_MAP]
-    O, R, T, TR, RS, I = [], [], [], [], [], []
+    pidx = [_lib.INFO_FIELDS.index(f) for f in ("perf_count", "perf_max_speed", "perf_first_fast", "simulation_time")]
+    O, R, T, TR, RS, I, PF = [], [], [], [], [], [], []
     for k in range(len(d["actions"])):
         if d["reset"][k]:
             o = env.reset().cpu().numpy()
@@ -78,7 +80,9 @@ def test_golden_trace_gpu(name):
             rs = env.termination_reason().cpu().numpy()
         if keep is None or k in keep:
             O.append(o.copy())
-            I.append(env.info_tensor().cpu().numpy()[:, :, fidx])
+            inf = env.info_tensor().cpu().numpy()
+            I.append(inf[:, :, fidx])
+            PF.append(inf[:, :, pidx])
         R.append(r.copy()); T.append(t.copy()); TR.append(tr.copy()); RS.append(rs.copy())
     O, R, T, TR, RS, I = map(np.array, (O, R, T, TR, RS, I))
     gi = d["info"][:, :, [c for c, _ in INFO_MAP]]
@@ -89,6 +93,18 @@ def test_golden_trace_gpu(name):
         assert np.array_equal(T[:, e], d["terminated"]) and np.array_equal(TR[:, e], d["truncated"])
         assert np.array_equal(RS[:, e], d["reason"])
         assert first_mismatch(I[:, e], gi) == -1, f"info diverge at {first_mismatch(I[:, e], gi)}"
+    if "perf" in d:   # Car.validate_performance from the device velocity history (src/car.py:1060-1098), exact
+        from nascargymnasium_amd.car_env import DT, physics_stats, validate_performance
+        for j, rows in enumerate(PF):
+            for e in range(E):
+                for i in range(C):
+                    cnt, mx, first, sim = rows[e, i]
+                    p = validate_performance(int(cnt), float(mx), int(first))
+                    got = [p["current_max_speed"], p["estimated_0_100_time"], float(p["performance_valid"])]
+                    assert got == d["perf"][j, i].tolist(), (j, e, i, got, d["perf"][j, i])
+                    ph = physics_stats(int(round(sim / DT)), int(d["physics"][j, i, 3]))
+                    got = [float(ph["physics_steps"]), ph["simulation_time"], ph["average_fps"], float(ph["bodies_in_world"])]
+                    assert got == d["physics"][j, i].tolist(), (j, e, i, got, d["physics"][j, i])
     env.close()
 
 

@@ -79,3 +79,43 @@ def test_env_trace_bit_exact(name):
     assert np.array_equal(RS, d["reason"])
     gi = d["info"][:, :, [c for c, _ in INFO_MAP]]
     assert first_mismatch(I, gi) == -1, f"info diverge at step {first_mismatch(I, gi)}"
+
+
+@pytest.mark.parametrize("name", [s for s in scenarios() if "perf" in load(s)])
+def test_performance_info_bit_exact(name):
+    """Car.validate_performance / CarPhysics.get_performance_stats (src/car.py:1060-1098, src/car_physics.py:573-592)
+    restated on the host (nascargymnasium_amd.car_env) from a window summary of the speed history -- the same
+    summary the device's info_kernel reports -- equal the reference's dicts recorded in the golden trace."""
+    from collections import deque
+    from nascargymnasium_amd.car_env import DT, physics_stats, validate_performance
+    d = load(name)
+    C = int(d["C"])
+    env = OracleEnv(os.path.join(TRACKS, str(d["track"])), 1, C, bool(d["reset_on_lap"]))
+    env.reset()
+    hist = [deque(maxlen=600) for _ in range(C)]
+    speed = [0.0] * C
+    keep = set(d["obs_steps"].tolist()) if "obs_steps" in d else None
+    j, steps = 0, 0
+    for k in range(len(d["actions"])):
+        if d["reset"][k]:
+            env.reset(0)
+            hist = [deque(maxlen=600) for _ in range(C)]
+            speed, steps = [0.0] * C, 0
+        else:
+            for i in range(C):
+                hist[i].append(speed[i])          # Car.update_physics: |v| at the start of the step
+            env.step(continuous_actions(d, k)[None])
+            speed = [env.car_info(i)["speed"] for i in range(C)]
+            steps += 1
+        if keep is None or k in keep:
+            for i in range(C):
+                h = list(hist[i])
+                first = next((n for n, v in enumerate(h) if v >= 100.0 * 0.277778), -1)
+                p = validate_performance(len(h), max(h) if h else 0.0, first)
+                got = [p["current_max_speed"], p["estimated_0_100_time"], float(p["performance_valid"])]
+                assert got == d["perf"][j, i].tolist(), (k, i, got, d["perf"][j, i])
+                ph = physics_stats(steps, int(d["physics"][j, i, 3]))
+                got = [float(ph["physics_steps"]), ph["simulation_time"], ph["average_fps"], float(ph["bodies_in_world"])]
+                assert got == d["physics"][j, i].tolist(), (k, i, got, d["physics"][j, i])
+            j += 1
+    assert j == len(d["perf"])

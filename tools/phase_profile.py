@@ -140,6 +140,15 @@ def main():
                     iso = f", isolated single-lane TOI {cp[i, 13] / cp[i, 9]:.0f} cycles/call" if cp[i, 9] else ""
                     print(f"    car {i} solve_toi cycles: TOI calls {cp[i, 10]} (GJK {cp[i, 14]}, separation fn {cp[i, 15]}), "
                           f"island solves {cp[i, 11]}, event contact updates {cp[i, 12]}{iso}")
+            ev = np.argsort(-cp[:, 4])[:12]
+            print("  cars with the most TOI events: car, wave b2 cycles, events, TOI solved, contacts at start, "
+                  "TOI-call cycles, island-solve cycles, event contact-update cycles, outer iterations")
+            for i in ev:
+                if cp[i, 4]:
+                    print("   ", i, cp[i, 0], cp[i, 4], cp[i, 2], cp[i, 1], cp[i, 10], cp[i, 11], cp[i, 12], cp[i, 6])
+            evw = cp[cp[:, 4] > 0, 0]
+            if len(evw):
+                print(f"  b2 cycles of cars with TOI events: mean {evw.mean():.0f}, max {evw.max()}; cars with events {len(evw)}")
             m9 = cp[:, 9] > 0
             if m9.any():
                 print(f"  isolated single-lane TOI: {cp[m9, 13].sum() / cp[m9, 9].sum():.0f} cycles/call over {cp[m9, 9].sum()} calls")
@@ -174,6 +183,9 @@ def main():
             ncar = a.envs * a.cars
             print(f"model counters per car-step: TOI solved {cb[4] / ncar:.3f}, TOI culled {cb[5] / ncar:.3f}, "
                   f"contact updates {cb[6] / ncar:.3f}, TOI events {cb[7] / ncar:.4f}")
+        ck = b[2 * NW * 16 + 16:2 * NW * 16 + 18]
+        if ck[0]:
+            print(f"TOI cull check: culled TOIs re-run {ck[0]}, of which TOUCHING (cull violations) {ck[1]}")
         if cb[0]:
             print(f"ray_sensor_kernel: rays {cb[0]}, fallback rays {cb[1]} ({100 * cb[1] / cb[0]:.2f}%), "
                   f"list entries per ray {cb[3] / max(1, cb[0] - cb[1]):.2f}, walked {cb[2] / max(1, cb[0] - cb[1]):.2f}")
