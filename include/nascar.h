@@ -49,7 +49,8 @@ int nascar_add_track(NascarHandle* h, const double* segments, int32_t nseg, doub
                      const double* walls, int32_t nwall);
 /* per-env track ids (host array of E ints); envs are grouped per track into workgroups.  A changed id takes
  * effect at that env's next nascar_reset (fresh physics worlds on the new track, as CarEnv.reset recreates
- * CarPhysics, src/car_env.py:375-394); until then the env keeps stepping on its old track. */
+ * CarPhysics, src/car_env.py:375-394); until then the env keeps stepping on its old track.  On a handle that has
+ * not been reset, stepped or restored yet the ids apply at once. */
 int nascar_set_env_tracks(NascarHandle* h, const int32_t* env_track);
 
 /* CarEnv.reset (src/car_env.py:316-535) for the envs whose env_mask[e] != 0 (device uint8[E];
@@ -112,6 +113,10 @@ int nascar_policy_actions(NascarHandle* h, int32_t policy, uint64_t seed, int64_
  * (game/control/sac_control_class.py:48-115) with one fused bf16-MFMA kernel. */
 int nascar_set_actor(NascarHandle* h, const float* w1, const float* b1, const float* w2, const float* b2,
                      const float* w3, const float* b3, int32_t obs_dim, int32_t hidden, int32_t act_dim);
+/* Actor arithmetic for policy 2 and nascar_actor_forward: 1 (default) = float32 throughout (the reference's
+ * model.predict precision; <= 1e-5 on the reference's sac_1235 checkpoint, tests/test_gpu_actor.py), 0 = the
+ * bf16-operand MFMA kernel (fp32 accumulation; ~5x faster, max |delta action| 0.40 on sac_1235). */
+int nascar_set_actor_precision(NascarHandle* h, int32_t fp32);
 /* The loaded actor on any device batch: obs [n][38] float32 -> actions [n][2] float32 (both 8-byte aligned). */
 int nascar_actor_forward(NascarHandle* h, const float* obs, int32_t n, float* actions, void* stream);
 

@@ -91,6 +91,8 @@ def lib():
     fp = ctypes.POINTER(ctypes.c_float)
     L.nascar_set_actor.argtypes = [vp, fp, fp, fp, fp, fp, fp, i32, i32, i32]
     L.nascar_set_actor.restype = ctypes.c_int
+    L.nascar_set_actor_precision.argtypes = [vp, i32]
+    L.nascar_set_actor_precision.restype = ctypes.c_int
     L.nascar_actor_forward.argtypes = [vp, vp, i32, vp, vp]
     L.nascar_actor_forward.restype = ctypes.c_int
     L.nascar_debug_sincosf.argtypes = [vp, vp, vp, i32, vp]
@@ -103,7 +105,7 @@ def lib():
 
 EXPORTED = ["nascar_create", "nascar_destroy", "nascar_last_error", "nascar_add_track", "nascar_set_env_tracks",
             "nascar_reset", "nascar_step", "nascar_rollout", "nascar_get_info", "nascar_set_perf_history", "nascar_state_bytes", "nascar_get_state",
-            "nascar_set_state", "nascar_policy_actions", "nascar_set_actor", "nascar_actor_forward",
+            "nascar_set_state", "nascar_policy_actions", "nascar_set_actor", "nascar_set_actor_precision", "nascar_actor_forward",
             "nascar_debug_sincosf", "nascar_debug_sensors"]
 
 

@@ -167,12 +167,18 @@ class BatchedCarEnv:
     def termination_reason(self) -> torch.Tensor:
         return (self.env_flags >> 4) & 7
 
-    def set_actor(self, weights):
-        """Load an SB3 SAC MlpPolicy actor: a dict from nascargymnasium_amd.policy.load_sb3_actor / random_actor."""
+    def set_actor(self, weights, precision: str = "fp32"):
+        """Load an SB3 SAC MlpPolicy actor: a dict from nascargymnasium_amd.policy.load_sb3_actor / random_actor.
+        precision "fp32" (default): float32 throughout, the reference's model.predict precision (<= 1e-5 on the
+        reference's sac_1235 checkpoint); "bf16": the MFMA kernel (bf16 operands, fp32 accumulation), ~5x faster but
+        NOT faithful for trained policies (max |delta action| 0.40 on sac_1235)."""
         from .policy import actor_arrays
+        if precision not in ("bf16", "fp32"):
+            raise ValueError("precision must be 'bf16' or 'fp32'")
         arrs = actor_arrays(weights)
         fp = ctypes.POINTER(ctypes.c_float)
         _lib.check(self.L.nascar_set_actor(self.h, *[a.ctypes.data_as(fp) for a in arrs], 38, 256, 2))
+        _lib.check(self.L.nascar_set_actor_precision(self.h, int(precision == "fp32")))
         self._actor_arrays = arrs
 
     def actor_forward(self, obs: torch.Tensor) -> torch.Tensor:

@@ -221,4 +221,82 @@ __global__ void __launch_bounds__(64 * ACT_WAVES) __attribute__((amdgpu_waves_pe
   (void)ntiles_done;
 }
 
+// ------------------------------------------------------------------ reference-precision (fp32) actor
+// The same SB3 MlpPolicy actor in float32 throughout (fp32 FMAs, fp32 tanh): the precision of the reference's
+// model.predict (PyTorch fp32), up to summation order -- |delta action| ~1e-6 against a PyTorch fp32 forward.
+// One 256-thread workgroup per 32-observation tile: thread t owns hidden unit t for the tile's 32 rows (32
+// accumulators), the tile's observations / ReLU'd activations sit in LDS and are read as broadcasts, the
+// weights are read transposed ([k][unit], one coalesced 1 KB row per k, L2-resident), layer 3 on 64 lanes.
+// VALU-bound: 151 kFLOP per observation (~2x the bf16 MFMA kernel's time at the fp32 vector peak).
+struct ActorF32 {
+  const float* w1t;   // [38][256]  W1 transposed
+  const float* b1;    // [256]
+  const float* w2t;   // [256][256] W2 transposed
+  const float* b2;    // [256]
+  const float* w3;    // [2][256]   mu.weight
+  const float* b3;    // [2]
+};
+#define AF_TILE 32
+__global__ void __launch_bounds__(256) actor_fp32_kernel(int N, const float* __restrict__ obs, float* __restrict__ act,
+                                                         ActorF32 A) {
+  __shared__ float4 xs[ACT_OBS][AF_TILE / 4];   // observations, [feature][row]
+  __shared__ float4 hs[ACT_H][AF_TILE / 4];     // relu(H1) then relu(H2), [unit][row]
+  const int t = threadIdx.x;
+  const float b1 = A.b1[t], b2 = A.b2[t];
+  for (int tile = blockIdx.x; tile * AF_TILE < N; tile += gridDim.x) {
+    const int row0 = tile * AF_TILE;
+    float* xf = (float*)xs;
+    for (int i = t; i < AF_TILE * ACT_OBS; i += 256) {
+      const int o = i / ACT_OBS, k = i - o * ACT_OBS;
+      xf[k * AF_TILE + o] = row0 + o < N ? obs[(size_t)row0 * ACT_OBS + i] : 0.0f;
+    }
+    __syncthreads();
+    float acc[AF_TILE];
+#pragma unroll
+    for (int o = 0; o < AF_TILE; ++o) acc[o] = 0.0f;
+#pragma unroll 2
+    for (int k = 0; k < ACT_OBS; ++k) {
+      const float w = A.w1t[k * ACT_H + t];
+#pragma unroll
+      for (int q = 0; q < AF_TILE / 4; ++q) {
+        const float4 x = xs[k][q];
+        acc[4 * q] = fmaf(x.x, w, acc[4 * q]); acc[4 * q + 1] = fmaf(x.y, w, acc[4 * q + 1]);
+        acc[4 * q + 2] = fmaf(x.z, w, acc[4 * q + 2]); acc[4 * q + 3] = fmaf(x.w, w, acc[4 * q + 3]);
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < AF_TILE / 4; ++q)
+      hs[t][q] = make_float4(fmaxf(acc[4 * q] + b1, 0.0f), fmaxf(acc[4 * q + 1] + b1, 0.0f),
+                             fmaxf(acc[4 * q + 2] + b1, 0.0f), fmaxf(acc[4 * q + 3] + b1, 0.0f));
+    __syncthreads();
+#pragma unroll
+    for (int o = 0; o < AF_TILE; ++o) acc[o] = 0.0f;
+#pragma unroll 4
+    for (int k = 0; k < ACT_H; ++k) {
+      const float w = A.w2t[k * ACT_H + t];
+#pragma unroll
+      for (int q = 0; q < AF_TILE / 4; ++q) {
+        const float4 x = hs[k][q];
+        acc[4 * q] = fmaf(x.x, w, acc[4 * q]); acc[4 * q + 1] = fmaf(x.y, w, acc[4 * q + 1]);
+        acc[4 * q + 2] = fmaf(x.z, w, acc[4 * q + 2]); acc[4 * q + 3] = fmaf(x.w, w, acc[4 * q + 3]);
+      }
+    }
+    __syncthreads();   // every lane has read relu(H1)
+#pragma unroll
+    for (int q = 0; q < AF_TILE / 4; ++q)
+      hs[t][q] = make_float4(fmaxf(acc[4 * q] + b2, 0.0f), fmaxf(acc[4 * q + 1] + b2, 0.0f),
+                             fmaxf(acc[4 * q + 2] + b2, 0.0f), fmaxf(acc[4 * q + 3] + b2, 0.0f));
+    __syncthreads();
+    if (t < 2 * AF_TILE) {
+      const int o = t >> 1, i = t & 1;
+      const float* hf = (const float*)hs;
+      float m = 0.0f;
+      for (int k = 0; k < ACT_H; ++k) m = fmaf(A.w3[i * ACT_H + k], hf[k * AF_TILE + o], m);
+      const float a = tanhf(m + A.b3[i]);
+      if (row0 + o < N) act[2 * (size_t)(row0 + o) + i] = -1.0f + ((0.5f * (a + 1.0f)) * 2.0f);   // unscale_action
+    }
+    __syncthreads();   // xs / hs are reused by the next tile
+  }
+}
+
 }  // namespace nascar

@@ -1050,10 +1050,10 @@ __device__ __forceinline__ void sweep_normalize(Sweep& s) {
 enum { SF_POINTS, SF_FACEA, SF_FACEB };
 // body B (the wall) is static in every TOI here: its sweep transforms go through sweep_xf_static with qB
 struct SepFn { Sweep sA, sB; Rot qB; int type; V2 lp, axis; };
+// xfA / xfB: the sweeps' transforms at t1 (the caller's, computed once per b2TimeOfImpact iteration)
 __device__ inline void sep_init(SepFn& f, const SCache& cache, const Poly* pA, const Sweep& sA, const Poly* pB, const Sweep& sB,
-                                Rot qB, float t1) {
+                                Rot qB, Xf xfA, Xf xfB) {
   f.sA = sA; f.sB = sB; f.qB = qB;
-  Xf xfA = sweep_xf(f.sA, t1), xfB = sweep_xf_static(f.sB, t1, qB);
   if (cache.count == 1) {
     f.type = SF_POINTS;
     V2 pointA = xmul(xfA, pv(pA, cache.iA0)), pointB = xmul(xfB, pv(pB, cache.iB0));
@@ -1082,8 +1082,8 @@ __device__ inline void sep_init(SepFn& f, const SCache& cache, const Poly* pA, c
     if (s < 0.0f) f.axis = vneg(f.axis);
   }
 }
-__device__ inline float sep_find_min(const SepFn& f, const Poly* pA, const Poly* pB, int* iA, int* iB, float t) {
-  Xf xfA = sweep_xf(f.sA, t), xfB = sweep_xf_static(f.sB, t, f.qB);
+// b2SeparationFunction::FindMinSeparation / Evaluate on the sweeps' transforms at t (xfA, xfB)
+__device__ inline float sep_find_min(const SepFn& f, const Poly* pA, const Poly* pB, int* iA, int* iB, Xf xfA, Xf xfB) {
   if (f.type == SF_POINTS) {
     V2 axisA = rmulT(xfA.q, f.axis), axisB = rmulT(xfB.q, vneg(f.axis));
     *iA = support(pA, axisA); *iB = support(pB, axisB);
@@ -1103,8 +1103,7 @@ __device__ inline float sep_find_min(const SepFn& f, const Poly* pA, const Poly*
     return vdot(vsub(pointA, pointB), normal);
   }
 }
-__device__ inline float sep_eval(const SepFn& f, const Poly* pA, const Poly* pB, int iA, int iB, float t) {
-  Xf xfA = sweep_xf(f.sA, t), xfB = sweep_xf_static(f.sB, t, f.qB);
+__device__ inline float sep_eval(const SepFn& f, const Poly* pA, const Poly* pB, int iA, int iB, Xf xfA, Xf xfB) {
   if (f.type == SF_POINTS) {
     V2 pointA = xmul(xfA, pv(pA, iA)), pointB = xmul(xfB, pv(pB, iB));
     return vdot(vsub(pointB, pointA), f.axis);
@@ -1131,11 +1130,11 @@ __device__ inline float time_of_impact(int* state, const Poly* pA, const Sweep& 
   int iter = 0;
   SCache cache; cache.count = 0; cache.metric = 0.0f;
   cache.iA0 = cache.iA1 = cache.iA2 = cache.iB0 = cache.iB1 = cache.iB2 = 0;
+  Xf xfA = sweep_xf(sA, t1), xfB = sweep_xf_static(sB, t1, qB);   // at t1; carried over when t1 takes t2's value
   for (;;) {
 #ifdef NASCAR_PROFILE
     const unsigned long long tg0 = __builtin_amdgcn_s_memtime();
 #endif
-    Xf xfA = sweep_xf(sA, t1), xfB = sweep_xf_static(sB, t1, qB);
     float distance = gjk_distance(cache, pA, xfA, pB, xfB);
 #ifdef NASCAR_PROFILE
     if (prof_cyc) prof_cyc[0] += __builtin_amdgcn_s_memtime() - tg0;
@@ -1144,16 +1143,19 @@ __device__ inline float time_of_impact(int* state, const Poly* pA, const Sweep& 
     if (distance <= 0.0f) { *state = TOI_OVERLAPPED; out_t = 0.0f; break; }
     if (distance < target + tolerance) { *state = TOI_TOUCHING; out_t = t1; break; }
     SepFn fcn;
-    sep_init(fcn, cache, pA, sA, pB, sB, qB, t1);
+    sep_init(fcn, cache, pA, sA, pB, sB, qB, xfA, xfB);
     bool done = false;
     float t2 = tMax;
+    // the sweeps' transforms at t2: b2TimeOfImpact re-derives them from t2 for FindMinSeparation; the root
+    // finder's last Evaluate was at the same t2 (t2 = t), so its transforms are reused (identical values)
+    Xf xfA2 = sweep_xf(sA, t2), xfB2 = sweep_xf_static(sB, t2, qB);
     int pushBackIter = 0;
     for (;;) {
       int indexA, indexB;
-      float s2 = sep_find_min(fcn, pA, pB, &indexA, &indexB, t2);
+      float s2 = sep_find_min(fcn, pA, pB, &indexA, &indexB, xfA2, xfB2);
       if (s2 > target + tolerance) { *state = TOI_SEPARATED; out_t = tMax; done = true; break; }
-      if (s2 > target - tolerance) { t1 = t2; break; }
-      float s1 = sep_eval(fcn, pA, pB, indexA, indexB, t1);
+      if (s2 > target - tolerance) { t1 = t2; xfA = xfA2; xfB = xfB2; break; }
+      float s1 = sep_eval(fcn, pA, pB, indexA, indexB, xfA, xfB);   // at t1
       if (s1 < target - tolerance) { *state = TOI_FAILED; out_t = t1; done = true; break; }
       if (s1 <= target + tolerance) { *state = TOI_TOUCHING; out_t = t1; done = true; break; }
       int rootIterCount = 0;
@@ -1166,8 +1168,9 @@ __device__ inline float time_of_impact(int* state, const Poly* pA, const Sweep& 
 #ifdef NASCAR_PROFILE
         if (prof_iters) ++prof_iters[1];
 #endif
-        float s = sep_eval(fcn, pA, pB, indexA, indexB, t);
-        if (fabsf(s - target) < tolerance) { t2 = t; break; }
+        const Xf xa = sweep_xf(sA, t), xb = sweep_xf_static(sB, t, qB);
+        float s = sep_eval(fcn, pA, pB, indexA, indexB, xa, xb);
+        if (fabsf(s - target) < tolerance) { t2 = t; xfA2 = xa; xfB2 = xb; break; }
         if (s > target) { a1 = t; s1 = s; } else { a2 = t; s2 = s; }
         if (rootIterCount == 50) break;
       }

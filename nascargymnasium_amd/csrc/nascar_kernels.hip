@@ -65,12 +65,24 @@ struct BeamGrid {
   const int* cell;          // [nx * ny]: first list of the cell (built cell id * BEAM_NB), -1: not built
   const uint32_t* start;    // [built cells * BEAM_NB + 1]
   const uint32_t* ent;
-  // [built cells * BEAM_NB] the first BEAM_HEAD entries of each list, padded with BEAM_PAD: one 16-byte load
-  // starts a walk (the rest of the list, ent[start[slot] + BEAM_HEAD ...], is read only past the head)
+  // [built cells * BEAM_NB][BEAM_HW] head records: the first BEAM_HEAD entries of each list (padded with
+  // BEAM_PAD) and a tail word -- the ent[] index of the list's next entry (bits 0-27) and how many follow
+  // (bits 28-31, 15 = "15 or more": read start[] for the end) -- so a walk starts with BEAM_HW independent
+  // 16-byte loads and reads the rest of a long list in chunks of 4 entries without a start[] lookup
   const uint4* head;
 };
-#define BEAM_HEAD 4
+#ifndef BEAM_HW
+#define BEAM_HW 2
+#endif
+#define BEAM_HEAD (4 * BEAM_HW - 1)
 #define BEAM_PAD 0xFFFFFFFFu   // bound 655.35 m: past every best hit (<= 2 * 250 m), so a walk always stops on it
+struct BeamHead { uint4 w[BEAM_HW]; };
+__device__ __forceinline__ BeamHead beam_head(const BeamGrid& G, int li) {
+  BeamHead h;
+#pragma unroll
+  for (int k = 0; k < BEAM_HW; ++k) h.w[k] = G.head[(size_t)li * BEAM_HW + k];
+  return h;
+}
 struct TrackDev {
   LWall* walls; int nwall;
   DSeg* segs; int nseg;
@@ -1221,10 +1233,12 @@ __device__ __forceinline__ void quad_transpose(const float v[4], float o[4], int
 // One ray's walk of its beam list (list index li, head record h = G.head[li]): the first BEAM_HEAD entries from
 // the head, the rest of the list only when all of them were walked; stops at the first entry whose distance
 // bound lies beyond the best hit.  Returns the best b2PolygonShape::RayCast fraction (2 = no hit).
-__device__ __forceinline__ float ray_walk(const BeamGrid& G, const float4* __restrict__ sw, int li, uint4 h, V2 p1, V2 p2,
-                                          float dx, float dy) {
+__device__ __forceinline__ float ray_walk(const BeamGrid& G, const float4* __restrict__ sw, int li, const BeamHead& h, V2 p1,
+                                          V2 p2, float dx, float dy) {
   float bi = 2.0f;
-  const uint32_t hv[BEAM_HEAD] = {h.x, h.y, h.z, h.w};
+  uint32_t hv[4 * BEAM_HW];
+#pragma unroll
+  for (int k = 0; k < BEAM_HW; ++k) { hv[4 * k] = h.w[k].x; hv[4 * k + 1] = h.w[k].y; hv[4 * k + 2] = h.w[k].z; hv[4 * k + 3] = h.w[k].w; }
   bool more = true;
 #pragma unroll
   for (int k = 0; k < BEAM_HEAD; ++k) {
@@ -1234,14 +1248,24 @@ __device__ __forceinline__ float ray_walk(const BeamGrid& G, const float4* __res
     PCOUNT(10, 1);
     bi = wall_cast(sw[2 * j], sw[2 * j + 1], p1, p2.x, p2.y, dx, dy, bi);
   }
-  if (more) {
-    const uint32_t s0 = G.start[li] + BEAM_HEAD, e0 = G.start[li + 1];
-    for (uint32_t k = s0; k < e0; ++k) {
-      const uint32_t v = G.ent[k];
-      if ((float)(v >> 16) * 0.01f > bi * 250.0f * 1.00001f + 0.01f) break;
-      const int j = (int)(v & 0xFFFFu);
-      PCOUNT(10, 1);
-      bi = wall_cast(sw[2 * j], sw[2 * j + 1], p1, p2.x, p2.y, dx, dy, bi);
+  const uint32_t tail = hv[BEAM_HEAD];
+  if (more && tail != 0u) {
+    const uint32_t s0 = tail & 0x0FFFFFFFu, c = tail >> 28;
+    const uint32_t e0 = c < 15u ? s0 + c : G.start[li + 1];
+    for (uint32_t k = s0; k < e0; k += 4) {   // 4 entries requested together, walked in order
+      uint32_t v4[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v4[q] = k + q < e0 ? G.ent[k + q] : BEAM_PAD;
+      bool stop = false;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const uint32_t v = v4[q];
+        if ((float)(v >> 16) * 0.01f > bi * 250.0f * 1.00001f + 0.01f) { stop = true; break; }
+        const int j = (int)(v & 0xFFFFu);
+        PCOUNT(10, 1);
+        bi = wall_cast(sw[2 * j], sw[2 * j + 1], p1, p2.x, p2.y, dx, dy, bi);
+      }
+      if (stop) break;
     }
   }
   return bi;
@@ -1295,7 +1319,7 @@ __device__ __forceinline__ void ray_lane(const Params& P, const TrackDev& T, con
       float bi = 2.0f;
       if (base >= 0) {
         const int sl = slot_of(i);
-        bi = ray_walk(G, sw, base + sl, G.head[base + sl], p1, p2, dx, dy);
+        bi = ray_walk(G, sw, base + sl, beam_head(G, base + sl), p1, p2, dx, dy);
       } else {
         PCOUNT(9, 1);
         bi = ray_fallback(T, p1, p2.x, p2.y, dx, dy, ps.z, i);
@@ -1346,7 +1370,7 @@ __device__ __forceinline__ void ray_block_batched(const Params& P, const TrackDe
     slot0[j] = beam_slot0((double)pa[j].z);
   }
   V2 p2[NJ][RPL];
-  uint4 hd[NJ][RPL];
+  BeamHead hd[NJ][RPL];
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
 #pragma unroll
@@ -1354,7 +1378,8 @@ __device__ __forceinline__ void ray_block_batched(const Params& P, const TrackDe
       double dxd, dyd;
       p2[j][q] = ray_end(P, pa[j].x, pa[j].y, pa[j].z, cs[j].x, cs[j].y, r + RAY_LPC * q, dxd, dyd);
       const int sl = (slot0[j] & ~15) | ((slot0[j] - (r + RAY_LPC * q)) & 15);
-      hd[j][q] = base[j] >= 0 ? G.head[base[j] + sl] : make_uint4(0, 0, 0, 0);
+      if (base[j] >= 0) hd[j][q] = beam_head(G, base[j] + sl);
+      else for (int k = 0; k < BEAM_HW; ++k) hd[j][q].w[k] = make_uint4(0, 0, 0, 0);
     }
   }
 #pragma unroll
@@ -1369,7 +1394,7 @@ __device__ __forceinline__ void ray_block_batched(const Params& P, const TrackDe
       const float dx = (e.x - p1.x) * 0.004f, dy = (e.y - p1.y) * 0.004f;   // cull only
       float bi;
       if (base[j] >= 0) {
-        const uint4 h = q == 0 ? hd[j][0] : q == 1 ? hd[j][1] : q == 2 ? hd[j][2] : hd[j][3];
+        const BeamHead h = q == 0 ? hd[j][0] : q == 1 ? hd[j][1] : q == 2 ? hd[j][2] : hd[j][3];
         const int sl = (slot0[j] & ~15) | ((slot0[j] - i) & 15);
         bi = ray_walk(G, sw, base[j] + sl, h, p1, e, dx, dy);
       } else {
@@ -2176,16 +2201,20 @@ static void build_beams(HostTrack& t) {
       B.ent.insert(B.ent.end(), L.begin(), L.end());
     }
   B.start.back() = (uint32_t)B.ent.size();
-  B.head.assign((size_t)ncell * BEAM_NB, make_uint4(BEAM_PAD, BEAM_PAD, BEAM_PAD, BEAM_PAD));
+  B.head.assign((size_t)ncell * BEAM_NB * BEAM_HW, make_uint4(BEAM_PAD, BEAM_PAD, BEAM_PAD, BEAM_PAD));
   for (size_t s = 0; s + 1 < B.start.size(); ++s) {
-    uint32_t h[BEAM_HEAD];
-    for (int k = 0; k < BEAM_HEAD; ++k) h[k] = B.start[s] + k < B.start[s + 1] ? B.ent[B.start[s] + k] : BEAM_PAD;
-    B.head[s] = make_uint4(h[0], h[1], h[2], h[3]);
+    uint32_t h[4 * BEAM_HW];
+    const uint32_t n = B.start[s + 1] - B.start[s];
+    for (int k = 0; k < BEAM_HEAD; ++k) h[k] = (uint32_t)k < n ? B.ent[B.start[s] + k] : BEAM_PAD;
+    const uint32_t rest = n > (uint32_t)BEAM_HEAD ? n - BEAM_HEAD : 0u;
+    h[BEAM_HEAD] = rest ? ((B.start[s] + BEAM_HEAD) | (std::min<uint32_t>(rest, 15u) << 28)) : 0u;
+    for (int k = 0; k < BEAM_HW; ++k) B.head[s * BEAM_HW + k] = make_uint4(h[4 * k], h[4 * k + 1], h[4 * k + 2], h[4 * k + 3]);
   }
   B.build_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
 }
 static int upload_beams(HostTrack& t) {
   auto& B = t.beam;
+  if (B.ent.size() >= (1u << 28)) return fail("beam lists hold %zu entries (head tail offsets are 28-bit)", B.ent.size());
   HIPCHK(hipMalloc(&B.d_cell, sizeof(int) * B.cell.size()));
   HIPCHK(hipMemcpy(B.d_cell, B.cell.data(), sizeof(int) * B.cell.size(), hipMemcpyHostToDevice));
   HIPCHK(hipMalloc(&B.d_start, sizeof(uint32_t) * B.start.size()));
@@ -2223,6 +2252,7 @@ struct NascarHandle {
   int map_identity = 0, one_track = -1;   // Params shortcuts of the block map (prepare)
   std::vector<int> env_track;
   std::vector<int> pending_track;   // nascar_set_env_tracks, applied per env by its next nascar_reset
+  bool pristine = true;             // no reset / step / rollout / set_state yet: track changes apply at once
   float* d_vhist = nullptr;  // [VH_RING][N] speed history (nascar_set_perf_history), outside the snapshot arena
   double* d_ctl = nullptr;   // rule-driver state for nascar_policy_actions (inside the arena: snapshots keep it)
   float4* d_pose = nullptr;  // [2][N] step/reset -> sensor_kernel hand-off
@@ -2232,6 +2262,8 @@ struct NascarHandle {
   void* d_params = nullptr;  // device copy of the launch Params (rollout_kernel) and the host image last uploaded
   Params params_up; bool params_valid = false;
   ActorDev actor{};
+  void* d_actor32 = nullptr; ActorF32 actor32{};   // fp32 copies (nascar_set_actor_precision)
+  int actor_fp32 = 1;   // default: reference precision
   size_t max_lds = 0, max_sensor_lds = 0, max_sensor_groups_lds = 0;
   bool dirty_tracks = true;
 };
@@ -2280,7 +2312,7 @@ extern "C" int nascar_create(const NascarConfig* cfg, NascarHandle** out) {
 extern "C" void nascar_destroy(NascarHandle* h) {
   if (!h) return;
   hipFree(h->d_vhist);
-  hipFree(h->arena); hipFree(h->d_pose); hipFree(h->d_pose_cs); hipFree(h->d_ray_cs); hipFree(h->d_actor); hipFree(h->d_params);
+  hipFree(h->arena); hipFree(h->d_pose); hipFree(h->d_pose_cs); hipFree(h->d_ray_cs); hipFree(h->d_actor); hipFree(h->d_actor32); hipFree(h->d_params);
   for (auto& t : h->tracks) {
     hipFree(t.d_walls); hipFree(t.d_segs); hipFree(t.d_prefix);
     hipFree(t.bp.d_start); hipFree(t.bp.d_idx); hipFree(t.bp.d_box); hipFree(t.sn.d_start); hipFree(t.sn.d_idx); hipFree(t.d_groups); hipFree(t.d_swall);
@@ -2390,6 +2422,12 @@ extern "C" int nascar_set_env_tracks(NascarHandle* h, const int32_t* env_track) 
   // recorded only: an env moves to its new track at its next nascar_reset, with fresh physics worlds (CarEnv.reset
   // recreates CarPhysics on a track change, src/car_env.py:375-394); until then it keeps stepping on its old track
   // (its Box2D contacts hold wall indices of that track)
+  if (h->pristine) {   // nothing stepped or reset yet: no state on the old track, apply now
+    h->env_track.assign(env_track, env_track + h->E);
+    h->pending_track.clear();
+    h->dirty_tracks = true;
+    return 0;
+  }
   h->pending_track.assign(env_track, env_track + h->E);
   return 0;
 }
@@ -2506,6 +2544,7 @@ static void launch_sensors(NascarHandle* h, const Params& P, float* obs, float* 
 
 extern "C" int nascar_reset(NascarHandle* h, const uint8_t* env_mask, float* obs, void* stream) {
   if (!h || !obs) return fail("null argument");
+  h->pristine = false;
   if (apply_pending_tracks(h, env_mask, stream)) return -1;
   if (prepare(h)) return -1;
   Params P = make_params(h);
@@ -2519,6 +2558,7 @@ extern "C" int nascar_reset(NascarHandle* h, const uint8_t* env_mask, float* obs
 extern "C" int nascar_step(NascarHandle* h, const void* actions, int32_t discrete, float* obs, float* reward,
                            uint8_t* car_flags, uint8_t* env_flags, int32_t auto_reset, float* terminal_obs, void* stream) {
   if (!h || !actions || !obs || !reward) return fail("null argument");
+  h->pristine = false;
   if (prepare(h)) return -1;
   Params P = make_params(h);
   // model_kernel -> logic_kernel -> sensor_kernel (pass A for every car, pass B for auto-reset cars).
@@ -2542,6 +2582,7 @@ extern "C" int nascar_rollout(NascarHandle* h, int32_t policy, uint64_t seed, in
   if (policy != 0 && policy != 1 && policy != 3) return fail("rollout policy must be 0, 1 or 3 (got %d)", policy);
   if (steps < 0) return fail("steps must be >= 0");
   if (steps == 0) return 0;
+  h->pristine = false;
   if (prepare(h)) return -1;
   Params P = make_params(h);
   if (!h->d_params) {
@@ -2586,10 +2627,12 @@ extern "C" int nascar_get_state(NascarHandle* h, void* dst, void* stream) {
 }
 extern "C" int nascar_set_state(NascarHandle* h, const void* src, void* stream) {
   if (!h || !src) return fail("null argument");
+  h->pristine = false;
   HIPCHK(hipMemcpyAsync(h->arena, src, h->arena_bytes, hipMemcpyDeviceToDevice, (hipStream_t)stream));
   return 0;
 }
 
+static void launch_actor(NascarHandle* h, int n, const float* obs, float* actions, void* stream);
 extern "C" int nascar_policy_actions(NascarHandle* h, int32_t policy, uint64_t seed, int64_t step, const float* obs,
                                      float* actions, void* stream) {
   if (!h || !actions) return fail("null argument");
@@ -2598,7 +2641,7 @@ extern "C" int nascar_policy_actions(NascarHandle* h, int32_t policy, uint64_t s
   if (policy == 2) {
     if (!h->d_actor) return fail("policy 2 needs an actor (nascar_set_actor)");
     if (((uintptr_t)obs | (uintptr_t)actions) & 7) return fail("actor obs/actions must be 8-byte aligned");
-    hipLaunchKernelGGL(actor_kernel, dim3(actor_grid(h->N)), dim3(64 * ACT_WAVES), 0, (hipStream_t)stream, h->N, obs, actions, h->actor);
+    launch_actor(h, h->N, obs, actions, stream);
     HIPCHK(hipGetLastError());
     return 0;
   }
@@ -2673,7 +2716,47 @@ extern "C" int nascar_set_actor(NascarHandle* h, const float* w1, const float* b
   HIPCHK(hipMemcpy(d + o_b3, b3, ACT_OUT * 4, hipMemcpyHostToDevice));
   h->actor.w1p = (const bf16x8*)(d + o_w1); h->actor.w2p = (const bf16x8*)(d + o_w2);
   h->actor.b2 = (const float*)(d + o_b2); h->actor.w3p = (const bf16x8*)(d + o_w3); h->actor.b3 = (const float*)(d + o_b3);
+  {   // float32 copies for the reference-precision kernel: W1 and W2 transposed ([k][unit])
+    std::vector<float> f((size_t)ACT_OBS * ACT_H + ACT_H + (size_t)ACT_H * ACT_H + ACT_H + 2 * ACT_H + 2);
+    float* p = f.data();
+    float* w1t = p; p += (size_t)ACT_OBS * ACT_H;
+    float* b1c = p; p += ACT_H;
+    float* w2t = p; p += (size_t)ACT_H * ACT_H;
+    float* b2c = p; p += ACT_H;
+    float* w3c = p; p += 2 * ACT_H;
+    float* b3c = p;
+    for (int o = 0; o < ACT_H; ++o)
+      for (int i = 0; i < ACT_OBS; ++i) w1t[(size_t)i * ACT_H + o] = w1[(size_t)o * ACT_OBS + i];
+    for (int o = 0; o < ACT_H; ++o)
+      for (int i = 0; i < ACT_H; ++i) w2t[(size_t)i * ACT_H + o] = w2[(size_t)o * ACT_H + i];
+    memcpy(b1c, b1, 4 * ACT_H); memcpy(b2c, b2, 4 * ACT_H); memcpy(w3c, w3, 8 * ACT_H); memcpy(b3c, b3, 8);
+    if (!h->d_actor32) HIPCHK(hipMalloc(&h->d_actor32, f.size() * 4));
+    HIPCHK(hipMemcpy(h->d_actor32, f.data(), f.size() * 4, hipMemcpyHostToDevice));
+    const float* d32 = (const float*)h->d_actor32;
+    h->actor32.w1t = d32 + (w1t - f.data()); h->actor32.b1 = d32 + (b1c - f.data());
+    h->actor32.w2t = d32 + (w2t - f.data()); h->actor32.b2 = d32 + (b2c - f.data());
+    h->actor32.w3 = d32 + (w3c - f.data()); h->actor32.b3 = d32 + (b3c - f.data());
+  }
   return 0;
+}
+
+extern "C" int nascar_set_actor_precision(NascarHandle* h, int32_t fp32) {
+  if (!h) return fail("null argument");
+  if (fp32 != 0 && fp32 != 1) return fail("precision must be 0 (bf16 MFMA) or 1 (fp32)");
+  h->actor_fp32 = fp32;
+  return 0;
+}
+
+static void launch_actor(NascarHandle* h, int n, const float* obs, float* actions, void* stream) {
+  if (h->actor_fp32) {
+    static int cus = 0;
+    if (!cus) { int dev = 0; hipGetDevice(&dev); hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev); if (cus <= 0) cus = 256; }
+    const int tiles = (n + AF_TILE - 1) / AF_TILE;
+    hipLaunchKernelGGL(actor_fp32_kernel, dim3(std::max(1, std::min(tiles, 2 * cus))), dim3(256), 0, (hipStream_t)stream,
+                       n, obs, actions, h->actor32);
+  } else {
+    hipLaunchKernelGGL(actor_kernel, dim3(actor_grid(n)), dim3(64 * ACT_WAVES), 0, (hipStream_t)stream, n, obs, actions, h->actor);
+  }
 }
 
 // Actor forward on an arbitrary device batch: obs [n][38] float32 -> actions [n][2] float32.
@@ -2682,7 +2765,7 @@ extern "C" int nascar_actor_forward(NascarHandle* h, const float* obs, int32_t n
   if (!h->d_actor) return fail("no actor loaded (nascar_set_actor)");
   if (((uintptr_t)obs | (uintptr_t)actions) & 7) return fail("actor obs/actions must be 8-byte aligned");
   if (n == 0) return 0;
-  hipLaunchKernelGGL(actor_kernel, dim3(actor_grid(n)), dim3(64 * ACT_WAVES), 0, (hipStream_t)stream, n, obs, actions, h->actor);
+  launch_actor(h, n, obs, actions, stream);
   HIPCHK(hipGetLastError());
   return 0;
 }

@@ -96,3 +96,22 @@ def test_sb3_actor_loader(tmp_path):
         buf2 = io.BytesIO(); torch.save({"x": torch.zeros(1)}, buf2); z.writestr("policy.pth", buf2.getvalue())
     with pytest.raises(ValueError):
         load_sb3_actor(str(bad))
+
+
+def test_sac_fixture_consistent():
+    """tests/golden/sac_1235_actor.npz: its actions are the float32 SB3 predict() restatement of its weights,
+    and (where the reference is present) its weights are sac_1235.zip's actor tensors."""
+    import os
+    import sys
+    import numpy as np
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(root, "oracle"))
+    from gen_actor_fixture import sb3_predict_fp32
+    from nascargymnasium_amd.policy import ACTOR_KEYS, load_sb3_actor
+    d = np.load(os.path.join(root, "tests", "golden", "sac_1235_actor.npz"))
+    w = {k: d[k.replace(".", "__")] for k in ACTOR_KEYS}
+    assert np.array_equal(sb3_predict_fp32(w, d["obs"]), d["actions_fp32"])
+    z = "/root/reference/game/control/models/sac_1235.zip"
+    if os.path.exists(z):
+        ref = load_sb3_actor(z)
+        assert all(np.array_equal(ref[k], w[k]) for k in ACTOR_KEYS)

@@ -67,7 +67,7 @@ def test_actor_matches_fp32_reference(n, seed):
     w = random_actor(seed)
     x = _obs_batch(n, seed)
     env = BatchedCarEnv(1, 1, "daytona", device="cuda:0")
-    env.set_actor(w)
+    env.set_actor(w, precision="bf16")
     got = env.actor_forward(torch.from_numpy(x).cuda()).cpu().numpy()
     env.close()
     ref = _ref_fp32(w, x)
@@ -81,10 +81,70 @@ def test_policy_2_is_the_actor_on_the_env_obs():
     from nascargymnasium_amd.batched import BatchedCarEnv
     from nascargymnasium_amd.policy import random_actor
     env = BatchedCarEnv(300, 3, "martinsville", device="cuda:0")
-    env.set_actor(random_actor(7))
+    env.set_actor(random_actor(7), precision="bf16")
     env.reset()
     for k in range(20):
         a = env.policy_actions(2).clone()
         assert torch.equal(a, env.actor_forward(env.obs))
         env.step(a, auto_reset=True)
     env.close()
+
+
+def _sac_1235():
+    import os
+    from golden_replay import GOLDEN
+    d = np.load(os.path.join(GOLDEN, "sac_1235_actor.npz"))
+    from nascargymnasium_amd.policy import ACTOR_KEYS
+    return {k: d[k.replace(".", "__")] for k in ACTOR_KEYS}, d["obs"], d["actions_fp32"]
+
+
+def test_sac_1235_fp32_matches_reference():
+    """The reference's own SAC checkpoint (game/control/models/sac_1235.zip, via oracle/gen_actor_fixture.py) on
+    2236 golden-trace observations: the fp32 actor kernel equals the float32 SB3 predict() restatement to 1e-5
+    (summation order only), through nascar_actor_forward and through policy 2 on an env's obs buffer."""
+    from nascargymnasium_amd.batched import BatchedCarEnv
+    w, x, want = _sac_1235()
+    env = BatchedCarEnv(1, 1, "daytona", device="cuda:0")
+    env.set_actor(w, precision="fp32")
+    got = env.actor_forward(torch.from_numpy(x).cuda()).cpu().numpy()
+    env.close()
+    d = np.abs(got - want)
+    assert d.max() <= 1e-5, d.max()
+    n = len(x) // 4 * 4
+    env = BatchedCarEnv(n // 4, 4, "daytona", device="cuda:0")
+    env.set_actor(w, precision="fp32")
+    env.obs.copy_(torch.from_numpy(x[:n].reshape(n // 4, 4, 38)).cuda())
+    got2 = env.policy_actions(2).cpu().numpy().reshape(n, 2)
+    env.close()
+    assert np.array_equal(got2, got[:n])
+
+
+def test_sac_1235_bf16_error_is_the_documented_one():
+    """The opt-in bf16-MFMA actor on the same checkpoint and observations.  Measured: max |delta| 0.40, mean 8.7e-3
+    -- the trained policy's pre-tanh means are large and sensitive, so bf16 operands are NOT faithful to the
+    reference here (fp32, the default, is); this pins the documented error, and the kernel must
+    still agree with a float64 emulation of its own bf16 operand rounding."""
+    from nascargymnasium_amd.batched import BatchedCarEnv
+    w, x, want = _sac_1235()
+    env = BatchedCarEnv(1, 1, "daytona", device="cuda:0")
+    env.set_actor(w, precision="bf16")
+    got = env.actor_forward(torch.from_numpy(x).cuda()).cpu().numpy()
+    env.close()
+    d = np.abs(got - want)
+    assert d.max() <= 0.45 and d.mean() <= 1e-2, (d.max(), d.mean())
+    emu = _ref_bf16(w, x)
+    emu = np.float32(-1.0) + (np.float32(0.5) * (emu.astype(np.float32) + np.float32(1.0)) * np.float32(2.0))
+    assert np.abs(got - emu).max() <= 1e-2
+
+
+@pytest.mark.parametrize("n,seed", [(4096, 0), (37, 2), (1, 3)])
+def test_actor_fp32_random_weights(n, seed):
+    from nascargymnasium_amd.batched import BatchedCarEnv
+    from nascargymnasium_amd.policy import random_actor
+    w = random_actor(seed)
+    x = _obs_batch(n, seed)
+    env = BatchedCarEnv(1, 1, "daytona", device="cuda:0")
+    env.set_actor(w, precision="fp32")
+    got = env.actor_forward(torch.from_numpy(x).cuda()).cpu().numpy()
+    env.close()
+    assert np.abs(got - _ref_fp32(w, x)).max() <= 1e-5
