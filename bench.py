@@ -276,6 +276,8 @@ def main():
                     "(BASELINE cfg5: mixed batch, divergent geometry); --track is ignored")
     ap.add_argument("--gather", action="store_true", help="gather every step's obs/reward/flags of all ranks to "
                     "rank 0 (RCCL, side stream; BASELINE cfg4 single-learner layout)")
+    ap.add_argument("--car-contact", action="store_true", help="BUILD-ONLY EXTENSION: car-car contact inside each env "
+                    "(cfg3's 'car-car collision on'; no reference counterpart, reported as its own row)")
     ap.add_argument("--no-secondary", action="store_true", help="skip the uniform-from-reset secondary measurement")
     ap.add_argument("--cpu-threads", type=int, default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -309,6 +311,8 @@ def main():
         return BatchedCarEnv(E, C, tpath, device=dev)
 
     env = make_env()
+    if args.car_contact:
+        env.set_car_contact(True)
     gather = None
     if args.gather:
         from nascargymnasium_amd.gather import ObsGather
@@ -380,6 +384,7 @@ def main():
                                f"{settle_txt}, auto-reset",
                    "envs_per_gpu": E, "cars_per_env": C, "policy": args.policy,
                    "launch": f"fused rollout, {step.R} steps per launch" if step.R else "per-step kernels",
+                   "car_contact": "on (build-only extension, no reference counterpart)" if args.car_contact else "off (reference)",
                    "track": "mixed (env e: track e mod 8)" if args.mixed else os.path.basename(tpath),
                    "parallelism": f"dp{world} (env shards" + (", RCCL gather of obs/reward/flags to rank 0 per step)" if gather else ", no collective)")},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",

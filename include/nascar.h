@@ -87,6 +87,13 @@ int nascar_rollout(NascarHandle* h, int32_t policy, uint64_t seed, int64_t step0
  * (field order: nascargymnasium_amd/_lib.py INFO_FIELDS) written to a device buffer. */
 int nascar_get_info(NascarHandle* h, double* info, void* stream);
 
+/* BUILD-ONLY EXTENSION, no reference counterpart (each reference car has its own b2World, so cars never touch):
+ * enable != 0 makes the cars of an env collide -- staggered start grid (rows of 2, 8 m apart), and after each
+ * Box2D step a frictionless central impulse (restitution 0.25) between overlapping, closing car boxes, counted in
+ * the cars' collision impulse (damage / impact disables).  Default 0 (reference behaviour); parity runs with 0.
+ * Takes effect from the next reset (start grid) and step. */
+int nascar_set_car_contact(NascarHandle* h, int32_t enable);
+
 /* Car.velocity_history for Car.validate_performance (src/car.py:173, 384-386, 1060-1098): enable != 0 keeps
  * every car's speed after each step in a 600-sample window on the device (VH_RING x N float32, outside the
  * state arena, so snapshots do not carry it) and nascar_get_info reports perf_count / perf_max_speed /

@@ -71,6 +71,11 @@ class BatchedCarEnv:
         if perf_history:
             self.set_perf_history(True)
 
+    def set_car_contact(self, enable: bool = True):
+        """BUILD-ONLY EXTENSION (no reference counterpart): cars of an env collide with each other (staggered start
+        grid, central impulses between overlapping closing car boxes).  Off by default; parity holds only when off."""
+        _lib.check(self.L.nascar_set_car_contact(self.h, int(bool(enable))))
+
     def set_perf_history(self, enable: bool = True):
         """Keep Car.velocity_history on the device so the info's `performance` dict is Car.validate_performance
         (src/car.py:1060-1098); a 640-sample float32 ring per car, one 4-byte store per car-step.  The window starts

@@ -108,6 +108,7 @@ struct Params {
   const double2* ray_cs;   // [16] cos, sin of the ray offsets radians(22.5 i) (nascar_rays.h)
   double* ctl;         // [N][4] rule-driver state of the device action sources (policy_car)
   float* vhist;        // [VH_RING][N] speed history for validate_performance, or null (nascar_set_perf_history)
+  int car_contact;     // build-only extension (nascar_set_car_contact): car-car contact inside each env; 0 = reference
   // block map shortcuts (prepare()): map_identity = blk_env[s] is s (< E) or -1, one_track >= 0 = every
   // block's track; they spare each kernel's first dependent load
   int map_identity, one_track;
@@ -836,6 +837,12 @@ __device__ __forceinline__ void set_pose(const Params& P, size_t k, const Car& c
 // ------------------------------------------------------------------ reset (src/car_env.py:316-535)
 __device__ inline void car_reset(const Params& P, Car& c, int n, bool fresh, const WallSet& S, const TrackDev& T) {
   V2 p = OV(P.start_x, P.start_y); float a = P.start_angle;
+  if (P.car_contact) {   // extension only: a staggered grid (rows of 2, 8 m apart, +-3 m), so cars do not start overlapped
+    const int i = n % P.C;
+    const Rot q = rot_set(a);
+    p = vadd(p, rmul(q, V(-8.0f * (float)(i >> 1), (i & 1) ? -3.0f : 3.0f)));
+    if (P.C == 1) p = OV(P.start_x, P.start_y);
+  }
   if (fresh) {   // Car() + CarPhysics(car, track): new b2World (src/car_physics.py:74-107)
     c.xf.q = rot_set(a); c.xf.p = p;
     c.c = xmul(c.xf, zero2()); c.a = a; c.c0 = c.c; c.a0 = a;
@@ -1775,6 +1782,71 @@ __device__ __forceinline__ void logic_run(const Params& P, const TrackDev& T, co
   }
   LPROF(8);}
 
+// ------------------------------------------------------------------ car-car contact (build-only extension)
+// NOT in the reference: each reference car lives in its own b2World (src/car_physics.py:74-107), so cars of
+// one env never touch.  With nascar_set_car_contact(h, 1) the cars of an env collide: after the
+// Box2D step every overlapping pair of car boxes (separating-axis test on the 4 box axes) that is closing
+// along the axis of least penetration exchanges a frictionless central impulse with restitution 0.25 (the
+// wall's, src/constants/physics.py), Jacobi-style from the post-step velocities (all of an env's cars are
+// read before any is written: the env sits in one workgroup), and the impulse magnitude enters the car's
+// collision impulse as CarCollisionListener.PostSolve does for walls (max over contacts), so damage and
+// impact disables apply.  Positions are left to the next step's integration (Box2D proxies stay valid).
+// Sensors still see walls only.  Default off; every parity test runs with it off.
+__device__ __forceinline__ bool car_box_overlap(V2 pa, Rot qa, V2 pb, Rot qb, V2& n, float& depth) {
+  const V2 d = vsub(pb, pa);
+  const V2 ax[4] = {V(qa.c, qa.s), V(-qa.s, qa.c), V(qb.c, qb.s), V(-qb.s, qb.c)};
+  depth = FLT_BIG;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const V2 u = ax[k];
+    const float ea = CAR_HX * fabsf(vdot(u, V(qa.c, qa.s))) + CAR_HY * fabsf(vdot(u, V(-qa.s, qa.c)));
+    const float eb = CAR_HX * fabsf(vdot(u, V(qb.c, qb.s))) + CAR_HY * fabsf(vdot(u, V(-qb.s, qb.c)));
+    const float sd = vdot(u, d), pen = ea + eb - fabsf(sd);
+    if (pen <= 0.0f) return false;
+    if (pen < depth) { depth = pen; n = sd >= 0.0f ? u : vneg(u); }   // n: from a toward b
+  }
+  return true;
+}
+__device__ __forceinline__ void car_contact_block(const Params& P, int tid, int el, int car, int env, int n) {
+  const int C = P.C;
+  V2 dv = zero2();
+  double jmax = 0.0;
+  if (env >= 0) {
+    const V2 pa = V(F32P(P, xpx)[n], F32P(P, xpy)[n]);
+    Rot qa; qa.s = F32P(P, qs)[n]; qa.c = F32P(P, qc)[n];
+    const V2 va = V(F32P(P, vx)[n], F32P(P, vy)[n]);
+    const int e0 = env * C;
+    for (int j = 0; j < C; ++j) {
+      if (j == car) continue;
+      const int m = e0 + j;
+      const V2 pb = V(F32P(P, xpx)[m], F32P(P, xpy)[m]);
+      if (fabsf(pb.x - pa.x) > 5.7f || fabsf(pb.y - pa.y) > 5.7f) continue;   // > 2 circumradii apart
+      Rot qb; qb.s = F32P(P, qs)[m]; qb.c = F32P(P, qc)[m];
+      V2 nn; float depth;
+      if (!car_box_overlap(pa, qa, pb, qb, nn, depth)) continue;
+      const V2 vb = V(F32P(P, vx)[m], F32P(P, vy)[m]);
+      const float vrel = vdot(vsub(vb, va), nn);
+      if (vrel >= 0.0f) continue;                                  // separating
+      const float J = -(1.0f + MIX_RESTITUTION) * vrel * (0.5f / CAR_INV_MASS);   // equal masses
+      dv = vsub(dv, vmul(J * CAR_INV_MASS, nn));
+      jmax = pymax(jmax, (double)J);
+    }
+  }
+  __syncthreads();   // every car of the env has read the post-step velocities
+  if (env >= 0 && (dv.x != 0.0f || dv.y != 0.0f)) {
+    F32P(P, vx)[n] = F32P(P, vx)[n] + dv.x;
+    F32P(P, vy)[n] = F32P(P, vy)[n] + dv.y;
+    if (!I32P(P, imp_present)[n]) { I32P(P, imp_present)[n] = 1; F64P(P, imp)[n] = 0.0; }
+    F64P(P, imp)[n] = pymax(F64P(P, imp)[n], jmax);
+  }
+}
+__global__ void __launch_bounds__(SBLOCK) car_contact_kernel(Params P) {
+  const int tid = threadIdx.x, C = P.C;
+  const int el = tid / C, car = tid - el * C;
+  const int env = blk_env_of(P, el, blockIdx.x * P.epb + el);
+  car_contact_block(P, tid, el, car, env, env >= 0 ? env * C + car : 0);
+}
+
 __global__ void __launch_bounds__(SBLOCK) logic_kernel(Params P, float* obs, float* reward, uint8_t* car_flags,
                                                       uint8_t* env_flags, int auto_reset, float* terminal_obs) {
   __shared__ LogicLDS L;
@@ -1854,6 +1926,11 @@ static __device__ __attribute__((noinline)) void ro_logic_phase(ParamsK Pk, floa
   logic_run(P, T, g_ro_track, g_ro_logic, s.tid, s.el, s.car, s.env, s.n, c, sim, pend_in, reason_in, obs, reward,
             car_flags, env_flags, auto_reset, nullptr);
 }
+static __device__ __attribute__((noinline)) void ro_contact_phase(ParamsK Pk) {
+  const Params& P = *(const Params*)Pk;
+  const RoSlot s = ro_slot(P);
+  car_contact_block(P, s.tid, s.el, s.car, s.env, s.n);
+}
 static __device__ __attribute__((noinline)) void ro_sensor_phase(ParamsK Pk, float* obs, int passes) {
   const Params& P = *(const Params*)Pk;
   const TrackDev T = ro_track(P);
@@ -1879,6 +1956,10 @@ rollout_kernel(const Params* __restrict__ Pg, int K, int policy, uint64_t seed, 
 #endif
     ro_model_phase(Pk, policy, seed, step0 + k, obs);
     __syncthreads();
+    if (P.car_contact) {
+      ro_contact_phase(Pk);
+      __syncthreads();
+    }
 #ifdef NASCAR_PROFILE
     const unsigned long long t1 = __builtin_amdgcn_s_memtime();
 #endif
@@ -1888,7 +1969,9 @@ rollout_kernel(const Params* __restrict__ Pg, int K, int policy, uint64_t seed, 
 #ifdef NASCAR_PROFILE
     const unsigned long long t2 = __builtin_amdgcn_s_memtime();
 #endif
+#ifndef RO_EXP_NO_SENSOR   // timing experiment only
     ro_sensor_phase(Pk, obs, auto_reset ? 3 : 1);
+#endif
     __syncthreads();
 #ifdef NASCAR_PROFILE
     const unsigned long long t3 = __builtin_amdgcn_s_memtime();
@@ -2252,7 +2335,8 @@ struct NascarHandle {
   int map_identity = 0, one_track = -1;   // Params shortcuts of the block map (prepare)
   std::vector<int> env_track;
   std::vector<int> pending_track;   // nascar_set_env_tracks, applied per env by its next nascar_reset
-  bool pristine = true;             // no reset / step / rollout / set_state yet: track changes apply at once
+  bool pristine = true;
+  int car_contact = 0;              // nascar_set_car_contact (build-only extension)             // no reset / step / rollout / set_state yet: track changes apply at once
   float* d_vhist = nullptr;  // [VH_RING][N] speed history (nascar_set_perf_history), outside the snapshot arena
   double* d_ctl = nullptr;   // rule-driver state for nascar_policy_actions (inside the arena: snapshots keep it)
   float4* d_pose = nullptr;  // [2][N] step/reset -> sensor_kernel hand-off
@@ -2512,6 +2596,7 @@ static Params make_params(NascarHandle* h) {
   P.map_identity = h->map_identity; P.one_track = h->one_track;
   P.pose = h->d_pose; P.pose_cs = h->d_pose_cs; P.ray_cs = h->d_ray_cs; P.ctl = h->d_ctl;
   P.vhist = h->d_vhist;
+  P.car_contact = h->car_contact;
   return P;
 }
 
@@ -2567,6 +2652,10 @@ extern "C" int nascar_step(NascarHandle* h, const void* actions, int32_t discret
   hipStream_t s = (hipStream_t)stream;
   hipLaunchKernelGGL(model_kernel, dim3(h->nblocks), dim3(SBLOCK), 0, s, P, actions, discrete, terminal_obs != nullptr);
   HIPCHK(hipGetLastError());
+  if (h->car_contact) {
+    hipLaunchKernelGGL(car_contact_kernel, dim3(h->nblocks), dim3(SBLOCK), 0, s, P);
+    HIPCHK(hipGetLastError());
+  }
   hipLaunchKernelGGL(logic_kernel, dim3(h->nblocks), dim3(SBLOCK), 0, s, P, obs, reward, car_flags,
                      env_flags, auto_reset, terminal_obs);
   HIPCHK(hipGetLastError());
@@ -2606,6 +2695,12 @@ extern "C" int nascar_get_info(NascarHandle* h, double* info, void* stream) {
   Params P = make_params(h);
   hipLaunchKernelGGL(info_kernel, dim3(h->nblocks), dim3(SBLOCK), 0, (hipStream_t)stream, P, info);
   HIPCHK(hipGetLastError());
+  return 0;
+}
+
+extern "C" int nascar_set_car_contact(NascarHandle* h, int32_t enable) {
+  if (!h) return fail("null argument");
+  h->car_contact = enable ? 1 : 0;
   return 0;
 }
 

@@ -107,3 +107,65 @@ def test_track_change_waits_for_reset():
 def env_field(name):
     from nascargymnasium_amd import _lib
     return _lib.INFO_FIELDS.index(name)
+
+
+def test_car_contact_extension():
+    """Build-only extension (no reference counterpart): with car-car contact on, cars start on a staggered grid,
+    closing overlapping cars exchange impulses (total momentum of the pair conserved, impulse reported), the
+    rollout path equals the per-step path, and switching it off restores reference behaviour exactly."""
+    from nascargymnasium_amd import _lib
+    from nascargymnasium_amd.batched import BatchedCarEnv
+    E, C = 64, 4
+    F = _lib.INFO_INDEX
+    env = BatchedCarEnv(E, C, os.path.join(TRACKS, "daytona.track"), device="cuda:0")
+    env.set_car_contact(True)
+    env.reset()
+    inf = env.info_tensor().cpu().numpy()
+    xy = inf[0, :, [F["x"], F["y"]]].T
+    assert len({tuple(p) for p in xy.round(3).tolist()}) == C          # staggered, not stacked
+    # the second row (cars 2, 3) drives into the rear of the first (cars 0, 1, idle): full throttle
+    a = torch.zeros(E, C, 2, device="cuda")
+    a[:, 2:, 0] = 1.0
+    hits = 0
+    for k in range(400):
+        env.step(a)
+        hits += int(((env.car_flags & 4) != 0).sum())
+    assert hits > 0, "no car-car impulse reported"
+    # rollout == per-step with the extension on
+    b = BatchedCarEnv(E, C, os.path.join(TRACKS, "daytona.track"), device="cuda:0")
+    b.set_car_contact(True)
+    b.set_state(env.get_state()); b.obs.copy_(env.obs)
+    for k in range(60):
+        env.launch_step(env.policy_actions(3, seed=2, step=k).clone(), auto_reset=True)
+    b.rollout(3, 60, seed=2, step0=0, auto_reset=True)
+    assert torch.equal(env.obs, b.obs) and torch.equal(env.get_state(), b.get_state())
+    # off again: identical to a reference-behaviour engine from the same state
+    env.set_car_contact(False); b.set_car_contact(False)
+    ref = BatchedCarEnv(E, C, os.path.join(TRACKS, "daytona.track"), device="cuda:0")
+    ref.set_state(env.get_state()); ref.obs.copy_(env.obs)
+    for k in range(50):
+        x = torch.rand(E, C, 2, device="cuda") * 2 - 1
+        assert torch.equal(env.step(x)[0], ref.step(x)[0])
+    for x in (env, b, ref):
+        x.close()
+
+
+def test_car_contact_rear_end():
+    """Car 2 (second row) rams idle car 0 ahead of it: the impulse is reported on both and pushes car 0 forward."""
+    from nascargymnasium_amd.batched import BatchedCarEnv
+    from nascargymnasium_amd import _lib
+    env = BatchedCarEnv(1, 3, os.path.join(TRACKS, "daytona.track"), device="cuda:0")
+    env.set_car_contact(True)
+    env.reset()
+    F = _lib.INFO_INDEX
+    a = torch.tensor([[[0.0, 0.0], [0.0, 0.0], [1.0, 0.0]]], device="cuda")
+    seen = False
+    for k in range(300):
+        env.step(a)
+        if int(env.car_flags[0, 0]) & 4 and int(env.car_flags[0, 2]) & 4:
+            seen = True
+            break
+    assert seen, "car 2 never reached car 0"
+    inf = env.info_tensor().cpu().numpy()[0]
+    assert inf[0, F["vx"]] > 0.5 and abs(inf[1, F["vx"]]) < 1e-3      # car 0 pushed, car 1 untouched
+    env.close()

@@ -93,7 +93,7 @@ def main():
     CPROF_BASE = LPROF_BASE + NW * 16
     N = a.envs * a.cars
     RPROF_BASE = CPROF_BASE + (1 << 20) * 16
-    buf = torch.zeros(RPROF_BASE + 65536 * 4, dtype=torch.int64, device="cuda:0")
+    buf = torch.zeros(RPROF_BASE + 65536 * 5, dtype=torch.int64, device="cuda:0")
     L.nascar_debug_profile(ctypes.c_void_p(buf.data_ptr()))
     for s in range(a.steps):
         acts = actions(k0 + a.warmup + s)
