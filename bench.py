@@ -121,10 +121,14 @@ def throughput(world, envs, cars, steps, elapsed_max):
 
 
 def stagger_schedule(E, settle):
-    """settle step at which env e is reset so that its age when timing starts is floor(e * 10800 / E) steps
-    (ages spread uniformly over one episode); envs whose age would exceed the settle length are not reset."""
+    """settle step at which env e is reset so that its age when timing starts is floor(pi(e) * 10800 / E) steps,
+    pi a fixed (seeded) random permutation: ages spread uniformly over one episode and uncorrelated with the env
+    index -- as after many episodes that end at different times -- rather than adjacent envs (one workgroup's)
+    being one step apart and driving the same stretch of track together.  Envs whose age would exceed the settle
+    length are not reset."""
     import numpy as np
-    age = (np.arange(E, dtype=np.int64) * EPISODE_STEPS) // E
+    perm = np.random.default_rng(20261016).permutation(E).astype(np.int64)
+    age = (perm * EPISODE_STEPS) // E
     at = settle - age
     return np.where(age < settle, at, -1)
 

@@ -1969,9 +1969,7 @@ rollout_kernel(const Params* __restrict__ Pg, int K, int policy, uint64_t seed, 
 #ifdef NASCAR_PROFILE
     const unsigned long long t2 = __builtin_amdgcn_s_memtime();
 #endif
-#ifndef RO_EXP_NO_SENSOR   // timing experiment only
     ro_sensor_phase(Pk, obs, auto_reset ? 3 : 1);
-#endif
     __syncthreads();
 #ifdef NASCAR_PROFILE
     const unsigned long long t3 = __builtin_amdgcn_s_memtime();

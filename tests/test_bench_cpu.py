@@ -43,6 +43,7 @@ def test_stagger_schedule_spreads_env_ages():
     assert age.min() == 0 and age.max() < 10800
     h = np.histogram(age, bins=10, range=(0, 10800))[0]
     assert h.min() > 0.9 * h.mean()
+    assert np.abs(np.diff(age[:120])).mean() > 1000    # a workgroup's envs are not at the same point of their lap
     short = bench.stagger_schedule(100, 600)          # settle shorter than an episode: old envs never reset
     assert (short == -1).sum() == 100 - ((600 * 100 + 10799) // 10800)
 
