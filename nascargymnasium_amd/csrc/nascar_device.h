@@ -1249,127 +1249,170 @@ __device__ __forceinline__ bool toi_far(const Car& c, const Poly* pa, const LWal
   return b - fabsf(c.a - c.a0) * R_CAR > TOI_CULL_DIST;
 }
 
-// b2World::SolveTOI
+// b2World::SolveTOI, wave-cooperative.  Box2D's loop per car: scan the contacts (a cached alpha, or a fresh
+// b2TimeOfImpact for each enabled contact without one), take the first contact of minimum alpha, and if
+// alpha < 1 advance the body to it, update that contact, solve the TOI island and find new contacts --
+// then scan again (the island's contacts lost their cached alphas).  Within one scan a car's sweep is fixed,
+// so its fresh TOIs are independent: here every lane first lists the (contact, wall) pairs it needs, the
+// wave computes all listed pairs in parallel -- any present lane takes any pair, its owner's sweep read from
+// LDS -- and each lane then runs its scan on the results.  The loop runs while any lane of the wave still
+// has events, so lanes that are done lend their time to a lane with a long event chain (a car scraping a
+// wall re-scans its 2-5 contacts after each event: sequential on one lane before).  Same alphas, same
+// scan order, same minimum, so the results are Box2D's.
+#define TOI_JOBCAP 128   // pairs per compute round per wave (more pairs: further rounds)
+struct ToiWaveLDS { float4 sw0[64], sw1[64]; int2 job[TOI_JOBCAP]; float res[TOI_JOBCAP]; };
+__device__ __forceinline__ void wave_lds_sync() {   // a wave's LDS writes visible to its later LDS reads
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+__device__ __forceinline__ int popc64(unsigned long long x) { return __popcll(x); }
+// lanes below this one in mask m
+__device__ __forceinline__ int rank_in(unsigned long long m) {
+  const unsigned long long below = __lane_id() == 0 ? 0ull : (~0ull >> (64 - __lane_id()));
+  return popc64(m & below);
+}
+// b2TimeOfImpact of the car's sweep against static wall wl -> alpha of SolveTOI (1 unless TOUCHING)
+__device__ __forceinline__ float toi_alpha(float4 s0, float4 s1, const LWall& wl) {
+  Poly pa; make_box(&pa, CAR_HX, CAR_HY);
+  Poly pb; make_box(&pb, wl.hx, wl.hy);
+  Sweep sA; sA.c0 = V(s0.x, s0.y); sA.c = V(s0.z, s0.w); sA.a0 = s1.x; sA.a = s1.y; sA.alpha0 = s1.z;
+  Sweep sB; sB.c0 = V(wl.px, wl.py); sB.c = sB.c0; sB.a0 = wl.ang; sB.a = wl.ang; sB.alpha0 = 0.0f;
+  int state;
+  const float beta = time_of_impact(&state, &pa, sA, &pb, sB, 1.0f);
+  return state == TOI_TOUCHING ? fminb(s1.z + (1.0f - s1.z) * beta, 1.0f) : 1.0f;
+}
 __device__ inline void solve_toi(Car& c, const WallSet& S, float dt, float friction) {
+  __shared__ ToiWaveLDS s_toi[SBLOCK / 64];
+  ToiWaveLDS& L = s_toi[threadIdx.x >> 6];
   const LWall* W = S.W;
   Poly pa; make_box(&pa, CAR_HX, CAR_HY);
+  const unsigned long long present = __ballot(1);    // lanes of this wave inside SolveTOI
+  const int prank = rank_in(present), npresent = popc64(present);
+  const int lane = (int)__lane_id();
   c.alpha0 = 0.0f;
   for (int i = 0; i < c.nct; ++i) { c.ct[i].flags &= ~(CT_TOI | CT_ISLAND); c.ct[i].toiCount = 0; c.ct[i].toi = 1.0f; }
+  bool active = true;
   for (;;) {
-    int minC = -1; float minAlpha = 1.0f;
-    for (int i = 0; i < c.nct; ++i) {
-      DContact& ct = c.ct[i];
-      if (!(ct.flags & CT_ENABLED)) continue;
-      if (ct.toiCount > MAX_SUBSTEPS) continue;
-      float alpha = 1.0f;
-      if (ct.flags & CT_TOI) alpha = ct.toi;
-      else {
-        if (!c.awake) continue;
-        float alpha0 = c.alpha0;
-        const LWall& wl = W[ct.wall];
-        if (toi_far(c, &pa, wl)) {
+    // (1) this lane's fresh TOIs of this scan: enabled, under the substep cap, no cached alpha, body awake,
+    // not provably far (toi_far: alpha = 1 without computing)
+    uint32_t need = 0u;   // bit i: contact i needs b2TimeOfImpact
+    if (active && c.awake) {
+      for (int i = 0; i < c.nct; ++i) {
+        DContact& ct = c.ct[i];
+        if (!(ct.flags & CT_ENABLED) || ct.toiCount > MAX_SUBSTEPS || (ct.flags & CT_TOI)) continue;
+        if (toi_far(c, &pa, W[ct.wall])) {
           PCOUNT(13, 1); CCOUNT(c, 3, 1);
-#ifdef NASCAR_TOI_CULL_CHECK   // verification build: run the culled TOI anyway, count TOUCHING outcomes
-          {
-            Poly pb; make_box(&pb, wl.hx, wl.hy);
-            Sweep sA; sA.c0 = c.c0; sA.c = c.c; sA.a0 = c.a0; sA.a = c.a; sA.alpha0 = c.alpha0;
-            Sweep sB; sB.c0 = V(wl.px, wl.py); sB.c = sB.c0; sB.a0 = wl.ang; sB.a = wl.ang; sB.alpha0 = 0.0f;
-            int st; (void)time_of_impact(&st, &pa, sA, &pb, sB, 1.0f);
-            PCOUNT(16, 1);
-            if (st == TOI_TOUCHING) PCOUNT(17, 1);
-          }
-#endif
           ct.toi = 1.0f; ct.flags |= CT_TOI;
-          continue;   // alpha = 1: never below minAlpha
+          continue;
         }
+        need |= 1u << i;
+      }
+    }
+    // (2) the wave's pairs, numbered lane by lane (prefix over the lanes' counts by bit ballots)
+    const int m = __popc(need);
+    int off = 0, total = 0;
+#pragma unroll
+    for (int bit = 0; bit < 5; ++bit) {
+      const unsigned long long b = __ballot((m >> bit) & 1);
+      off += rank_in(b) << bit;
+      total += popc64(b) << bit;
+    }
+    if (m) { L.sw0[lane] = make_float4(c.c0.x, c.c0.y, c.c.x, c.c.y); L.sw1[lane] = make_float4(c.a0, c.a, c.alpha0, 0.0f); }
+    for (int r0 = 0; r0 < total; r0 += TOI_JOBCAP) {   // wave-uniform
+      {
+        uint32_t nb = need; int k = off;
+        while (nb) {
+          const int i = __ffs(nb) - 1; nb &= nb - 1;
+          if (k >= r0 && k < r0 + TOI_JOBCAP) L.job[k - r0] = make_int2(lane | (i << 8), c.ct[i].wall);
+          ++k;
+        }
+      }
+      wave_lds_sync();
+      const int cnt = min(TOI_JOBCAP, total - r0);
+      for (int j = prank; j < cnt; j += npresent) {
+        const int2 jb = L.job[j];
+        const int owner = jb.x & 0xFF;
         PCOUNT(12, 1); CCOUNT(c, 2, 1);
-        Poly pb; make_box(&pb, wl.hx, wl.hy);
-        Sweep sA; sA.c0 = c.c0; sA.c = c.c; sA.a0 = c.a0; sA.a = c.a; sA.alpha0 = c.alpha0;
-        Sweep sB; sB.c0 = V(wl.px, wl.py); sB.c = sB.c0; sB.a0 = wl.ang; sB.a = wl.ang; sB.alpha0 = 0.0f;
-        int state;
-#ifdef NASCAR_PROFILE
-        int pit[2] = {0, 0};
-        unsigned long long pcy[2] = {0, 0};
-        CTIME_BEGIN();
-        float beta = time_of_impact(&state, &pa, sA, &pb, sB, 1.0f, pit, pcy);
-        CTIME_END(c, 10);
-        CCOUNT(c, 14, pcy[0]); CCOUNT(c, 15, pcy[1]);
-#ifdef NASCAR_PROFILE_TOI
-        {   // isolated single-lane latency of the same call (first lane of the active set only), 4 repeats
-          const unsigned long long act = __ballot(1);
-          if ((int)__lane_id() == __ffsll((long long)act) - 1) {
-            const unsigned long long ti0 = __builtin_amdgcn_s_memtime();
-            float acc = 0.0f;
-            for (int rep = 0; rep < 4; ++rep) { int st2; acc += time_of_impact(&st2, &pa, sA, &pb, sB, 1.0f); }
-            const unsigned long long ti1 = __builtin_amdgcn_s_memtime();
-            CCOUNT(c, 13, (ti1 - ti0) / 4 + (acc == 123.0f ? 1 : 0)); CCOUNT(c, 9, 1);
-          }
+        L.res[j] = toi_alpha(L.sw0[owner], L.sw1[owner], W[jb.y]);
+      }
+      wave_lds_sync();
+      {
+        uint32_t nb = need; int k = off;
+        while (nb) {
+          const int i = __ffs(nb) - 1; nb &= nb - 1;
+          if (k >= r0 && k < r0 + TOI_JOBCAP) { c.ct[i].toi = L.res[k - r0]; c.ct[i].flags |= CT_TOI; }
+          ++k;
         }
-#endif
-        CCOUNT(c, 6, pit[0]); CCOUNT(c, 7, pit[1]);
-        if (state == TOI_FAILED) CCOUNT(c, 1, 1000);
-#else
-        float beta = time_of_impact(&state, &pa, sA, &pb, sB, 1.0f);
-#endif
-        if (state == TOI_TOUCHING) alpha = fminb(alpha0 + (1.0f - alpha0) * beta, 1.0f);
-        else alpha = 1.0f;
-        ct.toi = alpha; ct.flags |= CT_TOI;
       }
-      if (alpha < minAlpha) { minC = i; minAlpha = alpha; }
+      wave_lds_sync();   // the next round's pairs overwrite job / res
     }
-    if (minC < 0 || 1.0f - 10.0f * FLT_EPS < minAlpha) break;
-    PCOUNT(15, 1); CCOUNT(c, 4, 1);
-    V2 bc0 = c.c0, bc = c.c; float ba0 = c.a0, ba = c.a, balpha0 = c.alpha0;
-    {
-      float beta = fdiv_cr(minAlpha - c.alpha0, 1.0f - c.alpha0);
-      c.c0 = vadd(c.c0, vmul(beta, vsub(c.c, c.c0)));
-      c.a0 += beta * (c.a - c.a0);
-      c.alpha0 = minAlpha;
-      c.c = c.c0; c.a = c.a0;
-      sync_transform(c);
-    }
-    {
-    CTIME_BEGIN();
-    contact_update(c, minC, W);
-    CTIME_END(c, 12);
-    }
-    c.ct[minC].flags &= ~CT_TOI;
-    ++c.ct[minC].toiCount;
-    if (!(c.ct[minC].flags & CT_ENABLED) || !(c.ct[minC].flags & CT_TOUCH)) {
-      c.ct[minC].flags &= ~CT_ENABLED;
-      c.c0 = bc0; c.c = bc; c.a0 = ba0; c.a = ba; c.alpha0 = balpha0;
-      sync_transform(c);
-      continue;
-    }
-    set_awake(c);
-    int cidx[MAX_ISLAND] = {0, 0, 0, 0, 0, 0, 0, 0}; int n = 0;
-    island_push(cidx, n, minC); c.ct[minC].flags |= CT_ISLAND;
-    {
-    CTIME_BEGIN();
-    for (int i = 0; i < c.nct; ++i) {
-      if (n == MAX_TOI_CONTACTS) break;
-      if (n == MAX_ISLAND) {   // more touching contacts than the island buffer: flag, keep going exactly-as-far-as-possible
-        if (!(c.ct[i].flags & CT_ISLAND)) { c.overflow = 2; }
-        break;
+    // (3) this lane's scan on cached alphas and its event, as Box2D
+    if (active) {
+      int minC = -1; float minAlpha = 1.0f;
+      for (int i = 0; i < c.nct; ++i) {
+        const DContact& ct = c.ct[i];
+        if (!(ct.flags & CT_ENABLED) || ct.toiCount > MAX_SUBSTEPS || !(ct.flags & CT_TOI)) continue;
+        if (ct.toi < minAlpha) { minC = i; minAlpha = ct.toi; }
       }
-      if (c.ct[i].flags & CT_ISLAND) continue;
-      contact_update(c, i, W);
-      if (!(c.ct[i].flags & CT_ENABLED)) continue;
-      if (!(c.ct[i].flags & CT_TOUCH)) continue;
-      c.ct[i].flags |= CT_ISLAND;
-      island_push(cidx, n, i);
+      if (minC < 0 || 1.0f - 10.0f * FLT_EPS < minAlpha) {
+        active = false;
+      } else {
+        PCOUNT(15, 1); CCOUNT(c, 4, 1);
+        V2 bc0 = c.c0, bc = c.c; float ba0 = c.a0, ba = c.a, balpha0 = c.alpha0;
+        {
+          float beta = fdiv_cr(minAlpha - c.alpha0, 1.0f - c.alpha0);
+          c.c0 = vadd(c.c0, vmul(beta, vsub(c.c, c.c0)));
+          c.a0 += beta * (c.a - c.a0);
+          c.alpha0 = minAlpha;
+          c.c = c.c0; c.a = c.a0;
+          sync_transform(c);
+        }
+        {
+        CTIME_BEGIN();
+        contact_update(c, minC, W);
+        CTIME_END(c, 12);
+        }
+        c.ct[minC].flags &= ~CT_TOI;
+        ++c.ct[minC].toiCount;
+        if (!(c.ct[minC].flags & CT_ENABLED) || !(c.ct[minC].flags & CT_TOUCH)) {
+          c.ct[minC].flags &= ~CT_ENABLED;
+          c.c0 = bc0; c.c = bc; c.a0 = ba0; c.a = ba; c.alpha0 = balpha0;
+          sync_transform(c);
+        } else {
+          set_awake(c);
+          int cidx[MAX_ISLAND] = {0, 0, 0, 0, 0, 0, 0, 0}; int n = 0;
+          island_push(cidx, n, minC); c.ct[minC].flags |= CT_ISLAND;
+          {
+          CTIME_BEGIN();
+          for (int i = 0; i < c.nct; ++i) {
+            if (n == MAX_TOI_CONTACTS) break;
+            if (n == MAX_ISLAND) {   // more touching contacts than the island buffer: flag, keep going exactly-as-far-as-possible
+              if (!(c.ct[i].flags & CT_ISLAND)) { c.overflow = 2; }
+              break;
+            }
+            if (c.ct[i].flags & CT_ISLAND) continue;
+            contact_update(c, i, W);
+            if (!(c.ct[i].flags & CT_ENABLED)) continue;
+            if (!(c.ct[i].flags & CT_TOUCH)) continue;
+            c.ct[i].flags |= CT_ISLAND;
+            island_push(cidx, n, i);
+          }
+          CTIME_END(c, 12);
+          }
+          float subdt = (1.0f - minAlpha) * dt;
+          {
+          CTIME_BEGIN();
+          island_solve_toi(c, W, cidx, n, subdt, friction);
+          CTIME_END(c, 11);
+          }
+          sync_fixtures(c);
+          for (int i = 0; i < c.nct; ++i) c.ct[i].flags &= ~(CT_TOI | CT_ISLAND);
+          find_new_contacts(c, S);
+        }
+      }
     }
-    CTIME_END(c, 12);
-    }
-    float subdt = (1.0f - minAlpha) * dt;
-    {
-    CTIME_BEGIN();
-    island_solve_toi(c, W, cidx, n, subdt, friction);
-    CTIME_END(c, 11);
-    }
-    sync_fixtures(c);
-    for (int i = 0; i < c.nct; ++i) c.ct[i].flags &= ~(CT_TOI | CT_ISLAND);
-    find_new_contacts(c, S);
+    if (!__any(active)) break;   // wave-uniform exit
   }
 }
 
