@@ -565,6 +565,26 @@ __device__ inline void contact_update(Car& c, int ci, const LWall* W) {
 }
 
 // b2ContactManager::Collide
+// ------------------------------------------------------------------ wave-cooperative work lists (LDS, per wave)
+// Per-car Box2D work whose size varies by car (a car's TOI pairs) is listed per lane and computed by every
+// present lane of the wave, so a wave's time follows its total work rather than its busiest car.  (The same
+// scheme for b2World::Collide's manifolds was parity-green but measured neutral: 118.5 vs 118.8 us.)
+#define TOI_JOBCAP 128    // b2TimeOfImpact pairs per compute round per wave (more pairs: further rounds)
+struct ToiWaveLDS { float4 sw0[64], sw1[64]; int2 job[TOI_JOBCAP]; float res[TOI_JOBCAP]; };
+union WaveLDS { ToiWaveLDS toi; };
+__shared__ WaveLDS g_wave_lds[SBLOCK / 64];   // model_kernel / rollout_kernel (the Box2D step)
+__device__ __forceinline__ void wave_lds_sync() {   // a wave's LDS writes visible to its later LDS reads
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+__device__ __forceinline__ int popc64(unsigned long long x) { return __popcll(x); }
+// lanes below this one in mask m
+__device__ __forceinline__ int rank_in(unsigned long long m) {
+  const unsigned long long below = __lane_id() == 0 ? 0ull : (~0ull >> (64 - __lane_id()));
+  return popc64(m & below);
+}
+
 __device__ inline void collide(Car& c, const LWall* W) {
   int i = 0;
   while (i < c.nct) {
@@ -591,7 +611,10 @@ struct VC {
 struct BodyState { V2 c; float a; V2 v; float w; };
 // unroll count of the per-contact loops below: full for islands of <= 2 contacts (register-resident), else a loop
 #define UNROLL_SMALL NUNR<NMAX>::v
-template <int NMAX> struct NUNR { static constexpr int v = NMAX <= 2 ? NMAX : 1; };
+#ifndef ISLAND_MID
+#define ISLAND_MID 3     // islands of 3 .. ISLAND_MID contacts also solved register-resident (0: off; 4 measured slower)
+#endif
+template <int NMAX> struct NUNR { static constexpr int v = NMAX <= 2 || NMAX == ISLAND_MID ? NMAX : 1; };
 
 template <int NMAX> __device__ __forceinline__ void cs_init(VC* vc, int n, const Car& c, const int* cidx, const LWall* W, bool warm, float dtRatio) {
 #pragma unroll UNROLL_SMALL   // registers for small islands; the general bound stays a loop
@@ -890,8 +913,14 @@ __device__ inline void solve(Car& c, const WallSet& S, float dt, float dtRatio, 
     island_push(cidx, n, i);
   }
   const float h = dt;
+#if ISLAND_MID
+  const int positionSolved = n <= 2 ? solve_island<2>(c, W, cidx, n, dt, dtRatio, friction)
+                           : n <= ISLAND_MID ? solve_island<ISLAND_MID>(c, W, cidx, n, dt, dtRatio, friction)
+                                             : solve_island<MAX_ISLAND>(c, W, cidx, n, dt, dtRatio, friction);
+#else
   const int positionSolved = n <= 2 ? solve_island<2>(c, W, cidx, n, dt, dtRatio, friction)
                                     : solve_island<MAX_ISLAND>(c, W, cidx, n, dt, dtRatio, friction);
+#endif
   {
     float minSleepTime = FLT_BIG;
     const float linTolSqr = LINEAR_SLEEP_TOL * LINEAR_SLEEP_TOL;
@@ -1204,6 +1233,9 @@ __device__ __forceinline__ void island_solve_toi_n(Car& c, const LWall* W, const
 }
 __device__ inline void island_solve_toi(Car& c, const LWall* W, const int* cidx, int n, float subdt, float friction) {
   if (n <= 2) island_solve_toi_n<2>(c, W, cidx, n, subdt, friction);
+#if ISLAND_MID
+  else if (n <= ISLAND_MID) island_solve_toi_n<ISLAND_MID>(c, W, cidx, n, subdt, friction);
+#endif
   else island_solve_toi_n<MAX_ISLAND>(c, W, cidx, n, subdt, friction);
 }
 
@@ -1259,19 +1291,6 @@ __device__ __forceinline__ bool toi_far(const Car& c, const Poly* pa, const LWal
 // has events, so lanes that are done lend their time to a lane with a long event chain (a car scraping a
 // wall re-scans its 2-5 contacts after each event: sequential on one lane before).  Same alphas, same
 // scan order, same minimum, so the results are Box2D's.
-#define TOI_JOBCAP 128   // pairs per compute round per wave (more pairs: further rounds)
-struct ToiWaveLDS { float4 sw0[64], sw1[64]; int2 job[TOI_JOBCAP]; float res[TOI_JOBCAP]; };
-__device__ __forceinline__ void wave_lds_sync() {   // a wave's LDS writes visible to its later LDS reads
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-__device__ __forceinline__ int popc64(unsigned long long x) { return __popcll(x); }
-// lanes below this one in mask m
-__device__ __forceinline__ int rank_in(unsigned long long m) {
-  const unsigned long long below = __lane_id() == 0 ? 0ull : (~0ull >> (64 - __lane_id()));
-  return popc64(m & below);
-}
 // b2TimeOfImpact of the car's sweep against static wall wl -> alpha of SolveTOI (1 unless TOUCHING)
 __device__ __forceinline__ float toi_alpha(float4 s0, float4 s1, const LWall& wl) {
   Poly pa; make_box(&pa, CAR_HX, CAR_HY);
@@ -1283,8 +1302,7 @@ __device__ __forceinline__ float toi_alpha(float4 s0, float4 s1, const LWall& wl
   return state == TOI_TOUCHING ? fminb(s1.z + (1.0f - s1.z) * beta, 1.0f) : 1.0f;
 }
 __device__ inline void solve_toi(Car& c, const WallSet& S, float dt, float friction) {
-  __shared__ ToiWaveLDS s_toi[SBLOCK / 64];
-  ToiWaveLDS& L = s_toi[threadIdx.x >> 6];
+  ToiWaveLDS& L = g_wave_lds[threadIdx.x >> 6].toi;
   const LWall* W = S.W;
   Poly pa; make_box(&pa, CAR_HX, CAR_HY);
   const unsigned long long present = __ballot(1);    // lanes of this wave inside SolveTOI
