@@ -75,6 +75,9 @@ struct BeamGrid {
 #define BEAM_HW 2
 #endif
 #define BEAM_HEAD (4 * BEAM_HW - 1)
+#ifndef RAY_CHUNK
+#define RAY_CHUNK 4    // list entries past the head requested together
+#endif
 #define BEAM_PAD 0xFFFFFFFFu   // bound 655.35 m: past every best hit (<= 2 * 250 m), so a walk always stops on it
 struct BeamHead { uint4 w[BEAM_HW]; };
 __device__ __forceinline__ BeamHead beam_head(const BeamGrid& G, int li) {
@@ -1259,13 +1262,13 @@ __device__ __forceinline__ float ray_walk(const BeamGrid& G, const float4* __res
   if (more && tail != 0u) {
     const uint32_t s0 = tail & 0x0FFFFFFFu, c = tail >> 28;
     const uint32_t e0 = c < 15u ? s0 + c : G.start[li + 1];
-    for (uint32_t k = s0; k < e0; k += 4) {   // 4 entries requested together, walked in order
-      uint32_t v4[4];
+    for (uint32_t k = s0; k < e0; k += RAY_CHUNK) {   // RAY_CHUNK entries requested together, walked in order
+      uint32_t v4[RAY_CHUNK];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) v4[q] = k + q < e0 ? G.ent[k + q] : BEAM_PAD;
+      for (int q = 0; q < RAY_CHUNK; ++q) v4[q] = k + q < e0 ? G.ent[k + q] : BEAM_PAD;
       bool stop = false;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
+      for (int q = 0; q < RAY_CHUNK; ++q) {
         const uint32_t v = v4[q];
         if ((float)(v >> 16) * 0.01f > bi * 250.0f * 1.00001f + 0.01f) { stop = true; break; }
         const int j = (int)(v & 0xFFFFu);
