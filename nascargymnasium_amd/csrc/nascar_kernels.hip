@@ -2585,6 +2585,7 @@ static int prepare(NascarHandle* h) {
 
 static Params make_params(NascarHandle* h) {
   Params P;
+  memset(&P, 0, sizeof P);   // padding too: nascar_rollout compares the bytes before re-uploading
   P.E = h->E; P.C = h->C; P.N = h->N; P.epb = h->epb; P.nblocks = h->nblocks; P.reset_on_lap = h->cfg.reset_on_lap;
   P.dt_d = 1.0 / 60.0; P.dt_f = (float)P.dt_d;
   P.friction = sqrtf(0.7f * 0.333f);
