@@ -502,28 +502,35 @@ __device__ inline void car_update_physics(const Params& P, Car& c, int n, const 
     double lon = ax * fwd.x + ay * fwd.y, lat = ax * rtx + ay * rty;
     lon = pymax(-12.0, pymin(12.0, lon));
     lat = pymax(-12.0, pymin(12.0, lat));
-    // history kept oldest-first in HBM (acc_head stays 0): load the 10 slots (independent loads,
-    // issued together), shift/append in registers, sum oldest -> newest like Python's sum(), store back
+    // history as a ring in HBM (acc_head = slot of the oldest sample): the 10 slots are loaded oldest-first
+    // (independent loads, issued together), the new sample is appended in registers and summed oldest ->
+    // newest like Python's sum(), and only its slot is written back (16 B per car-step, not the whole deque)
     double* acc = P.acc;
     const size_t N = P.N;
+    const int h0 = c.acc_head;
     double hl[10], ht[10];
 #pragma unroll
-    for (int q = 0; q < 10; ++q) { hl[q] = acc[(size_t)(2 * q) * N + n]; ht[q] = acc[(size_t)(2 * q + 1) * N + n]; }
-    if (c.acc_len == 10) {
+    for (int q = 0; q < 10; ++q) {
+      const int sq = h0 + q < 10 ? h0 + q : h0 + q - 10;
+      hl[q] = acc[(size_t)(2 * sq) * N + n]; ht[q] = acc[(size_t)(2 * sq + 1) * N + n];
+    }
+    int wslot;
+    if (c.acc_len == 10) {   // deque(maxlen=10).append: the oldest sample drops out
 #pragma unroll
       for (int q = 0; q < 9; ++q) { hl[q] = hl[q + 1]; ht[q] = ht[q + 1]; }
       hl[9] = lon; ht[9] = lat;
+      wslot = h0;
+      c.acc_head = h0 + 1 < 10 ? h0 + 1 : 0;
     } else {
 #pragma unroll
       for (int q = 0; q < 10; ++q) if (q == c.acc_len) { hl[q] = lon; ht[q] = lat; }
+      wslot = h0 + c.acc_len < 10 ? h0 + c.acc_len : h0 + c.acc_len - 10;
       c.acc_len++;
     }
-    c.acc_head = 0;
     double s0 = 0.0, s1 = 0.0;
 #pragma unroll
     for (int q = 0; q < 10; ++q) if (q < c.acc_len) { s0 += hl[q]; s1 += ht[q]; }
-#pragma unroll
-    for (int q = 0; q < 10; ++q) { acc[(size_t)(2 * q) * N + n] = hl[q]; acc[(size_t)(2 * q + 1) * N + n] = ht[q]; }
+    acc[(size_t)(2 * wslot) * N + n] = lon; acc[(size_t)(2 * wslot + 1) * N + n] = lat;
     alon = s0 / c.acc_len; alat = s1 / c.acc_len;
     DBG(n, 6, alon); DBG(n, 7, alat);
 
