@@ -4,7 +4,7 @@
 #   tools/kt_ss.sh ab/a.so ab/b.so ...
 ROOT="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 mkdir -p "$ROOT/gpurun_out"
-timeout -k 10 300 python "$ROOT/bench.py" --save-state /tmp/nascar_ss.pt --no-cpu-baseline --no-secondary --steps 20 \
+timeout -k 10 300 python "$ROOT/bench.py" --save-state /tmp/nascar_ss.pt --no-cpu-baseline --no-secondary --steps 20 $BENCH_ARGS \
     > "$ROOT/gpurun_out/kt_ss_settle.log" 2>&1 || exit 1
 cd /tmp && export TMPDIR=/tmp
 for L in "$@"; do
