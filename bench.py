@@ -149,8 +149,10 @@ class Stepper:
         return self.env.policy_actions(self.pol, seed=self.seed, step=i)
 
     def __call__(self, i):
-        a = self.actions(i)
-        self.env.launch_step(a, auto_reset=True)
+        if self.acts is None and self.pol != 2:   # device driver computed inside the step launch (nascar_step_driven)
+            self.env.step_driven(self.pol, seed=self.seed, step=i, auto_reset=True)
+        else:
+            self.env.launch_step(self.actions(i), auto_reset=True)
         if self.gather is not None:
             self.gather.push(self.env.obs, self.env.reward, self.env.car_flags, self.env.env_flags)
 

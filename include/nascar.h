@@ -70,6 +70,12 @@ int nascar_reset(NascarHandle* h, const uint8_t* env_mask, float* obs, void* str
 int nascar_step(NascarHandle* h, const void* actions, int32_t discrete, float* obs, float* reward,
                 uint8_t* car_flags, uint8_t* env_flags, int32_t auto_reset, float* terminal_obs, void* stream);
 
+/* nascar_step with the actions of device action source `policy` (0, 1, 3: see nascar_policy_actions) computed on
+ * the current obs inside the step launch -- one closed-loop driver step (game/control drivers' loop) without a
+ * separate action launch; identical results to nascar_policy_actions(policy, seed, step) + nascar_step. */
+int nascar_step_driven(NascarHandle* h, int32_t policy, uint64_t seed, int64_t step, float* obs, float* reward,
+                       uint8_t* car_flags, uint8_t* env_flags, int32_t auto_reset, float* terminal_obs, void* stream);
+
 /* Fused multi-step rollout: `steps` x (device action source on the current obs + CarEnv.step), i.e. the loop
  * of game/control drivers / learn/genetic_trainer.py:225-283 evaluation rollouts (actions from a policy on the
  * previous observation, src/car_env.py:678-803 per step), in one launch.  Identical results to `steps` calls of

@@ -74,6 +74,8 @@ def lib():
     L.nascar_reset.restype = ctypes.c_int
     L.nascar_step.argtypes = [vp, vp, i32, vp, vp, vp, vp, i32, vp, vp]
     L.nascar_step.restype = ctypes.c_int
+    L.nascar_step_driven.argtypes = [vp, i32, u64, i64, vp, vp, vp, vp, i32, vp, vp]
+    L.nascar_step_driven.restype = ctypes.c_int
     L.nascar_rollout.argtypes = [vp, i32, u64, i64, i32, vp, vp, vp, vp, i32, i32, vp]
     L.nascar_rollout.restype = ctypes.c_int
     L.nascar_set_car_contact.argtypes = [vp, i32]
@@ -106,7 +108,7 @@ def lib():
 
 
 EXPORTED = ["nascar_create", "nascar_destroy", "nascar_last_error", "nascar_add_track", "nascar_set_env_tracks",
-            "nascar_reset", "nascar_step", "nascar_rollout", "nascar_get_info", "nascar_set_perf_history", "nascar_set_car_contact", "nascar_state_bytes", "nascar_get_state",
+            "nascar_reset", "nascar_step", "nascar_step_driven", "nascar_rollout", "nascar_get_info", "nascar_set_perf_history", "nascar_set_car_contact", "nascar_state_bytes", "nascar_get_state",
             "nascar_set_state", "nascar_policy_actions", "nascar_set_actor", "nascar_set_actor_precision", "nascar_actor_forward",
             "nascar_debug_sincosf", "nascar_debug_sensors"]
 

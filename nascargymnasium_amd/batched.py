@@ -139,6 +139,16 @@ class BatchedCarEnv:
                                           _ptr(self.car_flags), _ptr(self.env_flags), int(auto_reset),
                                           _ptr(self.terminal_obs) if terminal_obs else None, _stream()))
 
+    def step_driven(self, policy: int, seed: int = 0, step: int = 0, auto_reset: bool = True, terminal_obs: bool = False):
+        """One env step whose actions come from device action source `policy` (0 uniform, 1 rule driver, 3 noisy rule
+        driver) on the current obs, computed inside the step launch; equals policy_actions(policy, seed, step) +
+        step(...)."""
+        with torch.cuda.device(self.device):
+            _lib.check(self.L.nascar_step_driven(self.h, int(policy), int(seed), int(step), _ptr(self.obs), _ptr(self.reward),
+                                                 _ptr(self.car_flags), _ptr(self.env_flags), int(auto_reset),
+                                                 _ptr(self.terminal_obs) if terminal_obs else None, _stream()))
+        return self.obs, self.reward
+
     def rollout(self, policy: int, steps: int, seed: int = 0, step0: int = 0, auto_reset: bool = True,
                 trajectory: bool = False, out=None):
         """`steps` env steps in one fused launch, actions from device action source `policy` (0 uniform, 1 rule

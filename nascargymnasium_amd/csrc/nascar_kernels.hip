@@ -1533,7 +1533,10 @@ __device__ __forceinline__ void model_car(const Params& P, Car& c, int n, const 
 #ifndef MODEL_WPE
 #define MODEL_WPE 2   // 256 VGPRs + 40 spilled (vs 256 + 44 AGPRs at 1 wave/SIMD): 103.6 -> 100.6 us/step
 #endif
-__global__ void __launch_bounds__(SBLOCK) __attribute__((amdgpu_waves_per_eu(MODEL_WPE))) model_kernel(Params P, const void* actions, int discrete, int want_term) {
+// policy >= 0: the actions come from device action source `policy` (policy_car, nascar_step_driven) on the
+// current obs instead of the actions buffer -- the closed-loop driver's step without a policy_kernel launch
+__global__ void __launch_bounds__(SBLOCK) __attribute__((amdgpu_waves_per_eu(MODEL_WPE))) model_kernel(Params P, const void* actions, int discrete, int want_term,
+                                                                                                    int policy, uint64_t seed, int64_t step, const float* pobs) {
   const int tid = threadIdx.x, C = P.C;
   const int el = tid / C, car = tid - el * C;
   const int slot = blockIdx.x * P.epb + el;
@@ -1549,7 +1552,9 @@ __global__ void __launch_bounds__(SBLOCK) __attribute__((amdgpu_waves_per_eu(MOD
   c.pid = n;
   // actions (BaseEnv._convert_to_internal_action / _discrete_to_continuous, np.float32)
   float tb = 0.0f, st = 0.0f;
-  if (env >= 0) {
+  if (env >= 0 && policy >= 0) {
+    policy_car(policy, seed, step, n, pobs, P.ctl, tb, st);
+  } else if (env >= 0) {
     if (discrete) {
       int a = ((const int*)actions)[n];
       tb = a == 1 ? 1.0f : (a == 2 ? -1.0f : 0.0f);
@@ -2649,9 +2654,24 @@ extern "C" int nascar_reset(NascarHandle* h, const uint8_t* env_mask, float* obs
   return 0;
 }
 
+static int step_impl(NascarHandle* h, const void* actions, int32_t discrete, int policy, uint64_t seed, int64_t step,
+                     float* obs, float* reward, uint8_t* car_flags, uint8_t* env_flags, int32_t auto_reset,
+                     float* terminal_obs, void* stream);
 extern "C" int nascar_step(NascarHandle* h, const void* actions, int32_t discrete, float* obs, float* reward,
                            uint8_t* car_flags, uint8_t* env_flags, int32_t auto_reset, float* terminal_obs, void* stream) {
   if (!h || !actions || !obs || !reward) return fail("null argument");
+  return step_impl(h, actions, discrete, -1, 0, 0, obs, reward, car_flags, env_flags, auto_reset, terminal_obs, stream);
+}
+extern "C" int nascar_step_driven(NascarHandle* h, int32_t policy, uint64_t seed, int64_t step, float* obs, float* reward,
+                                  uint8_t* car_flags, uint8_t* env_flags, int32_t auto_reset, float* terminal_obs,
+                                  void* stream) {
+  if (!h || !obs || !reward) return fail("null argument");
+  if (policy != 0 && policy != 1 && policy != 3) return fail("driven step policy must be 0, 1 or 3 (got %d)", policy);
+  return step_impl(h, nullptr, 0, policy, seed, step, obs, reward, car_flags, env_flags, auto_reset, terminal_obs, stream);
+}
+static int step_impl(NascarHandle* h, const void* actions, int32_t discrete, int policy, uint64_t seed, int64_t step,
+                     float* obs, float* reward, uint8_t* car_flags, uint8_t* env_flags, int32_t auto_reset,
+                     float* terminal_obs, void* stream) {
   h->pristine = false;
   if (prepare(h)) return -1;
   Params P = make_params(h);
@@ -2659,7 +2679,8 @@ extern "C" int nascar_step(NascarHandle* h, const void* actions, int32_t discret
   // Kept on the caller's stream: a cross-stream event hop measured 10-15 us on the MI355X box, more than
   // running logic_kernel and sensor pass A concurrently would save.
   hipStream_t s = (hipStream_t)stream;
-  hipLaunchKernelGGL(model_kernel, dim3(h->nblocks), dim3(SBLOCK), 0, s, P, actions, discrete, terminal_obs != nullptr);
+  hipLaunchKernelGGL(model_kernel, dim3(h->nblocks), dim3(SBLOCK), 0, s, P, actions, discrete, terminal_obs != nullptr,
+                     policy, seed, step, (const float*)obs);
   HIPCHK(hipGetLastError());
   if (h->car_contact) {
     hipLaunchKernelGGL(car_contact_kernel, dim3(h->nblocks), dim3(SBLOCK), 0, s, P);

@@ -67,3 +67,17 @@ def test_rollout_last_step_outputs_and_errors():
     with pytest.raises(RuntimeError):
         env.rollout(2, 5)                        # the SAC actor is not a rollout action source
     env.close()
+
+
+@pytest.mark.parametrize("policy", [0, 1, 3])
+def test_step_driven_equals_policy_plus_step(policy):
+    """nascar_step_driven (device action source inside the step launch) == nascar_policy_actions + nascar_step."""
+    a, b = _engine(["daytona.track"], 48, 10), _engine(["daytona.track"], 48, 10)
+    a.reset(); b.reset()
+    for k in range(300):
+        a.launch_step(a.policy_actions(policy, seed=4, step=k).clone(), auto_reset=True)
+        b.step_driven(policy, seed=4, step=k, auto_reset=True)
+        assert torch.equal(a.obs, b.obs) and torch.equal(a.reward, b.reward), k
+        assert torch.equal(a.car_flags, b.car_flags) and torch.equal(a.env_flags, b.env_flags), k
+    assert torch.equal(a.get_state(), b.get_state())
+    a.close(); b.close()
