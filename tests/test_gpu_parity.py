@@ -116,7 +116,8 @@ def _random_actions(rng, E, C, k):
 
 
 @pytest.mark.parametrize("track,E,C,steps", [("daytona.track", 48, 3, 1500), ("martinsville.track", 32, 2, 1500),
-                                              ("talladega.track", 16, 10, 600), ("michigan.track", 40, 1, 1200)])
+                                              ("talladega.track", 16, 10, 600), ("michigan.track", 40, 1, 1200),
+                                              ("daytona.track", 64, 4, 1000)])   # cfg4's car count
 def test_random_batch_vs_oracle(track, E, C, steps):
     """Seeded random driving (crashes, disables, stuck cars) on E x C cars: GPU == CPU oracle, every step."""
     from oracle_lib import OracleEnv
