@@ -1301,16 +1301,18 @@ __device__ __forceinline__ void ray_lane(const Params& P, const TrackDev& T, con
   constexpr int RPL = 16 / RAY_LPC;
   // pose loads after the staging barrier: issuing them (and pass A's cos/sin) before it, or the beam-cell
   // lookup too, measured 2.5 / 9 us slower (registers held across the staging)
+  // each pass loads its own pose (pass B's only for auto-reset cars): no pose is held across the other pass's
+  // walks (held, both had been spilled to scratch at 80 VGPRs); pass B's mode word is read up front
   int mode = 0;
-  float4 pa = make_float4(0.f, 0.f, 0.f, 0.f), pb = pa;
-  if (passes & 1) { pa = P.pose[n]; mode = __float_as_int(pa.w) & (PM_A_OBS | PM_A_TERM); }
-  if (passes & 2) { pb = P.pose[P.N + n]; mode |= __float_as_int(pb.w) & PM_B_OBS; }
+  if (passes & 2) mode = __float_as_int(P.pose[P.N + n].w) & PM_B_OBS;
   const BeamGrid G = T.beam;
 #pragma unroll 1
   for (int pass = 0; pass < 2; ++pass) {
-    const bool active = pass == 0 ? (mode & (PM_A_OBS | PM_A_TERM)) != 0 : (mode & PM_B_OBS) != 0;
-    if (!active) continue;
-    const float4 ps = pass == 0 ? pa : pb;
+    if (pass == 0 && !(passes & 1)) continue;
+    if (pass == 1 && !(mode & PM_B_OBS)) continue;
+    const float4 ps = P.pose[pass == 0 ? (size_t)n : (size_t)P.N + n];
+    if (pass == 0) mode |= __float_as_int(ps.w) & (PM_A_OBS | PM_A_TERM);
+    if (pass == 0 && !(mode & (PM_A_OBS | PM_A_TERM))) continue;
     const V2 p1 = V(ps.x, ps.y);
     const double px = ps.x, py = ps.y, ang = ps.z;
     const double2 cs = P.pose_cs[pass == 0 ? (size_t)n : (size_t)P.N + n];
