@@ -1333,7 +1333,9 @@ __device__ __forceinline__ void ray_lane(const Params& P, const TrackDev& T, con
     for (int q = 0; q < RPL; ++q) {
       const int i = r + RAY_LPC * q;
       double dxd, dyd;
-      const V2 p2 = ray_end(P, px, py, ang, cs.x, cs.y, i, dxd, dyd);
+      float fx = ps.x, fy = ps.y, fa = ps.z;   // widened per ray: three floats live across the walks, not three doubles
+      asm volatile("" : "+v"(fx), "+v"(fy), "+v"(fa));
+      const V2 p2 = ray_end(P, (double)fx, (double)fy, (double)fa, cs.x, cs.y, i, dxd, dyd);
       const float dx = (p2.x - p1.x) * 0.004f, dy = (p2.y - p1.y) * 0.004f;   // cull only
       float bi = 2.0f;
       if (base >= 0) {
@@ -1346,9 +1348,13 @@ __device__ __forceinline__ void ray_lane(const Params& P, const TrackDev& T, con
       PCOUNT(8, 1);
       put4(v, q, sensor_value(bi));
     }
+    // lane index and car index made opaque here, so the transpose indices and the store addresses derived from
+    // them are computed now rather than held (spilled) across the walks
+    int rq = r, nq = n;
+    asm volatile("" : "+v"(rq), "+v"(nq));
     float o[4];
-    quad_transpose(v, o, r);
-    const size_t at = (size_t)n * 38 + 22 + 4 * r;   // 8-byte aligned (rows are 152 B)
+    quad_transpose(v, o, rq);
+    const size_t at = (size_t)nq * 38 + 22 + 4 * rq;   // 8-byte aligned (rows are 152 B)
     const float2 lo = make_float2(o[0], o[1]), hi = make_float2(o[2], o[3]);
     if (pass == 1 || (mode & PM_A_OBS)) { *(float2*)(obs + at) = lo; *(float2*)(obs + at + 2) = hi; }
     if (pass == 0 && (mode & PM_A_TERM)) { *(float2*)(terminal_obs + at) = lo; *(float2*)(terminal_obs + at + 2) = hi; }
