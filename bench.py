@@ -275,9 +275,12 @@ def main():
     ap.add_argument("--no-stagger", action="store_true", help="all envs start together (no staggered resets)")
     ap.add_argument("--save-state", default=None, help="write the settled state (engine arena + obs) to this file")
     ap.add_argument("--load-state", default=None, help="start from a state written by --save-state (no settle)")
-    ap.add_argument("--rollout", type=int, default=0,
-                    help="steps per fused nascar_rollout launch for the device action sources (0: per-step path, "
-                         "nascar_policy_actions + nascar_step per step)")
+    ap.add_argument("--rollout", type=int, default=50,
+                    help="steps per nascar_rollout call for the device action sources (default 50: the sharded rollout, "
+                         "bit-identical to the per-step path, which is timed beside it); 0: per-step path only "
+                         "(nascar_step_driven per step)")
+    ap.add_argument("--rollout-streams", type=int, default=None,
+                    help="shards (internal streams) of the --rollout path; 0: the fused rollout kernel (default: engine's 4)")
     ap.add_argument("--mixed", action="store_true", help="env e on track e mod 8 of the sorted bundled tracks "
                     "(BASELINE cfg5: mixed batch, divergent geometry); --track is ignored")
     ap.add_argument("--gather", action="store_true", help="gather every step's obs/reward/flags of all ranks to "
@@ -317,6 +320,8 @@ def main():
         return BatchedCarEnv(E, C, tpath, device=dev)
 
     env = make_env()
+    if args.rollout_streams is not None:
+        env.set_rollout_streams(args.rollout_streams)
     if args.car_contact:
         env.set_car_contact(True)
     gather = None
@@ -339,8 +344,8 @@ def main():
         env.set_state(blob["state"])
         env.obs.copy_(blob["obs"])
         base = int(blob["step"])
-    else:
-        settle(env, step, S, closed and not args.no_stagger, dev)
+    else:   # per-step settle whatever the timed path: each staggered reset lands on its exact step
+        settle(env, Stepper(env, args.policy, rank, acts, None, 0), S, closed and not args.no_stagger, dev)
         base = S
     torch.cuda.synchronize()
     t_settle = time.perf_counter() - t_settle
@@ -353,7 +358,15 @@ def main():
     elapsed = timed(step, base + W, K, world)
     KR = min(K, 50)
     kern_ms, tally = stats_pass(env, step, base + W + K, KR)
+    per_step = None
+    if step.R:   # the per-step path on the same envs, timed the same way (labelled secondary)
+        ps = Stepper(env, args.policy, rank, acts, None, 0)
+        first = base + W + K + 2 * KR
+        ps.run(first, W)
+        per_step = timed(ps, first + W, K, world)
     elapsed, kern_ms = reduce_max([elapsed, kern_ms], dev)
+    if per_step is not None:
+        per_step = reduce_max([per_step], dev)[0]
     tally = reduce_sum(tally, dev)
     value = throughput(world, E, C, K, elapsed)
     achieved = E * C * ALGO_BYTES_PER_CAR_STEP / (kern_ms * 1e-3) / 1e9
@@ -381,6 +394,18 @@ def main():
     settle_txt = (f", steady state after {S} settle steps" + (" (env ages staggered over the 180 s episode)"
                   if closed and not args.no_stagger else "")) if S else (", from a saved steady state" if args.load_state
                                                                         else ", from reset")
+    nshard = env.rollout_streams if step.R else 0
+    if not step.R:
+        launch_txt = "per-step kernels (nascar_step_driven)"
+        kernel_txt = "model_kernel + logic_kernel + ray_sensor_kernel (one env step)"
+    elif nshard == 0:
+        launch_txt = f"fused rollout kernel, {step.R} steps per launch"
+        kernel_txt = f"rollout_kernel ({step.R} fused env steps per launch; per-step time)"
+    else:
+        launch_txt = (f"sharded rollout: {step.R} steps per nascar_rollout call, envs in {nshard} shards on {nshard} "
+                      f"streams (bit-identical to the per-step path)")
+        kernel_txt = (f"model_kernel + logic_kernel + ray_sensor_kernel over {nshard} env shards on {nshard} streams "
+                      f"(per-step time of a {step.R}-step rollout, HIP events on the caller's stream)")
     out = {
         "metric": "env-steps/sec (cars x envs), daytona 10-car",
         "value": value, "unit": "car-steps/s", "n_gpus": world, "steps": K, "warmup": W,
@@ -389,18 +414,21 @@ def main():
         "config": {"workload": f"{track_name} {C}-car: {E} envs x {C} cars per GPU, {POLICY_TEXT[args.policy]}"
                                f"{settle_txt}, auto-reset",
                    "envs_per_gpu": E, "cars_per_env": C, "policy": args.policy,
-                   "launch": f"fused rollout, {step.R} steps per launch" if step.R else "per-step kernels",
+                   "launch": launch_txt,
                    "car_contact": "on (build-only extension, no reference counterpart)" if args.car_contact else "off (reference)",
                    "track": "mixed (env e: track e mod 8)" if args.mixed else os.path.basename(tpath),
                    "parallelism": f"dp{world} (env shards" + (", RCCL gather of obs/reward/flags to rank 0 per step)" if gather else ", no collective)")},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": tnote,
-                     "kernel": (f"rollout_kernel ({step.R} fused env steps per launch; per-step time)" if step.R else
-                                "model_kernel + logic_kernel + ray_sensor_kernel (one env step)"), "kernel_ms": kern_ms,
+                     "kernel": kernel_txt, "kernel_ms": kern_ms,
                      "algo_bytes_per_car_step": ALGO_BYTES_PER_CAR_STEP},
         "workload_stats": wstats,
         "engine_errors": int(tally[5]),
     }
+    if per_step is not None:
+        out["per_step"] = {"value": throughput(world, E, C, K, per_step), "ms_per_step": per_step / K * 1e3,
+                           "note": "secondary: the same envs and driver stepped by one whole-batch launch per step "
+                                   "(nascar_step_driven), every step waiting for the batch's slowest car"}
     if not args.no_secondary and args.policy != "uniform" and not args.gather:
         # secondary, labelled: round 1's workload (uniform U[-1,1]^2 from reset) on a fresh engine
         del step

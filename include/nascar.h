@@ -76,10 +76,12 @@ int nascar_step(NascarHandle* h, const void* actions, int32_t discrete, float* o
 int nascar_step_driven(NascarHandle* h, int32_t policy, uint64_t seed, int64_t step, float* obs, float* reward,
                        uint8_t* car_flags, uint8_t* env_flags, int32_t auto_reset, float* terminal_obs, void* stream);
 
-/* Fused multi-step rollout: `steps` x (device action source on the current obs + CarEnv.step), i.e. the loop
+/* Multi-step rollout: `steps` x (device action source on the current obs + CarEnv.step), i.e. the loop
  * of game/control drivers / learn/genetic_trainer.py:225-283 evaluation rollouts (actions from a policy on the
- * previous observation, src/car_env.py:678-803 per step), in one launch.  Identical results to `steps` calls of
- * nascar_policy_actions(policy, seed, step0 + k) + nascar_step(auto_reset).
+ * previous observation, src/car_env.py:678-803 per step), enqueued in one call with no host synchronisation.
+ * Identical results to `steps` calls of nascar_policy_actions(policy, seed, step0 + k) + nascar_step(auto_reset).
+ * Default implementation: the envs split into shards stepped on internal streams, forked from `stream` at the
+ * start and joined into it at the end (nascar_set_rollout_streams); streams = 0 selects one fused launch.
  *   policy:  0 uniform, 1 BaseController._fallback_control, 3 noisy rule driver (policy 1 with 15 % of the
  *            car-steps uniform) -- see nascar_policy_actions
  *   obs:     [E*C*38] float32, in: the current observation, out: the last step's
@@ -88,6 +90,15 @@ int nascar_step_driven(NascarHandle* h, int32_t policy, uint64_t seed, int64_t s
  * car_flags / env_flags may be NULL.  No terminal observations (auto-reset obs overwrite the final ones). */
 int nascar_rollout(NascarHandle* h, int32_t policy, uint64_t seed, int64_t step0, int32_t steps, float* obs,
                    float* reward, uint8_t* car_flags, uint8_t* env_flags, int32_t auto_reset, int32_t traj, void* stream);
+
+/* Rollout implementation (no reference counterpart: a scheduling choice with identical results).
+ * streams >= 1: the envs split into `streams` shards of contiguous workgroups, each stepped by per-step launches
+ * on its own stream (shard 0 on the caller's), so one shard's slow cars overlap the other shards' work; default:
+ * one shard per hardware queue of the process (GPU_MAX_HW_QUEUES, HIP's default 4);
+ * streams = 0: the fused rollout kernel (all steps in one launch, block barriers between the phases).
+ * nascar_get_rollout_streams returns the current setting (-1 for a NULL handle). */
+int nascar_set_rollout_streams(NascarHandle* h, int32_t streams);
+int nascar_get_rollout_streams(NascarHandle* h);
 
 /* Info builder (src/car_env.py:1160-1227, src/lap_timer.py:354-372): per-car float64 [E*C*N_INFO]
  * (field order: nascargymnasium_amd/_lib.py INFO_FIELDS) written to a device buffer. */

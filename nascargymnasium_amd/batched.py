@@ -76,6 +76,17 @@ class BatchedCarEnv:
         grid, central impulses between overlapping closing car boxes).  Off by default; parity holds only when off."""
         _lib.check(self.L.nascar_set_car_contact(self.h, int(bool(enable))))
 
+    def set_rollout_streams(self, streams: int = 4):
+        """How `rollout` schedules its steps (identical results either way): streams >= 1 splits the envs into that
+        many shards, each stepped on its own stream (shard 0 on the current one), so one shard's slow cars (Box2D
+        TOI chains) overlap the other shards' work (default: one per hardware queue, GPU_MAX_HW_QUEUES, 4); 0 runs
+        all steps in one fused launch."""
+        _lib.check(self.L.nascar_set_rollout_streams(self.h, int(streams)))
+
+    @property
+    def rollout_streams(self) -> int:
+        return int(self.L.nascar_get_rollout_streams(self.h))
+
     def set_perf_history(self, enable: bool = True):
         """Keep Car.velocity_history on the device so the info's `performance` dict is Car.validate_performance
         (src/car.py:1060-1098); a 640-sample float32 ring per car, one 4-byte store per car-step.  The window starts

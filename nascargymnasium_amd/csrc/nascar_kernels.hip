@@ -115,6 +115,7 @@ struct Params {
   // block map shortcuts (prepare()): map_identity = blk_env[s] is s (< E) or -1, one_track >= 0 = every
   // block's track; they spare each kernel's first dependent load
   int map_identity, one_track;
+  int blk0;            // first step-kernel workgroup of this launch (sharded rollout, nascar_set_rollout_streams); else 0
 };
 __device__ __forceinline__ int blk_env_of(const Params& P, int el, int s) {
   if (el >= P.epb) return -1;
@@ -981,7 +982,7 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(SENS
   __shared__ unsigned s_best[CPW * 16];     // [car][ray]: best fraction so far (float bits, >= 0)
   float4* swa = (float4*)smem;
   constexpr int SUB = (SBLOCK + CPW - 1) / CPW;   // sensor workgroups per step-kernel workgroup
-  const int b = blockIdx.x / SUB, sub = blockIdx.x - b * SUB;
+  const int bx = blockIdx.x, b = bx / SUB + P.blk0, sub = bx % SUB;
   const int t = threadIdx.x, lc = t / LPC, r = t - lc * LPC;
   const int C = P.C;
   const int slot = sub * CPW + lc;          // car slot within the step kernel's workgroup b
@@ -1445,7 +1446,7 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(RSEN
 ray_sensor_kernel(Params P, float* obs, float* terminal_obs, int passes) {
   constexpr int CPW = BLOCK / RAY_LPC;
   constexpr int SUB = (SBLOCK + CPW - 1) / CPW;   // sensor workgroups per step-kernel workgroup
-  const int b = blockIdx.x / SUB, sub = blockIdx.x - b * SUB;
+  const int bx = blockIdx.x, b = bx / SUB + P.blk0, sub = bx % SUB;
   const int t = threadIdx.x, lc = t / RAY_LPC, r = t - lc * RAY_LPC;
   const int C = P.C;
   const int slot = sub * CPW + lc;
@@ -1547,7 +1548,7 @@ __global__ void __launch_bounds__(SBLOCK) __attribute__((amdgpu_waves_per_eu(MOD
                                                                                                     int policy, uint64_t seed, int64_t step, const float* pobs) {
   const int tid = threadIdx.x, C = P.C;
   const int el = tid / C, car = tid - el * C;
-  const int slot = blockIdx.x * P.epb + el;
+  const int slot = (blockIdx.x + P.blk0) * P.epb + el;
   const int env = blk_env_of(P, el, slot);
   const int n = env >= 0 ? env * C + car : 0;
   PROF_RT(14);
@@ -1571,7 +1572,7 @@ __global__ void __launch_bounds__(SBLOCK) __attribute__((amdgpu_waves_per_eu(MOD
       tb = ((const float*)actions)[2 * n]; st = ((const float*)actions)[2 * n + 1];
     }
   }
-  TrackDev T = P.tracks[blk_track_of(P, blockIdx.x)];
+  TrackDev T = P.tracks[blk_track_of(P, (blockIdx.x + P.blk0))];
   if (tid < T.nseg) s_segs[tid] = T.segs[tid];
   __syncthreads();
   T.segs = s_segs;
@@ -1866,7 +1867,7 @@ __device__ __forceinline__ void car_contact_block(const Params& P, int tid, int 
 __global__ void __launch_bounds__(SBLOCK) car_contact_kernel(Params P) {
   const int tid = threadIdx.x, C = P.C;
   const int el = tid / C, car = tid - el * C;
-  const int env = blk_env_of(P, el, blockIdx.x * P.epb + el);
+  const int env = blk_env_of(P, el, (blockIdx.x + P.blk0) * P.epb + el);
   car_contact_block(P, tid, el, car, env, env >= 0 ? env * C + car : 0);
 }
 
@@ -1876,7 +1877,7 @@ __global__ void __launch_bounds__(SBLOCK) logic_kernel(Params P, float* obs, flo
   __shared__ TrackLDS TL;
   const int tid = threadIdx.x, C = P.C;
   const int el = tid / C, car = tid - el * C;
-  const int slot = blockIdx.x * P.epb + el;
+  const int slot = (blockIdx.x + P.blk0) * P.epb + el;
   const int env = blk_env_of(P, el, slot);
   const int n = env >= 0 ? env * C + car : 0;
   LPROF(0);
@@ -1884,7 +1885,7 @@ __global__ void __launch_bounds__(SBLOCK) logic_kernel(Params P, float* obs, flo
   double sim;
   int pend_in, reason_in;
   logic_load(P, env, car, n, c, sim, pend_in, reason_in);   // state loads issued before the staging barrier
-  TrackDev T = P.tracks[blk_track_of(P, blockIdx.x)];
+  TrackDev T = P.tracks[blk_track_of(P, (blockIdx.x + P.blk0))];
   stage_track_lds(T, TL, tid);
   __syncthreads();
   T.segs = TL.segs; T.prefix = TL.prefix;
@@ -2356,8 +2357,8 @@ struct NascarHandle {
   int map_identity = 0, one_track = -1;   // Params shortcuts of the block map (prepare)
   std::vector<int> env_track;
   std::vector<int> pending_track;   // nascar_set_env_tracks, applied per env by its next nascar_reset
-  bool pristine = true;
-  int car_contact = 0;              // nascar_set_car_contact (build-only extension)             // no reset / step / rollout / set_state yet: track changes apply at once
+  bool pristine = true;             // no reset / step / rollout / set_state yet: track changes apply at once
+  int car_contact = 0;              // nascar_set_car_contact (build-only extension)
   float* d_vhist = nullptr;  // [VH_RING][N] speed history (nascar_set_perf_history), outside the snapshot arena
   double* d_ctl = nullptr;   // rule-driver state for nascar_policy_actions (inside the arena: snapshots keep it)
   float4* d_pose = nullptr;  // [2][N] step/reset -> sensor_kernel hand-off
@@ -2371,6 +2372,12 @@ struct NascarHandle {
   int actor_fp32 = 1;   // default: reference precision
   size_t max_lds = 0, max_sensor_lds = 0, max_sensor_groups_lds = 0;
   bool dirty_tracks = true;
+  // sharded rollout (nascar_set_rollout_streams): shard s steps workgroups [nblocks*s/S, nblocks*(s+1)/S) on its
+  // own stream; the caller's stream forks to them at the launch and joins them at its end
+  int ro_streams = 4;               // nascar_create: the process's hardware queues (GPU_MAX_HW_QUEUES, HIP default 4)
+  std::vector<hipStream_t> sub_stream;
+  hipEvent_t ev_fork = nullptr;
+  std::vector<hipEvent_t> ev_join;
 };
 
 static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
@@ -2410,6 +2417,11 @@ extern "C" int nascar_create(const NascarConfig* cfg, NascarHandle** out) {
   HIPCHK(hipMalloc(&h->d_ray_cs, sizeof(h_ray_cs)));
   HIPCHK(hipMemcpy(h->d_ray_cs, h_ray_cs, sizeof(h_ray_cs), hipMemcpyHostToDevice));
   h->env_track.assign(E, 0);
+  {   // one shard per hardware queue: more streams than queues put two shards on one queue, run back to back
+    const char* q = getenv("GPU_MAX_HW_QUEUES");
+    const int nq = q ? atoi(q) : 4;
+    h->ro_streams = std::max(1, std::min(nq > 0 ? nq : 4, 16));
+  }
   *out = h;
   return 0;
 }
@@ -2424,6 +2436,9 @@ extern "C" void nascar_destroy(NascarHandle* h) {
     hipFree(t.beam.d_cell); hipFree(t.beam.d_start); hipFree(t.beam.d_ent); hipFree(t.beam.d_head);
   }
   hipFree(h->d_tracks); hipFree(h->d_blk_track); hipFree(h->d_blk_env);
+  for (auto st : h->sub_stream) hipStreamDestroy(st);
+  for (auto ev : h->ev_join) hipEventDestroy(ev);
+  if (h->ev_fork) hipEventDestroy(h->ev_fork);
   delete h;
 }
 
@@ -2630,23 +2645,24 @@ static int sensor_impl() {
   if (m < 0) { const char* e = getenv("NASCAR_SENSOR"); m = (e && !strcmp(e, "groups")) ? 0 : 1; }
   return m;
 }
-static void launch_sensors_impl(NascarHandle* h, const Params& P, float* obs, float* terminal_obs, int passes,
+// nb step-kernel workgroups from P.blk0 (each is SUB sensor workgroups)
+static void launch_sensors_impl(NascarHandle* h, const Params& P, int nb, float* obs, float* terminal_obs, int passes,
                                 void* stream, int impl) {
   if (impl == 1) {
     constexpr int CPW = BLOCK / RAY_LPC;
     const int sub = (SBLOCK + CPW - 1) / CPW;
     const size_t rlds = h->max_sensor_lds;   // >= 2 float4 per wall
-    hipLaunchKernelGGL(ray_sensor_kernel, dim3(h->nblocks * sub), dim3(BLOCK), rlds, (hipStream_t)stream, P, obs,
+    hipLaunchKernelGGL(ray_sensor_kernel, dim3(nb * sub), dim3(BLOCK), rlds, (hipStream_t)stream, P, obs,
                        terminal_obs, passes);
     return;
   }
   const size_t lds = h->max_sensor_groups_lds;
   const int sub = (SBLOCK + BLOCK / SENSOR_LPC - 1) / (BLOCK / SENSOR_LPC);
-  hipLaunchKernelGGL(sensor_kernel<SENSOR_LPC>, dim3(h->nblocks * sub), dim3(BLOCK), lds, (hipStream_t)stream,
+  hipLaunchKernelGGL(sensor_kernel<SENSOR_LPC>, dim3(nb * sub), dim3(BLOCK), lds, (hipStream_t)stream,
                      P, obs, terminal_obs, passes);
 }
 static void launch_sensors(NascarHandle* h, const Params& P, float* obs, float* terminal_obs, int passes, void* stream) {
-  launch_sensors_impl(h, P, obs, terminal_obs, passes, stream, sensor_impl());
+  launch_sensors_impl(h, P, h->nblocks, obs, terminal_obs, passes, stream, sensor_impl());
 }
 
 extern "C" int nascar_reset(NascarHandle* h, const uint8_t* env_mask, float* obs, void* stream) {
@@ -2677,28 +2693,90 @@ extern "C" int nascar_step_driven(NascarHandle* h, int32_t policy, uint64_t seed
   if (policy != 0 && policy != 1 && policy != 3) return fail("driven step policy must be 0, 1 or 3 (got %d)", policy);
   return step_impl(h, nullptr, 0, policy, seed, step, obs, reward, car_flags, env_flags, auto_reset, terminal_obs, stream);
 }
+// one env step of step-kernel workgroups [P.blk0, P.blk0 + nb) on stream s:
+// model_kernel -> logic_kernel -> sensor_kernel (pass A for every car, pass B for auto-reset cars)
+static int launch_step_range(NascarHandle* h, const Params& P, int nb, const void* actions, int32_t discrete, int policy,
+                             uint64_t seed, int64_t step, float* obs, float* reward, uint8_t* car_flags,
+                             uint8_t* env_flags, int32_t auto_reset, float* terminal_obs, hipStream_t s) {
+  hipLaunchKernelGGL(model_kernel, dim3(nb), dim3(SBLOCK), 0, s, P, actions, discrete, terminal_obs != nullptr,
+                     policy, seed, step, (const float*)obs);
+  HIPCHK(hipGetLastError());
+  if (h->car_contact) {
+    hipLaunchKernelGGL(car_contact_kernel, dim3(nb), dim3(SBLOCK), 0, s, P);
+    HIPCHK(hipGetLastError());
+  }
+  hipLaunchKernelGGL(logic_kernel, dim3(nb), dim3(SBLOCK), 0, s, P, obs, reward, car_flags,
+                     env_flags, auto_reset, terminal_obs);
+  HIPCHK(hipGetLastError());
+  launch_sensors_impl(h, P, nb, obs, terminal_obs, auto_reset ? 3 : 1, s, sensor_impl());
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
 static int step_impl(NascarHandle* h, const void* actions, int32_t discrete, int policy, uint64_t seed, int64_t step,
                      float* obs, float* reward, uint8_t* car_flags, uint8_t* env_flags, int32_t auto_reset,
                      float* terminal_obs, void* stream) {
   h->pristine = false;
   if (prepare(h)) return -1;
   Params P = make_params(h);
-  // model_kernel -> logic_kernel -> sensor_kernel (pass A for every car, pass B for auto-reset cars).
-  // Kept on the caller's stream: a cross-stream event hop measured 10-15 us on the MI355X box, more than
-  // running logic_kernel and sensor pass A concurrently would save.
-  hipStream_t s = (hipStream_t)stream;
-  hipLaunchKernelGGL(model_kernel, dim3(h->nblocks), dim3(SBLOCK), 0, s, P, actions, discrete, terminal_obs != nullptr,
-                     policy, seed, step, (const float*)obs);
-  HIPCHK(hipGetLastError());
-  if (h->car_contact) {
-    hipLaunchKernelGGL(car_contact_kernel, dim3(h->nblocks), dim3(SBLOCK), 0, s, P);
-    HIPCHK(hipGetLastError());
+  // Whole grid on the caller's stream: splitting one step over streams needs a fork and a join per step, and
+  // the per-step barrier measured slower than one grid (tools/streams_exp.py: 2 / 4 shards 0.252 / 0.277 ms vs
+  // 0.224 ms).  Shards pay off only when they run many steps unsynchronised: the sharded nascar_rollout.
+  return launch_step_range(h, P, h->nblocks, actions, discrete, policy, seed, step, obs, reward, car_flags, env_flags,
+                           auto_reset, terminal_obs, (hipStream_t)stream);
+}
+
+// Sharded rollout: the workgroups split into S contiguous ranges (shards of whole envs), each stepped `steps`
+// times by per-step launches on its own stream -- shard 0 on the caller's stream, shards 1.. on internal streams
+// forked from it at the start and joined into it at the end (S streams in all: the process has few hardware
+// queues, GPU_MAX_HW_QUEUES = 4, and two shards on one queue run one after the other).  Envs are independent, so
+// a shard needs only its own previous step: while one shard's slowest cars finish a step (the Box2D TOI chains
+// that set each kernel's tail) the other shards' kernels fill the idle CUs, and the shards drift apart by up to
+// the whole rollout.  Same kernels and arguments as nascar_step_driven, so the results equal `steps` x
+// nascar_step_driven bit for bit (tests/test_gpu_rollout.py).
+static int rollout_sharded(NascarHandle* h, int S, int32_t policy, uint64_t seed, int64_t step0, int32_t steps, float* obs,
+                           float* reward, uint8_t* car_flags, uint8_t* env_flags, int32_t auto_reset, int32_t traj,
+                           hipStream_t stream) {
+  S = std::max(1, std::min(S, h->nblocks));
+  while ((int)h->sub_stream.size() < S - 1) {
+    hipStream_t st; hipEvent_t ev;
+    HIPCHK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    h->sub_stream.push_back(st);
+    HIPCHK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    h->ev_join.push_back(ev);
   }
-  hipLaunchKernelGGL(logic_kernel, dim3(h->nblocks), dim3(SBLOCK), 0, s, P, obs, reward, car_flags,
-                     env_flags, auto_reset, terminal_obs);
-  HIPCHK(hipGetLastError());
-  launch_sensors(h, P, obs, terminal_obs, auto_reset ? 3 : 1, stream);
-  HIPCHK(hipGetLastError());
+  if (S > 1 && !h->ev_fork) HIPCHK(hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming));
+  auto shard_stream = [&](int s) { return s == 0 ? stream : h->sub_stream[s - 1]; };
+  const Params P0 = make_params(h);
+  if (S > 1) {
+    HIPCHK(hipEventRecord(h->ev_fork, stream));
+    for (int s = 1; s < S; ++s) HIPCHK(hipStreamWaitEvent(shard_stream(s), h->ev_fork, 0));
+  }
+  const size_t NC = (size_t)h->N, E = (size_t)h->E;
+  for (int k = 0; k < steps; ++k) {
+    const size_t ko = traj ? (size_t)k : 0;
+    for (int s = 0; s < S; ++s) {
+      const int b0 = (int)((int64_t)h->nblocks * s / S), b1 = (int)((int64_t)h->nblocks * (s + 1) / S);
+      Params P = P0;
+      P.blk0 = b0;
+      if (launch_step_range(h, P, b1 - b0, nullptr, 0, policy, seed, step0 + k, obs, reward + ko * NC,
+                            car_flags ? car_flags + ko * NC : nullptr, env_flags ? env_flags + ko * E : nullptr,
+                            auto_reset, nullptr, shard_stream(s)))
+        return -1;
+    }
+  }
+  for (int s = 1; s < S; ++s) {
+    HIPCHK(hipEventRecord(h->ev_join[s - 1], shard_stream(s)));
+    HIPCHK(hipStreamWaitEvent(stream, h->ev_join[s - 1], 0));
+  }
+  return 0;
+}
+
+extern "C" int nascar_get_rollout_streams(NascarHandle* h) { return h ? h->ro_streams : -1; }
+extern "C" int nascar_set_rollout_streams(NascarHandle* h, int32_t streams) {
+  if (!h) return fail("null argument");
+  if (streams < 0 || streams > 16) return fail("rollout streams must be in [0, 16] (got %d)", streams);
+  h->ro_streams = streams;
   return 0;
 }
 
@@ -2711,7 +2789,10 @@ extern "C" int nascar_rollout(NascarHandle* h, int32_t policy, uint64_t seed, in
   if (steps == 0) return 0;
   h->pristine = false;
   if (prepare(h)) return -1;
-  Params P = make_params(h);
+  if (h->ro_streams > 0)
+    return rollout_sharded(h, h->ro_streams, policy, seed, step0, steps, obs, reward, car_flags, env_flags, auto_reset,
+                           traj, (hipStream_t)stream);
+  Params P = make_params(h);   // ro_streams == 0: the fused rollout_kernel
   if (!h->d_params) {
     HIPCHK(hipMalloc(&h->d_params, sizeof(Params)));
     memset(&h->params_up, 0, sizeof(Params));
@@ -2928,7 +3009,7 @@ extern "C" int nascar_debug_sensors(NascarHandle* h, const float* poses, float* 
   Params P = make_params(h);
   hipLaunchKernelGGL(debug_pose_kernel, dim3((h->N + 255) / 256), dim3(256), 0, (hipStream_t)stream, P, poses);
   HIPCHK(hipGetLastError());
-  launch_sensors_impl(h, P, obs, nullptr, 1, stream, impl);
+  launch_sensors_impl(h, P, h->nblocks, obs, nullptr, 1, stream, impl);
   HIPCHK(hipGetLastError());
   return 0;
 }

@@ -1,4 +1,4 @@
-"""nascar_rollout (fused multi-step rollout kernel) against the per-step path: K x (nascar_policy_actions +
+"""nascar_rollout (sharded over internal streams, the default, and the fused multi-step kernel) against the per-step path: K x (nascar_policy_actions +
 nascar_step with auto-reset) from the same state must give the same per-step rewards / car flags / env flags,
 the same final observation and the same final engine state, bit for bit."""
 import os
@@ -27,15 +27,18 @@ def _per_step(env, policy, seed, step0, K):
     return torch.stack(R), torch.stack(CF), torch.stack(EF)
 
 
+@pytest.mark.parametrize("streams", [4, 0])        # sharded rollout (default) / fused rollout kernel
 @pytest.mark.parametrize("tracks,E,C,policy,warm,K", [
     (["daytona.track"], 48, 10, 3, 600, 900),          # the bench workload: noisy driver, contacts
     (["daytona.track"], 16, 2, 1, 0, 400),             # rule driver from reset
     (["martinsville.track"], 32, 4, 0, 3500, 300),     # uniform, reset_on_lap: the t > 60 s termination + auto-reset
     (["talladega.track", "michigan.track", "nascar2.track", "trioval.track"], 40, 3, 3, 900, 600),   # mixed tracks
+    (["daytona.track", "nascar.track"], 500, 10, 3, 1200, 200),   # 42 workgroups: uneven shards, 2 track groups
 ])
-def test_rollout_equals_per_step(tracks, E, C, policy, warm, K):
+def test_rollout_equals_per_step(tracks, E, C, policy, warm, K, streams):
     rol = policy == 0
     a, b = _engine(tracks, E, C, rol), _engine(tracks, E, C, rol)
+    b.set_rollout_streams(streams if E < 500 or streams == 0 else 3)
     a.reset()
     if warm:                                    # leave the reset state first (cars spread, contacts active)
         a.rollout(policy, warm, seed=5, step0=0, auto_reset=True)

@@ -6,9 +6,13 @@ Reads the rocprofv3 CSVs under <out_dir>/{kt,fetch,write}, and writes
   profiles/<tag>_kernel_stats.csv  (rocprofv3 --stats summary, copied verbatim)
   profiles/<tag>_pmc_step.json     (per-dispatch FETCH_SIZE / WRITE_SIZE of the two kernels of a step)
   profiles/pmc_traffic.json        (read by bench.py for roofline.traffic)
-One env step = one model_kernel + logic_kernel + ray_sensor_kernel launch each.  HBM bytes = (2 * FETCH_SIZE + WRITE_SIZE)
-* 1024: FETCH_SIZE/WRITE_SIZE are in KiB and gfx950 FETCH_SIZE tallies half the bytes of a wide
-coalesced read (MI355X_MICROARCH.md "HBM").
+One env step = model_kernel + logic_kernel + ray_sensor_kernel over every workgroup: one launch each (per-step
+path) or one launch each per env shard (sharded rollout, a grid of 1/S of the workgroups).  A run holds both, so
+every dispatch's counter is scaled to the full grid (value / its grid size x the full grid size) before averaging.
+HBM bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024: FETCH_SIZE/WRITE_SIZE are in KiB and gfx950 FETCH_SIZE tallies
+half the bytes of a wide coalesced read (MI355X_MICROARCH.md "HBM").
+The sharded step time is read from the kernel trace: the span of each unbroken run of shard dispatches divided by
+the env steps it holds (its model_kernel workgroups / the full grid's), to check the bench's HIP-event time.
 """
 import csv
 import glob
@@ -41,12 +45,57 @@ def _base(name):
 
 
 def _per_dispatch(path, counter, kernel):
-    vals = defaultdict(float)
+    """per-dispatch counter totals scaled to the kernel's full grid"""
+    vals, grid = defaultdict(float), {}
     for row in csv.DictReader(open(path)):
         if _base(row.get("Kernel_Name", "")) != kernel or row.get("Counter_Name") != counter:
             continue
         vals[row["Dispatch_Id"]] += float(row["Counter_Value"])
-    return list(vals.values())
+        grid[row["Dispatch_Id"]] = int(row["Grid_Size"])
+    if not vals:
+        return []
+    full = max(grid.values())
+    return [v / grid[d] * full for d, v in vals.items()]
+
+
+def _trace_steps(path):
+    """full-grid average duration per kernel, and the sharded rollout's per-step time (ns) from a kernel trace"""
+    rows = []
+    for row in csv.DictReader(open(path)):
+        kn = _base(row.get("Kernel_Name", ""))
+        if kn in KERNELS:
+            g = int(row["Grid_Size_X"]) * int(row["Grid_Size_Y"]) * int(row["Grid_Size_Z"])
+            rows.append((int(row["Start_Timestamp"]), int(row["End_Timestamp"]), kn, g))
+    if not rows:
+        return {}
+    rows.sort()
+    full = {kn: max(g for _, _, k, g in rows if k == kn) for kn in KERNELS if any(k == kn for _, _, k, _ in rows)}
+    res = {}
+    for kn in full:
+        d = [e - s for s, e, k, g in rows if k == kn and g == full[kn]]
+        if d:
+            res[f"{kn}_full_grid_avg_ns"] = sum(d) / len(d)
+            res[f"{kn}_full_grid_calls"] = len(d)
+    spans, steps, run = 0.0, 0.0, []
+
+    def close(run):
+        nonlocal spans, steps
+        if run:
+            mg = sum(g for _, _, k, g in run if k == "model_kernel")
+            if mg:
+                spans += max(e for _, e, _, _ in run) - min(s for s, _, _, _ in run)
+                steps += mg / full["model_kernel"]
+    for r in rows:
+        if r[3] < full[r[2]]:
+            run.append(r)
+        else:
+            close(run)
+            run = []
+    close(run)
+    if steps:
+        res["sharded_step_ns"] = spans / steps
+        res["sharded_steps_traced"] = steps
+    return res
 
 
 def main():
@@ -63,6 +112,9 @@ def main():
                     res[f"{kn}_rocprof_avg_ns"] = float(row["AverageNs"])
                     res[f"{kn}_rocprof_calls"] = int(row["Calls"])
         res["step_rocprof_avg_ns"] = sum(res.get(f"{kn}_rocprof_avg_ns", 0.0) for kn in KERNELS)
+    kt = _find(os.path.join(out, "kt"), "kernel_trace.csv")
+    if kt:
+        res.update(_trace_steps(kt))
     b = _bench_line(os.path.join(out, "kt.log"))
     if b:
         res["bench_under_rocprof"] = b
