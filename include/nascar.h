@@ -94,7 +94,7 @@ int nascar_rollout(NascarHandle* h, int32_t policy, uint64_t seed, int64_t step0
 /* Rollout implementation (no reference counterpart: a scheduling choice with identical results).
  * streams >= 1: the envs split into `streams` shards of contiguous workgroups, each stepped by per-step launches
  * on its own stream (shard 0 on the caller's), so one shard's slow cars overlap the other shards' work; default:
- * one shard per hardware queue of the process (GPU_MAX_HW_QUEUES, HIP's default 4);
+ * 4, or the process's hardware queues if fewer (GPU_MAX_HW_QUEUES; two shards on one queue run back to back);
  * streams = 0: the fused rollout kernel (all steps in one launch, block barriers between the phases).
  * nascar_get_rollout_streams returns the current setting (-1 for a NULL handle). */
 int nascar_set_rollout_streams(NascarHandle* h, int32_t streams);

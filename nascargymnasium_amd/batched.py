@@ -79,8 +79,8 @@ class BatchedCarEnv:
     def set_rollout_streams(self, streams: int = 4):
         """How `rollout` schedules its steps (identical results either way): streams >= 1 splits the envs into that
         many shards, each stepped on its own stream (shard 0 on the current one), so one shard's slow cars (Box2D
-        TOI chains) overlap the other shards' work (default: one per hardware queue, GPU_MAX_HW_QUEUES, 4); 0 runs
-        all steps in one fused launch."""
+        TOI chains) overlap the other shards' work (default 4, or GPU_MAX_HW_QUEUES if fewer); 0 runs all steps in
+        one fused launch."""
         _lib.check(self.L.nascar_set_rollout_streams(self.h, int(streams)))
 
     @property

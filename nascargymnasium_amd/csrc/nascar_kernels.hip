@@ -2374,7 +2374,7 @@ struct NascarHandle {
   bool dirty_tracks = true;
   // sharded rollout (nascar_set_rollout_streams): shard s steps workgroups [nblocks*s/S, nblocks*(s+1)/S) on its
   // own stream; the caller's stream forks to them at the launch and joins them at its end
-  int ro_streams = 4;               // nascar_create: the process's hardware queues (GPU_MAX_HW_QUEUES, HIP default 4)
+  int ro_streams = 4;               // nascar_create: min(4, the process's hardware queues GPU_MAX_HW_QUEUES)
   std::vector<hipStream_t> sub_stream;
   hipEvent_t ev_fork = nullptr;
   std::vector<hipEvent_t> ev_join;
@@ -2417,10 +2417,12 @@ extern "C" int nascar_create(const NascarConfig* cfg, NascarHandle** out) {
   HIPCHK(hipMalloc(&h->d_ray_cs, sizeof(h_ray_cs)));
   HIPCHK(hipMemcpy(h->d_ray_cs, h_ray_cs, sizeof(h_ray_cs), hipMemcpyHostToDevice));
   h->env_track.assign(E, 0);
-  {   // one shard per hardware queue: more streams than queues put two shards on one queue, run back to back
+  {   // 4 shards, fewer if the process has fewer hardware queues (two shards on one queue run back to back);
+      // more than 4 measured slower even with as many queues (tools/ro_queues_ab.sh: 6 / 8 / 12 shards on 6 / 8 / 12
+      // queues 0.275 / 0.276 / 0.350 ms per step vs 0.193 ms for 4)
     const char* q = getenv("GPU_MAX_HW_QUEUES");
     const int nq = q ? atoi(q) : 4;
-    h->ro_streams = std::max(1, std::min(nq > 0 ? nq : 4, 16));
+    h->ro_streams = std::max(1, std::min(nq > 0 ? nq : 4, 4));
   }
   *out = h;
   return 0;
