@@ -140,7 +140,8 @@ class Stepper:
 
     def __init__(self, env, policy, seed, acts=None, gather=None, rollout=0):
         self.env, self.pol, self.seed, self.acts, self.gather = env, POLICY_ID[policy], seed, acts, gather
-        self.R = rollout if (acts is None and gather is None and self.pol != 2) else 0
+        # device action sources (policy 2, the SAC actor, only on the sharded schedule) step through nascar_rollout
+        self.R = rollout if (acts is None and gather is None and (self.pol != 2 or env.rollout_streams > 0)) else 0
         self.traj = None
 
     def actions(self, i):

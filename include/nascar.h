@@ -83,7 +83,9 @@ int nascar_step_driven(NascarHandle* h, int32_t policy, uint64_t seed, int64_t s
  * Default implementation: the envs split into shards stepped on internal streams, forked from `stream` at the
  * start and joined into it at the end (nascar_set_rollout_streams); streams = 0 selects one fused launch.
  *   policy:  0 uniform, 1 BaseController._fallback_control, 3 noisy rule driver (policy 1 with 15 % of the
- *            car-steps uniform) -- see nascar_policy_actions
+ *            car-steps uniform) -- see nascar_policy_actions; 2 the SAC actor (nascar_set_actor; sharded
+ *            rollout only: each shard runs the actor on its own cars, one shard unless the envs sit in one
+ *            track's workgroups in order)
  *   obs:     [E*C*38] float32, in: the current observation, out: the last step's
  *   traj != 0: reward [steps][E*C], car_flags [steps][E*C], env_flags [steps][E] (per-step records);
  *   traj == 0: reward [E*C], car_flags [E*C], env_flags [E] hold the last step's values.

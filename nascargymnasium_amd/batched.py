@@ -162,9 +162,10 @@ class BatchedCarEnv:
 
     def rollout(self, policy: int, steps: int, seed: int = 0, step0: int = 0, auto_reset: bool = True,
                 trajectory: bool = False, out=None):
-        """`steps` env steps in one fused launch, actions from device action source `policy` (0 uniform, 1 rule
-        driver, 3 noisy rule driver) on the previous observation; equals `steps` x (policy_actions(policy, seed,
-        step0 + k) + step(..., auto_reset)).  Returns (obs, reward, car_flags, env_flags): the last step's, or with
+        """`steps` env steps in one call (sharded over streams, or one fused launch: set_rollout_streams), actions
+        from device action source `policy` (0 uniform, 1 rule driver, 2 the SAC actor -- sharded only, 3 noisy rule
+        driver) on the previous observation; equals `steps` x (policy_actions(policy, seed, step0 + k) +
+        step(..., auto_reset)).  Returns (obs, reward, car_flags, env_flags): the last step's, or with
         trajectory=True the per-step records [steps, E, C] / [steps, E] (obs is always the last step's)."""
         steps = int(steps)
         if trajectory and out is not None:      # caller-owned per-step buffers (at least `steps` records)

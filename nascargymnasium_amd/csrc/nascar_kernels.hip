@@ -2378,6 +2378,7 @@ struct NascarHandle {
   std::vector<hipStream_t> sub_stream;
   hipEvent_t ev_fork = nullptr;
   std::vector<hipEvent_t> ev_join;
+  float* d_ro_act = nullptr;        // [N][2] actions of a policy-2 (SAC actor) sharded rollout
 };
 
 static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
@@ -2441,6 +2442,7 @@ extern "C" void nascar_destroy(NascarHandle* h) {
   for (auto st : h->sub_stream) hipStreamDestroy(st);
   for (auto ev : h->ev_join) hipEventDestroy(ev);
   if (h->ev_fork) hipEventDestroy(h->ev_fork);
+  hipFree(h->d_ro_act);
   delete h;
 }
 
@@ -2736,10 +2738,21 @@ static int step_impl(NascarHandle* h, const void* actions, int32_t discrete, int
 // that set each kernel's tail) the other shards' kernels fill the idle CUs, and the shards drift apart by up to
 // the whole rollout.  Same kernels and arguments as nascar_step_driven, so the results equal `steps` x
 // nascar_step_driven bit for bit (tests/test_gpu_rollout.py).
+// Policy 2 (the SAC actor): each shard runs the actor on its own cars' observations, then steps them -- the
+// cars of a shard are contiguous when the block map is the identity (one track, envs in workgroup order);
+// otherwise the rollout runs as one shard.
+static void launch_actor(NascarHandle* h, int n, const float* obs, float* actions, void* stream);
 static int rollout_sharded(NascarHandle* h, int S, int32_t policy, uint64_t seed, int64_t step0, int32_t steps, float* obs,
                            float* reward, uint8_t* car_flags, uint8_t* env_flags, int32_t auto_reset, int32_t traj,
                            hipStream_t stream) {
   S = std::max(1, std::min(S, h->nblocks));
+  const bool actor = policy == 2;
+  if (actor) {
+    if (!h->d_actor) return fail("policy 2 needs an actor (nascar_set_actor)");
+    if ((uintptr_t)obs & 7) return fail("actor obs must be 8-byte aligned");
+    if (!h->map_identity) S = 1;
+    if (!h->d_ro_act) HIPCHK(hipMalloc(&h->d_ro_act, sizeof(float) * 2 * (size_t)h->N));
+  }
   while ((int)h->sub_stream.size() < S - 1) {
     hipStream_t st; hipEvent_t ev;
     HIPCHK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
@@ -2761,7 +2774,14 @@ static int rollout_sharded(NascarHandle* h, int S, int32_t policy, uint64_t seed
       const int b0 = (int)((int64_t)h->nblocks * s / S), b1 = (int)((int64_t)h->nblocks * (s + 1) / S);
       Params P = P0;
       P.blk0 = b0;
-      if (launch_step_range(h, P, b1 - b0, nullptr, 0, policy, seed, step0 + k, obs, reward + ko * NC,
+      if (actor) {
+        const size_t c0 = S == 1 ? 0 : (size_t)b0 * h->epb * h->C;
+        const size_t c1 = S == 1 ? NC : std::min((size_t)b1 * h->epb, E) * h->C;
+        if (c1 > c0) launch_actor(h, (int)(c1 - c0), obs + c0 * 38, h->d_ro_act + c0 * 2, shard_stream(s));
+        HIPCHK(hipGetLastError());
+      }
+      if (launch_step_range(h, P, b1 - b0, actor ? h->d_ro_act : nullptr, 0, actor ? -1 : policy, seed, step0 + k, obs,
+                            reward + ko * NC,
                             car_flags ? car_flags + ko * NC : nullptr, env_flags ? env_flags + ko * E : nullptr,
                             auto_reset, nullptr, shard_stream(s)))
         return -1;
@@ -2786,7 +2806,8 @@ extern "C" int nascar_rollout(NascarHandle* h, int32_t policy, uint64_t seed, in
                               float* reward, uint8_t* car_flags, uint8_t* env_flags, int32_t auto_reset, int32_t traj,
                               void* stream) {
   if (!h || !obs || !reward) return fail("null argument");
-  if (policy != 0 && policy != 1 && policy != 3) return fail("rollout policy must be 0, 1 or 3 (got %d)", policy);
+  if (policy < 0 || policy > 3) return fail("rollout policy must be 0, 1, 2 or 3 (got %d)", policy);
+  if (policy == 2 && h->ro_streams == 0) return fail("the fused rollout kernel has no actor (policy 2): use the sharded rollout");
   if (steps < 0) return fail("steps must be >= 0");
   if (steps == 0) return 0;
   h->pristine = false;

@@ -68,8 +68,41 @@ def test_rollout_last_step_outputs_and_errors():
     obs, rew, cf, ef = env.rollout(3, 50, seed=1)
     assert rew.shape == (8, 2) and obs.shape == (8, 2, 38) and cf.dtype == torch.uint8
     with pytest.raises(RuntimeError):
-        env.rollout(2, 5)                        # the SAC actor is not a rollout action source
+        env.rollout(2, 5)                        # policy 2 without an actor
+    from nascargymnasium_amd.policy import random_actor
+    env.set_actor(random_actor(0))
+    env.set_rollout_streams(0)
+    with pytest.raises(RuntimeError):
+        env.rollout(2, 5)                        # the fused rollout kernel has no actor
     env.close()
+
+
+@pytest.mark.parametrize("tracks,E,precision", [
+    (["daytona.track"], 480, "fp32"),            # 40 workgroups: 4 shards, each its own actor launch
+    (["daytona.track"], 480, "bf16"),
+    (["daytona.track", "nascar.track"], 96, "fp32"),   # non-identity block map: one shard
+])
+def test_sharded_rollout_sac_equals_per_step(tracks, E, precision):
+    """policy 2 in the sharded rollout (the actor per shard on its own cars) == per step: actor on the whole
+    batch (nascar_policy_actions) + nascar_step."""
+    from nascargymnasium_amd.policy import random_actor
+    C, warm, K = 10, 300, 150
+    a, b = _engine(tracks, E, C), _engine(tracks, E, C)
+    for e in (a, b):
+        e.set_actor(random_actor(3), precision=precision)
+    a.reset()
+    a.rollout(3, warm, seed=2, step0=0, auto_reset=True)
+    b.set_state(a.get_state())
+    b.obs.copy_(a.obs)
+    R, CF, EF = _per_step(a, 2, 0, 0, K)
+    obs_b, Rb, CFb, EFb = b.rollout(2, K, auto_reset=True, trajectory=True)
+    torch.cuda.synchronize()
+    for k in range(K):
+        assert torch.equal(R[k], Rb[k]), f"reward differs at step {k}"
+        assert torch.equal(CF[k], CFb[k]) and torch.equal(EF[k], EFb[k]), f"flags differ at step {k}"
+    assert torch.equal(a.obs, obs_b)
+    assert torch.equal(a.get_state(), b.get_state())
+    a.close(); b.close()
 
 
 @pytest.mark.parametrize("policy", [0, 1, 3])
