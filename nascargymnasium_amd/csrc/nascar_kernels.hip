@@ -2753,14 +2753,21 @@ static int rollout_sharded(NascarHandle* h, int S, int32_t policy, uint64_t seed
     if (!h->map_identity) S = 1;
     if (!h->d_ro_act) HIPCHK(hipMalloc(&h->d_ro_act, sizeof(float) * 2 * (size_t)h->N));
   }
-  while ((int)h->sub_stream.size() < S - 1) {
-    hipStream_t st; hipEvent_t ev;
-    HIPCHK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
-    h->sub_stream.push_back(st);
-    HIPCHK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-    h->ev_join.push_back(ev);
+  if ((int)h->sub_stream.size() < S - 1 || (S > 1 && !h->ev_fork)) {   // on the handle's device, whatever is current
+    int cur = 0;
+    HIPCHK(hipGetDevice(&cur));
+    if (cur != h->cfg.device) HIPCHK(hipSetDevice(h->cfg.device));
+    bool ok = true;
+    while (ok && (int)h->sub_stream.size() < S - 1) {   // a stream and its join event, both or neither
+      hipStream_t st; hipEvent_t ev;
+      ok = hipStreamCreateWithFlags(&st, hipStreamNonBlocking) == hipSuccess;
+      if (ok && hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) { hipStreamDestroy(st); ok = false; }
+      if (ok) { h->sub_stream.push_back(st); h->ev_join.push_back(ev); }
+    }
+    if (ok && !h->ev_fork) ok = hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming) == hipSuccess;
+    if (cur != h->cfg.device) hipSetDevice(cur);
+    if (!ok) return fail("creating the rollout shard streams failed");
   }
-  if (S > 1 && !h->ev_fork) HIPCHK(hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming));
   auto shard_stream = [&](int s) { return s == 0 ? stream : h->sub_stream[s - 1]; };
   const Params P0 = make_params(h);
   if (S > 1) {
