@@ -302,9 +302,9 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)   # before the process group, so RCCL's barrier binds this rank's GPU
     if world > 1:
         dist.init_process_group("nccl")
-    torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     E, C, K, W = args.envs, args.cars, args.steps, args.warmup
     closed = args.policy != "uniform"
