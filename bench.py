@@ -213,14 +213,25 @@ def timed(step, first, K, world):
     torch.cuda.synchronize()
     # K steps back to back (no per-step events: each event record costs ~5 us of device time between kernels
     # on this stack, which would be charged to the throughput)
+    diag = os.environ.get("NASCAR_BENCH_DIAG")
+    if diag:      # where the window's wall time goes: GPU span (2 events) vs host enqueue vs sync
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
     t0 = time.perf_counter()
     step.run(first, K)
+    t_enq = time.perf_counter() - t0
+    if diag:
+        e1.record()
     if step.gather is not None:
         step.gather.wait()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    return time.perf_counter() - t0
+    el = time.perf_counter() - t0
+    if diag:
+        print(f"[diag] K={K} wall {el * 1e3:.3f} ms, gpu span {e0.elapsed_time(e1):.3f} ms, host enqueue "
+              f"{t_enq * 1e3:.3f} ms", file=sys.stderr, flush=True)
+    return el
 
 
 def stats_pass(env, step, first, KR):

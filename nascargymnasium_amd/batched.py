@@ -89,8 +89,10 @@ class BatchedCarEnv:
 
     def set_perf_history(self, enable: bool = True):
         """Keep Car.velocity_history on the device so the info's `performance` dict is Car.validate_performance
-        (src/car.py:1060-1098); a 640-sample float32 ring per car, one 4-byte store per car-step.  The window starts
-        at the next reset of each env."""
+        (src/car.py:1060-1098); a 640-sample float32 ring per car, one 4-byte store per car-step.  Enabled before the
+        first reset (as CarEnv does) it covers every episode; enabled mid-episode, an env's window holds steps taken
+        before the enable, so its info reports perf_count -1 ("history not kept") until its next reset or until
+        600 steps have been recorded since the enable."""
         with torch.cuda.device(self.device):
             _lib.check(self.L.nascar_set_perf_history(self.h, int(bool(enable)), _stream()))
 
@@ -168,10 +170,16 @@ class BatchedCarEnv:
         step(..., auto_reset)).  Returns (obs, reward, car_flags, env_flags): the last step's, or with
         trajectory=True the per-step records [steps, E, C] / [steps, E] (obs is always the last step's)."""
         steps = int(steps)
+        if out is not None and not trajectory:
+            raise ValueError("`out` buffers are written only with trajectory=True")
         if trajectory and out is not None:      # caller-owned per-step buffers (at least `steps` records)
+            if len(out) != 3:
+                raise ValueError("out must be (reward, car_flags, env_flags)")
             rew, cf, ef = out
-            if rew.shape[0] < steps or cf.shape[0] < steps or ef.shape[0] < steps:
-                raise ValueError("trajectory buffers hold fewer than `steps` records")
+            for name, t, dt, inner in (("reward", rew, torch.float32, (self.E, self.C)),
+                                       ("car_flags", cf, torch.uint8, (self.E, self.C)),
+                                       ("env_flags", ef, torch.uint8, (self.E,))):
+                self._check_record_buffer(name, t, dt, inner, steps)
         elif trajectory:
             rew = torch.empty(steps, self.E, self.C, dtype=torch.float32, device=self.device)
             cf = torch.empty(steps, self.E, self.C, dtype=torch.uint8, device=self.device)
@@ -184,6 +192,22 @@ class BatchedCarEnv:
         if trajectory and steps > 0:
             self.reward.copy_(rew[steps - 1]); self.car_flags.copy_(cf[steps - 1]); self.env_flags.copy_(ef[steps - 1])
         return self.obs, rew, cf, ef
+
+    def _check_record_buffer(self, name, t, dtype, inner, steps):
+        """the kernels write record k at data_ptr + k * prod(inner) elements: anything but a contiguous tensor of
+        this dtype on this device with shape [>= steps, *inner] would be written out of bounds"""
+        if not isinstance(t, torch.Tensor):
+            raise ValueError(f"out {name}: expected a torch.Tensor, got {type(t).__name__}")
+        if t.device != self.device:
+            raise ValueError(f"out {name}: on {t.device}, the env is on {self.device}")
+        if t.dtype != dtype:
+            raise ValueError(f"out {name}: dtype {t.dtype}, expected {dtype}")
+        if tuple(t.shape[1:]) != inner or t.dim() != len(inner) + 1:
+            raise ValueError(f"out {name}: shape {tuple(t.shape)}, expected [>= {steps}, {', '.join(map(str, inner))}]")
+        if t.shape[0] < steps:
+            raise ValueError(f"out {name}: holds {t.shape[0]} records, fewer than steps = {steps}")
+        if not t.is_contiguous():
+            raise ValueError(f"out {name}: must be contiguous")
 
     def info_tensor(self) -> torch.Tensor:
         """per-car info [E, C, N_INFO] float64 (fields: _lib.INFO_FIELDS)."""

@@ -2060,12 +2060,15 @@ __global__ void __launch_bounds__(SBLOCK) info_kernel(Params P, double* info) {
     const int k = (int)rint(P.env_time[env] * 60.0);
     const int cnt = k < VH_SIZE ? k : VH_SIZE, j0 = k - cnt;
     float mx = 0.0f; int first = -1;
+    bool valid = true;
     for (int j = j0; j < k; ++j) {
       const float v = j == 0 ? 0.0f : P.vhist[(size_t)(j % VH_RING) * P.N + n];
+      valid = valid && v == v;     // NaN: a slot not written since the history was enabled (mid-episode)
       if (j == j0 || v > mx) mx = v;
       if (first < 0 && (double)v >= 100.0 * 0.277778) first = j - j0;
     }
-    o[INFO_PERF_COUNT] = cnt; o[INFO_PERF_MAX] = cnt ? (double)mx : 0.0; o[INFO_PERF_FIRST] = first;
+    if (valid) { o[INFO_PERF_COUNT] = cnt; o[INFO_PERF_MAX] = cnt ? (double)mx : 0.0; o[INFO_PERF_FIRST] = first; }
+    else { o[INFO_PERF_COUNT] = -1.0; o[INFO_PERF_MAX] = 0.0; o[INFO_PERF_FIRST] = -1.0; }
   } else {
     o[INFO_PERF_COUNT] = -1.0; o[INFO_PERF_MAX] = 0.0; o[INFO_PERF_FIRST] = -1.0;
   }
@@ -2775,30 +2778,38 @@ static int rollout_sharded(NascarHandle* h, int S, int32_t policy, uint64_t seed
     for (int s = 1; s < S; ++s) HIPCHK(hipStreamWaitEvent(shard_stream(s), h->ev_fork, 0));
   }
   const size_t NC = (size_t)h->N, E = (size_t)h->E;
-  for (int k = 0; k < steps; ++k) {
-    const size_t ko = traj ? (size_t)k : 0;
-    for (int s = 0; s < S; ++s) {
-      const int b0 = (int)((int64_t)h->nblocks * s / S), b1 = (int)((int64_t)h->nblocks * (s + 1) / S);
-      Params P = P0;
-      P.blk0 = b0;
-      if (actor) {
-        const size_t c0 = S == 1 ? 0 : (size_t)b0 * h->epb * h->C;
-        const size_t c1 = S == 1 ? NC : std::min((size_t)b1 * h->epb, E) * h->C;
-        if (c1 > c0) launch_actor(h, (int)(c1 - c0), obs + c0 * 38, h->d_ro_act + c0 * 2, shard_stream(s));
-        HIPCHK(hipGetLastError());
+  auto enqueue = [&]() -> int {
+    for (int k = 0; k < steps; ++k) {
+      const size_t ko = traj ? (size_t)k : 0;
+      for (int s = 0; s < S; ++s) {
+        const int b0 = (int)((int64_t)h->nblocks * s / S), b1 = (int)((int64_t)h->nblocks * (s + 1) / S);
+        Params P = P0;
+        P.blk0 = b0;
+        if (actor) {
+          const size_t c0 = S == 1 ? 0 : (size_t)b0 * h->epb * h->C;
+          const size_t c1 = S == 1 ? NC : std::min((size_t)b1 * h->epb, E) * h->C;
+          if (c1 > c0) launch_actor(h, (int)(c1 - c0), obs + c0 * 38, h->d_ro_act + c0 * 2, shard_stream(s));
+          HIPCHK(hipGetLastError());
+        }
+        if (launch_step_range(h, P, b1 - b0, actor ? h->d_ro_act : nullptr, 0, actor ? -1 : policy, seed, step0 + k,
+                              obs, reward + ko * NC,
+                              car_flags ? car_flags + ko * NC : nullptr, env_flags ? env_flags + ko * E : nullptr,
+                              auto_reset, nullptr, shard_stream(s)))
+          return -1;
       }
-      if (launch_step_range(h, P, b1 - b0, actor ? h->d_ro_act : nullptr, 0, actor ? -1 : policy, seed, step0 + k, obs,
-                            reward + ko * NC,
-                            car_flags ? car_flags + ko * NC : nullptr, env_flags ? env_flags + ko * E : nullptr,
-                            auto_reset, nullptr, shard_stream(s)))
-        return -1;
     }
-  }
+    return 0;
+  };
+  const int rc = enqueue();
+  // join every shard into the caller's stream even when a launch failed part way: the shard work already queued
+  // must stay ordered before whatever the caller enqueues next (a reset, set_state, a reused tensor)
+  int jrc = 0;
   for (int s = 1; s < S; ++s) {
-    HIPCHK(hipEventRecord(h->ev_join[s - 1], shard_stream(s)));
-    HIPCHK(hipStreamWaitEvent(stream, h->ev_join[s - 1], 0));
+    const hipError_t e1 = hipEventRecord(h->ev_join[s - 1], shard_stream(s));
+    const hipError_t e2 = e1 == hipSuccess ? hipStreamWaitEvent(stream, h->ev_join[s - 1], 0) : e1;
+    if (e2 != hipSuccess && !jrc && !rc) jrc = fail("joining rollout shard %d failed: %s", s, hipGetErrorString(e2));
   }
-  return 0;
+  return rc ? rc : jrc;
 }
 
 extern "C" int nascar_get_rollout_streams(NascarHandle* h) { return h ? h->ro_streams : -1; }
@@ -2859,7 +2870,9 @@ extern "C" int nascar_set_perf_history(NascarHandle* h, int32_t enable, void* st
   if (h->d_vhist) return 0;
   const size_t bytes = sizeof(float) * (size_t)VH_RING * h->N;
   HIPCHK(hipMalloc(&h->d_vhist, bytes));
-  HIPCHK(hipMemsetAsync(h->d_vhist, 0, bytes, (hipStream_t)stream));
+  // every slot NaN: until an episode has written the whole window since the enable, info reports perf_count -1
+  // (enabling mid-episode would otherwise count the steps taken before it as zero speeds)
+  HIPCHK(hipMemsetAsync(h->d_vhist, 0xFF, bytes, (hipStream_t)stream));
   return 0;
 }
 

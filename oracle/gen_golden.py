@@ -479,7 +479,8 @@ def policy_action(mode, k, driver, obs, rng):
     raise ValueError(mode)
 
 
-def run_scenario(ref, name, track, C, steps, policy, reset_on_lap=False, reset_at=(), seed=0, discrete=False):
+def run_scenario(ref, name, track, C, steps, policy, reset_on_lap=False, reset_at=(), seed=0, discrete=False,
+                 start_position=None, start_angle=0.0):
     """Run the REFERENCE CarEnv (stub Box2D -> oracle Box2D) and record everything."""
     track_path = os.path.join(ref, "tracks", track)
     hb = oracle_lib.OracleEnv(track_path, 1, 1)
@@ -491,7 +492,7 @@ def run_scenario(ref, name, track, C, steps, policy, reset_on_lap=False, reset_a
     with contextlib.redirect_stdout(io.StringIO()):
         from src.car_env import CarEnv
         env = CarEnv(render_mode=None, track_file=track_path, num_cars=C, reset_on_lap=reset_on_lap,
-                     discrete_action_space=discrete)
+                     discrete_action_space=discrete, start_position=start_position, start_angle=start_angle)
         obs, info = env.reset()
     rng = np.random.default_rng(seed)
     drivers = [RuleDriver(ref) for _ in range(C)]
@@ -542,6 +543,9 @@ def run_scenario(ref, name, track, C, steps, policy, reset_on_lap=False, reset_a
                sim_time=np.array(rec["sim_time"]), info=np.array(rec["info"], np.float64)[keep],
                reset=np.array(rec["reset"]), obs0=rec["obs0"],
                perf=np.array(rec["perf"], np.float64)[keep], physics=np.array(rec["physics"], np.float64)[keep])
+    if start_position is not None or start_angle != 0.0:     # CarEnv(start_position=, start_angle=) (src/car_env.py:82-83)
+        out["start_position"] = np.array(start_position if start_position is not None else (np.nan, np.nan), np.float64)
+        out["start_angle"] = np.array(start_angle, np.float64)
     return out
 
 
@@ -589,11 +593,16 @@ SCENARIOS = [
     ("talladega_10car", "talladega.track", 10, 1500, ["rule", "rule_noisy", "random", "throttle", "throttle_left",
                                                       "brake_back", "idle", "rule_noisy", ("rule_bias", 0.2), "rule"],
      False, (900,)),
+    # round 3: non-default CarEnv(start_position=, start_angle=) (src/car_env.py:82-83,114-115,391,398)
+    ("nascar_start_pose", "nascar.track", 2, 1200, ["rule", "rule_noisy"], False, (600,),
+     {"start_position": (150.0, 4.0), "start_angle": 0.15}),
+    ("daytona_start_reversed", "daytona.track", 2, 900, ["rule", "rule_noisy"], False, (450,),
+     {"start_position": (60.0, -3.0), "start_angle": 3.0}),
 ]
 
 
 NEW = {"martinsville_all_idle", "daytona_low_reward", "daytona_damage", "nascar_backward", "nascar_banked_discrete",
-       "michigan_discrete1", "talladega_10car"}
+       "michigan_discrete1", "talladega_10car", "nascar_start_pose", "daytona_start_reversed"}
 
 
 def main():

@@ -918,6 +918,12 @@ EXPORT void *or_create(const char *track_path, int E, int C, int reset_on_lap) {
     e->truncated = calloc((size_t)E, sizeof(int));
     return e;
 }
+/* CarEnv(start_position=..., start_angle=...) (src/car_env.py:82-83,114-115): the pose Car() and
+   CarPhysics.reset_car use for every car (src/car_env.py:391,398); the default is the track's first
+   GRID/STARTLINE segment start (src/car_env.py:236-241) and angle 0. */
+EXPORT void or_set_start(void *h, double x, double y, double angle) {
+    oenv *e = h; e->start_x = x; e->start_y = y; e->start_angle = angle;
+}
 EXPORT void or_destroy(void *h) {
     oenv *e = h; if (!e) return;
     free(e->car); free(e->sim_time); free(e->created); free(e->pending); free(e->term_reason);

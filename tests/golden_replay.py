@@ -31,6 +31,15 @@ def continuous_actions(d, k):
     return DISCRETE_TO_CONTINUOUS[a] if is_discrete(d) else a
 
 
+def start_kwargs(d):
+    """CarEnv(start_position=, start_angle=) of a fixture recorded with a non-default start pose (else {})"""
+    if "start_angle" not in d:
+        return {}
+    sp = d["start_position"]
+    return {"start_position": None if np.isnan(sp).any() else (float(sp[0]), float(sp[1])),
+            "start_angle": float(d["start_angle"])}
+
+
 def first_mismatch(a, b):
     """index of the first step whose arrays differ (== semantics, NaN==NaN), or -1"""
     a = np.asarray(a); b = np.asarray(b)

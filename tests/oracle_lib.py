@@ -66,12 +66,20 @@ def _p(a, t):
 class OracleEnv:
     """E envs x C cars of the restated reference CarEnv on the CPU."""
 
-    def __init__(self, track_path, num_envs=1, num_cars=1, reset_on_lap=False):
+    def __init__(self, track_path, num_envs=1, num_cars=1, reset_on_lap=False, start_position=None, start_angle=0.0):
         self.L = lib()
         self.E, self.C = num_envs, num_cars
         self.h = self.L.or_create(track_path.encode(), num_envs, num_cars, int(reset_on_lap))
         if not self.h:
             raise FileNotFoundError(track_path)
+        if start_position is not None or start_angle != 0.0:
+            self.L.or_set_start.argtypes = [ctypes.c_void_p] + [ctypes.c_double] * 3
+            sx, sy = start_position if start_position is not None else (np.nan, np.nan)
+            if start_position is None:      # keep the track's default start point
+                s = self.segments()
+                row = next(r for r in s if r[0] in (0.0, 1.0))
+                sx, sy = row[2], row[3]
+            self.L.or_set_start(self.h, float(sx), float(sy), float(start_angle))
 
     def close(self):
         if self.h:
@@ -121,6 +129,63 @@ class OracleEnv:
         o = np.zeros(len(INFO_FIELDS), np.float64)
         self.L.or_car_info(self.h, idx, _p(o, ctypes.c_double))
         return dict(zip(INFO_FIELDS, o.tolist()))
+
+
+class OracleGroups:
+    """E envs of one batched run as several OracleEnv groups (one per track of a mixed batch, or shards of one
+    track), stepped in parallel host threads (the C step releases the GIL inside ctypes).  Global env e lives in
+    group g at local index j; outputs are gathered back into [E, ...] arrays in global env order."""
+
+    def __init__(self, tracks, num_cars, shards=1, threads=8):
+        from concurrent.futures import ThreadPoolExecutor
+        tracks = list(tracks)
+        self.E, self.C = len(tracks), num_cars
+        keys = sorted(set(tracks))
+        members = []
+        for t in keys:
+            envs = [e for e in range(self.E) if tracks[e] == t]
+            for s in range(shards):
+                part = envs[s::shards]
+                if part:
+                    members.append((t, np.array(part, np.int64)))
+        self.groups = [(OracleEnv(t, len(m), num_cars), m) for t, m in members]
+        self.where = {}
+        for g, (_, m) in enumerate(self.groups):
+            for j, e in enumerate(m.tolist()):
+                self.where[e] = (g, j)
+        self.pool = ThreadPoolExecutor(max_workers=min(threads, len(self.groups)))
+
+    def _gather(self, outs):
+        obs = np.zeros((self.E, self.C, 38), np.float32)
+        rew = np.zeros((self.E, self.C), np.float32)
+        cf = np.zeros((self.E, self.C), np.uint8)
+        ef = np.zeros((self.E, 3), np.int32)
+        for (_, m), (o, r, c, f) in zip(self.groups, outs):
+            obs[m], rew[m], cf[m], ef[m] = o, r, c, f
+        return obs, rew, cf, ef
+
+    def reset(self, envs=None):
+        if envs is None:
+            for env, _ in self.groups:
+                env.reset()
+        else:
+            for e in envs:
+                g, j = self.where[int(e)]
+                self.groups[g][0].reset(j)
+        return self.outputs()
+
+    def step(self, actions):
+        a = np.asarray(actions, np.float32).reshape(self.E, self.C, 2)
+        futs = [self.pool.submit(env.step, a[m]) for env, m in self.groups]
+        return self._gather([f.result() for f in futs])
+
+    def outputs(self):
+        return self._gather([env.outputs() for env, _ in self.groups])
+
+    def close(self):
+        self.pool.shutdown()
+        for env, _ in self.groups:
+            env.close()
 
 
 def car_state(env, idx, n_fields=71):

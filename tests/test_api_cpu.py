@@ -115,3 +115,43 @@ def test_sac_fixture_consistent():
     if os.path.exists(z):
         ref = load_sb3_actor(z)
         assert all(np.array_equal(ref[k], w[k]) for k in ACTOR_KEYS)
+
+
+def _shell_env(E=4, C=2):
+    """a BatchedCarEnv shell (no device handle) to exercise host-side argument checks on CPU"""
+    import torch
+    from nascargymnasium_amd.batched import BatchedCarEnv
+    env = BatchedCarEnv.__new__(BatchedCarEnv)
+    env.E, env.C, env.N, env.device = E, C, E * C, torch.device("cpu")
+    return env
+
+
+def test_rollout_out_buffers_rejected():
+    """rollout(trajectory=True, out=...) hands raw pointers to the kernels, which write record k at
+    ptr + k * E * C (or k * E): every malformed buffer is refused before any launch."""
+    import torch
+    env = _shell_env()
+    E, C, K = env.E, env.C, 5
+    good = (torch.zeros(K, E, C), torch.zeros(K, E, C, dtype=torch.uint8), torch.zeros(K, E, dtype=torch.uint8))
+    bad = {
+        "dtype": (torch.zeros(K, E, C, dtype=torch.float64), good[1], good[2]),
+        "flags dtype": (good[0], torch.zeros(K, E, C, dtype=torch.int32), good[2]),
+        "inner shape": (torch.zeros(K, E, C + 1), good[1], good[2]),
+        "env shape": (good[0], good[1], torch.zeros(K, E, C, dtype=torch.uint8)),
+        "rank": (torch.zeros(K, E * C), good[1], good[2]),
+        "too few": (torch.zeros(K - 1, E, C), good[1], good[2]),
+        "strided": (torch.zeros(K, C, E).transpose(1, 2), good[1], good[2]),
+        "not a tensor": (np.zeros((K, E, C), np.float32), good[1], good[2]),
+        "arity": good[:2],
+    }
+    for what, out in bad.items():
+        with pytest.raises(ValueError):
+            env.rollout(3, K, trajectory=True, out=out)
+        assert what
+    with pytest.raises(ValueError, match="trajectory=True"):
+        env.rollout(3, K, trajectory=False, out=good)
+    if torch.cuda.is_available():
+        return
+    env.device = torch.device("cuda", 0)          # right shapes, wrong device
+    with pytest.raises(ValueError, match="on cpu"):
+        env.rollout(3, K, trajectory=True, out=good)

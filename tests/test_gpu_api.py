@@ -5,7 +5,7 @@ import os
 import numpy as np
 import pytest
 
-from golden_replay import TRACKS, load
+from golden_replay import TRACKS, load, start_kwargs
 
 pytestmark = pytest.mark.gpu
 
@@ -16,7 +16,7 @@ def _replay_carenv(name, steps=None):
     C = int(d["C"])
     disc = bool(d.get("discrete", False))
     env = CarEnv(track_file=os.path.join(TRACKS, str(d["track"])), num_cars=C, reset_on_lap=bool(d["reset_on_lap"]),
-                 discrete_action_space=disc)
+                 discrete_action_space=disc, **start_kwargs(d))
     obs, info = env.reset(seed=0)
     want0 = d["obs0"][0] if C == 1 else d["obs0"]
     assert obs.shape == ((38,) if C == 1 else (C, 38)) and obs.dtype == np.float32
@@ -64,7 +64,7 @@ def _replay_carenv(name, steps=None):
 
 @pytest.mark.parametrize("name", ["daytona_mixed", "daytona_crash", "martinsville_lap", "nascar2_seam",
                                   "nascar_banked_discrete", "michigan_discrete1", "talladega_10car",
-                                  "daytona_low_reward"])
+                                  "daytona_low_reward", "nascar_start_pose", "daytona_start_reversed"])
 def test_carenv_golden(name):
     _replay_carenv(name)
 

@@ -10,16 +10,16 @@ import os
 import numpy as np
 import pytest
 
-from golden_replay import TRACKS, first_mismatch, is_discrete, load, scenarios
+from golden_replay import TRACKS, first_mismatch, is_discrete, load, scenarios, start_kwargs
 
 pytestmark = pytest.mark.gpu
 
 torch = pytest.importorskip("torch")
 
 
-def _env(track, E, C, reset_on_lap=False):
+def _env(track, E, C, reset_on_lap=False, **start):
     from nascargymnasium_amd.batched import BatchedCarEnv
-    return BatchedCarEnv(E, C, os.path.join(TRACKS, track), reset_on_lap=reset_on_lap, device="cuda:0")
+    return BatchedCarEnv(E, C, os.path.join(TRACKS, track), reset_on_lap=reset_on_lap, device="cuda:0", **start)
 
 
 def test_device_sincosf_matches_glibc():
@@ -59,7 +59,7 @@ def test_golden_trace_gpu(name):
     from nascargymnasium_amd import _lib
     d = load(name)
     C = int(d["C"]); E = 4
-    env = _env(str(d["track"]), E, C, bool(d["reset_on_lap"]))
+    env = _env(str(d["track"]), E, C, bool(d["reset_on_lap"]), **start_kwargs(d))
     env.set_perf_history(True)
     obs0 = env.reset().cpu().numpy()
     for e in range(E):

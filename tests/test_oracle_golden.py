@@ -14,7 +14,7 @@ import os
 import numpy as np
 import pytest
 
-from golden_replay import GOLDEN, TRACKS, continuous_actions, first_mismatch, load, scenarios
+from golden_replay import GOLDEN, TRACKS, continuous_actions, first_mismatch, load, scenarios, start_kwargs
 from oracle_lib import OracleEnv
 
 TRACK_NAMES = sorted(f[:-6] for f in os.listdir(TRACKS) if f.endswith(".track"))
@@ -50,7 +50,7 @@ INFO_MAP = [  # golden info column -> oracle field
 
 def replay_oracle(d):
     C = int(d["C"])
-    env = OracleEnv(os.path.join(TRACKS, str(d["track"])), 1, C, bool(d["reset_on_lap"]))
+    env = OracleEnv(os.path.join(TRACKS, str(d["track"])), 1, C, bool(d["reset_on_lap"]), **start_kwargs(d))
     obs0 = env.reset()[0][0]
     O, R, T, TR, RS, I = [], [], [], [], [], []
     keep = set(d["obs_steps"].tolist()) if "obs_steps" in d else None
@@ -90,7 +90,7 @@ def test_performance_info_bit_exact(name):
     from nascargymnasium_amd.car_env import DT, physics_stats, validate_performance
     d = load(name)
     C = int(d["C"])
-    env = OracleEnv(os.path.join(TRACKS, str(d["track"])), 1, C, bool(d["reset_on_lap"]))
+    env = OracleEnv(os.path.join(TRACKS, str(d["track"])), 1, C, bool(d["reset_on_lap"]), **start_kwargs(d))
     env.reset()
     hist = [deque(maxlen=600) for _ in range(C)]
     speed = [0.0] * C
