@@ -141,8 +141,9 @@ class Stepper:
     def __init__(self, env, policy, seed, acts=None, gather=None, rollout=0):
         self.env, self.pol, self.seed, self.acts, self.gather = env, POLICY_ID[policy], seed, acts, gather
         # device action sources (policy 2, the SAC actor, only on the sharded schedule) step through nascar_rollout
-        self.R = rollout if (acts is None and gather is None and (self.pol != 2 or env.rollout_streams > 0)) else 0
+        self.R = rollout if (acts is None and (self.pol != 2 or env.rollout_streams > 0)) else 0
         self.traj = None
+        self.gtraj = None
 
     def actions(self, i):
         if self.acts is not None:
@@ -150,6 +151,9 @@ class Stepper:
         return self.env.policy_actions(self.pol, seed=self.seed, step=i)
 
     def __call__(self, i):
+        if self.gather is not None and self.R:
+            self.run(i, 1)
+            return
         if self.acts is None and self.pol != 2:   # device driver computed inside the step launch (nascar_step_driven)
             self.env.step_driven(self.pol, seed=self.seed, step=i, auto_reset=True)
         else:
@@ -164,6 +168,21 @@ class Stepper:
                 self(i)
             return
         import torch
+        if self.gather is not None:   # K-step trajectory records (obs after every step + rewards / flags) to rank 0
+            e = self.env
+            if self.gtraj is None:
+                self.gtraj = (torch.empty(self.R + 1, e.E, e.C, 38, dtype=torch.float32, device=e.device),
+                              torch.empty(self.R, e.E, e.C, dtype=torch.float32, device=e.device),
+                              torch.empty(self.R, e.E, e.C, dtype=torch.uint8, device=e.device),
+                              torch.empty(self.R, e.E, dtype=torch.uint8, device=e.device))
+            k = 0
+            while k < K:
+                n = min(self.R, K - k)
+                ot, rew, cf, ef = e.rollout(self.pol, n, seed=self.seed, step0=first + k, auto_reset=True,
+                                            trajectory=True, obs_trajectory=True, out=self.gtraj)
+                self.gather.push(ot[1:n + 1], rew[:n], cf[:n], ef[:n])
+                k += n
+            return
         if trajectory and (self.traj is None or self.traj[0].shape[0] < K):
             e = self.env
             self.traj = (torch.empty(K, e.E, e.C, dtype=torch.float32, device=e.device),
@@ -241,20 +260,26 @@ def stats_pass(env, step, first, KR):
     what happened in those car-steps."""
     import torch
     tally = torch.zeros(7, dtype=torch.float64, device=env.device)
+    KR_timed = KR
     if step.R:
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         step.run(first, KR, trajectory=True)         # allocates the trajectory buffers outside the bracket
         e0.record()
         step.run(first + KR, KR, trajectory=True)
         e1.record()
-        rew, cf, ef = step.traj
-        cf, ef = cf[:KR], ef[:KR]
+        if step.gather is not None:                  # the gathered path: its last rollout call's records
+            n = KR % step.R or step.R
+            cf, ef = step.gtraj[2][:n], step.gtraj[3][:n]
+            KR = n
+        else:
+            rew, cf, ef = step.traj
+            cf, ef = cf[:KR], ef[:KR]
         tally += torch.stack([((cf & 4) != 0).sum(), ((cf & 8) != 0).sum(), ((cf & 1) != 0).sum(),
                               ((cf & 2) != 0).sum(), ((ef & 8) != 0).sum(), ((cf & 128) != 0).sum(),
                               torch.zeros((), device=env.device)]).double()
         tally[6] = env.obs[..., 4].double().sum() * KR    # speed sampled at the window's last step
         torch.cuda.synchronize()
-        return e0.elapsed_time(e1) / KR, tally.tolist()
+        return e0.elapsed_time(e1) / KR_timed, tally.tolist(), KR
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(KR)]
     for i in range(KR):
         a = step.actions(first + i)
@@ -267,7 +292,7 @@ def stats_pass(env, step, first, KR):
                               env.obs[..., 4].double().sum()]).double()
     torch.cuda.synchronize()
     kern_ms = sum(s.elapsed_time(e) for s, e in ev) / KR
-    return kern_ms, tally.tolist()
+    return kern_ms, tally.tolist(), KR
 
 
 def main():
@@ -339,7 +364,7 @@ def main():
     gather = None
     if args.gather:
         from nascargymnasium_amd.gather import ObsGather
-        gather = ObsGather(E, C, dev)
+        gather = ObsGather(E, C, dev, steps=max(1, args.rollout))
     if args.policy == "sac":
         from nascargymnasium_amd.policy import random_actor
         env.set_actor(random_actor(rank))
@@ -364,12 +389,10 @@ def main():
     if args.save_state:
         torch.save({"state": env.get_state().cpu(), "obs": env.obs.cpu(), "step": base}, args.save_state)
     step.gather = gather
-    if gather is not None:
-        step.R = 0
     step.run(base, W)
     elapsed = timed(step, base + W, K, world)
     KR = min(K, 50)
-    kern_ms, tally = stats_pass(env, step, base + W + K, KR)
+    kern_ms, tally, KT = stats_pass(env, step, base + W + K, KR)   # KT: the steps the tallies cover
     per_step = None
     if step.R:   # the per-step path on the same envs, timed the same way (labelled secondary)
         ps = Stepper(env, args.policy, rank, acts, None, 0)
@@ -396,11 +419,11 @@ def main():
             traffic = tj["bytes_per_step"]
             tnote = f"rocprofv3 FETCH_SIZE/WRITE_SIZE passes of this build and workload ({tj.get('tag')}, " \
                     f"profiles/pmc_traffic.json; not re-measured in this run)"
-    ncs = world * E * C * KR
+    ncs = world * E * C * KT
     wstats = {"source": POLICY_TEXT[args.policy], "settle_steps": S if not args.load_state else f"state file {args.load_state}",
               "staggered_env_ages": closed and not args.no_stagger, "window_car_steps": ncs,
               "contact_frac": tally[0] / ncs, "lap_completed_frac": tally[1] / ncs, "disabled_frac": tally[2] / ncs,
-              "just_disabled_frac": tally[3] / ncs, "env_reset_frac": tally[4] / (world * E * KR),
+              "just_disabled_frac": tally[3] / ncs, "env_reset_frac": tally[4] / (world * E * KT),
               "mean_speed_ms": tally[6] / ncs * 111.1, "settle_s": t_settle}
     track_name = "mixed 8-track" if args.mixed else os.path.basename(tpath)[:-6]
     settle_txt = (f", steady state after {S} settle steps" + (" (env ages staggered over the 180 s episode)"
@@ -429,7 +452,8 @@ def main():
                    "launch": launch_txt,
                    "car_contact": "on (build-only extension, no reference counterpart)" if args.car_contact else "off (reference)",
                    "track": "mixed (env e: track e mod 8)" if args.mixed else os.path.basename(tpath),
-                   "parallelism": f"dp{world} (env shards" + (", RCCL gather of obs/reward/flags to rank 0 per step)" if gather else ", no collective)")},
+                   "parallelism": f"dp{world} (env shards" + ((", RCCL gather to rank 0 of every step's obs/reward/flags, one trajectory record per rollout call)" if step.R
+                                   else ", RCCL gather of obs/reward/flags to rank 0 per step)") if gather else ", no collective)")},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": tnote,
                      "kernel": kernel_txt, "kernel_ms": kern_ms,

@@ -87,9 +87,14 @@ int nascar_step_driven(NascarHandle* h, int32_t policy, uint64_t seed, int64_t s
  *            rollout only: each shard runs the actor on its own cars, one shard unless the envs sit in one
  *            track's workgroups in order)
  *   obs:     [E*C*38] float32, in: the current observation, out: the last step's
- *   traj != 0: reward [steps][E*C], car_flags [steps][E*C], env_flags [steps][E] (per-step records);
+ *   traj & NASCAR_TRAJ_RECORDS: reward [steps][E*C], car_flags [steps][E*C], env_flags [steps][E] (per-step records);
  *   traj == 0: reward [E*C], car_flags [E*C], env_flags [E] hold the last step's values.
+ *   traj & NASCAR_TRAJ_OBS (with NASCAR_TRAJ_RECORDS; sharded rollout only): obs is [steps + 1][E*C*38]; record 0
+ *            holds the current observation on entry (read by the action source of step 0) and step k writes
+ *            record k + 1 (read by step k + 1) -- a learner's per-step observation buffer, no copies in between.
  * car_flags / env_flags may be NULL.  No terminal observations (auto-reset obs overwrite the final ones). */
+#define NASCAR_TRAJ_RECORDS 1
+#define NASCAR_TRAJ_OBS 2
 int nascar_rollout(NascarHandle* h, int32_t policy, uint64_t seed, int64_t step0, int32_t steps, float* obs,
                    float* reward, uint8_t* car_flags, uint8_t* env_flags, int32_t auto_reset, int32_t traj, void* stream);
 
@@ -136,7 +141,8 @@ int nascar_policy_actions(NascarHandle* h, int32_t policy, uint64_t seed, int64_
 /* SB3 SAC MlpPolicy actor weights (PyTorch layouts, host float32): w1 [256][38], b1 [256],
  * w2 [256][256], b2 [256], w3 = mu.weight [2][256], b3 = mu.bias [2]  (obs_dim 38, hidden 256,
  * act_dim 2; other shapes are rejected).  Replaces SAC.load + policy.predict
- * (game/control/sac_control_class.py:48-115) with one fused bf16-MFMA kernel. */
+ * (game/control/sac_control_class.py:48-115) with one fused actor kernel: float32 by default, the bf16-operand
+ * MFMA kernel on request (nascar_set_actor_precision). */
 int nascar_set_actor(NascarHandle* h, const float* w1, const float* b1, const float* w2, const float* b2,
                      const float* w3, const float* b3, int32_t obs_dim, int32_t hidden, int32_t act_dim);
 /* Actor arithmetic for policy 2 and nascar_actor_forward: 1 (default) = float32 throughout (the reference's

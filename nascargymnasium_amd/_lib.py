@@ -23,6 +23,7 @@ OBS_DIM = 38
 # car flag bits / env flag bits (csrc/nascar_layout.h)
 CF_DISABLED, CF_JUST_DISABLED, CF_COLLISION, CF_LAP, CF_ERROR = 1, 2, 4, 8, 128
 EF_TERMINATED, EF_TRUNCATED, EF_RESET = 1, 2, 8
+TRAJ_RECORDS, TRAJ_OBS = 1, 2          # nascar_rollout traj flags (include/nascar.h)
 REASONS = {0: None, 1: "all_cars_disabled", 2: "all_active_cars_low_reward (threshold: -250.0)",
            3: "time_limit", 4: "truncated"}
 

@@ -163,39 +163,59 @@ class BatchedCarEnv:
         return self.obs, self.reward
 
     def rollout(self, policy: int, steps: int, seed: int = 0, step0: int = 0, auto_reset: bool = True,
-                trajectory: bool = False, out=None):
+                trajectory: bool = False, out=None, obs_trajectory: bool = False):
         """`steps` env steps in one call (sharded over streams, or one fused launch: set_rollout_streams), actions
         from device action source `policy` (0 uniform, 1 rule driver, 2 the SAC actor -- sharded only, 3 noisy rule
         driver) on the previous observation; equals `steps` x (policy_actions(policy, seed, step0 + k) +
         step(..., auto_reset)).  Returns (obs, reward, car_flags, env_flags): the last step's, or with
-        trajectory=True the per-step records [steps, E, C] / [steps, E] (obs is always the last step's)."""
+        trajectory=True the per-step records [steps, E, C] / [steps, E] (obs the last step's).  obs_trajectory=True
+        (with trajectory=True, sharded rollout only) also records every step's observation: obs [steps + 1, E, C, 38],
+        record 0 the observation before the rollout, record k + 1 the one after step k (a learner's rollout buffer,
+        written by the kernels in place).  `out`: caller-owned buffers (reward, car_flags, env_flags), preceded by
+        obs when obs_trajectory, each with at least the records this call writes."""
         steps = int(steps)
         if out is not None and not trajectory:
             raise ValueError("`out` buffers are written only with trajectory=True")
+        if obs_trajectory and not trajectory:
+            raise ValueError("obs_trajectory needs trajectory=True")
         if trajectory and out is not None:      # caller-owned per-step buffers (at least `steps` records)
-            if len(out) != 3:
-                raise ValueError("out must be (reward, car_flags, env_flags)")
-            rew, cf, ef = out
-            for name, t, dt, inner in (("reward", rew, torch.float32, (self.E, self.C)),
-                                       ("car_flags", cf, torch.uint8, (self.E, self.C)),
-                                       ("env_flags", ef, torch.uint8, (self.E,))):
-                self._check_record_buffer(name, t, dt, inner, steps)
+            n_out = 4 if obs_trajectory else 3
+            if len(out) != n_out:
+                raise ValueError("out must be (" + ("obs, " if obs_trajectory else "") + "reward, car_flags, env_flags)")
+            ot = out[0] if obs_trajectory else None
+            rew, cf, ef = out[n_out - 3:]
+            checks = [("reward", rew, torch.float32, (self.E, self.C), steps),
+                      ("car_flags", cf, torch.uint8, (self.E, self.C), steps),
+                      ("env_flags", ef, torch.uint8, (self.E,), steps)]
+            if obs_trajectory:
+                checks.append(("obs", ot, torch.float32, (self.E, self.C, _lib.OBS_DIM), steps + 1))
+            for name, t, dt, inner, n in checks:
+                self._check_record_buffer(name, t, dt, inner, n)
         elif trajectory:
             rew = torch.empty(steps, self.E, self.C, dtype=torch.float32, device=self.device)
             cf = torch.empty(steps, self.E, self.C, dtype=torch.uint8, device=self.device)
             ef = torch.empty(steps, self.E, dtype=torch.uint8, device=self.device)
+            ot = (torch.empty(steps + 1, self.E, self.C, _lib.OBS_DIM, dtype=torch.float32, device=self.device)
+                  if obs_trajectory else None)
         else:
-            rew, cf, ef = self.reward, self.car_flags, self.env_flags
+            rew, cf, ef, ot = self.reward, self.car_flags, self.env_flags, None
+        traj = (_lib.TRAJ_RECORDS if trajectory else 0) | (_lib.TRAJ_OBS if obs_trajectory else 0)
         with torch.cuda.device(self.device):
-            _lib.check(self.L.nascar_rollout(self.h, int(policy), int(seed), int(step0), steps, _ptr(self.obs), _ptr(rew),
-                                             _ptr(cf), _ptr(ef), int(auto_reset), int(trajectory), _stream()))
-        if trajectory and steps > 0:
-            self.reward.copy_(rew[steps - 1]); self.car_flags.copy_(cf[steps - 1]); self.env_flags.copy_(ef[steps - 1])
-        return self.obs, rew, cf, ef
+            if ot is not None:
+                ot[0].copy_(self.obs)
+            _lib.check(self.L.nascar_rollout(self.h, int(policy), int(seed), int(step0), steps,
+                                             _ptr(ot if ot is not None else self.obs), _ptr(rew), _ptr(cf), _ptr(ef),
+                                             int(auto_reset), traj, _stream()))
+            if trajectory and steps > 0:
+                self.reward.copy_(rew[steps - 1]); self.car_flags.copy_(cf[steps - 1]); self.env_flags.copy_(ef[steps - 1])
+                if ot is not None:
+                    self.obs.copy_(ot[steps])
+        return (ot if ot is not None else self.obs), rew, cf, ef
 
     def _check_record_buffer(self, name, t, dtype, inner, steps):
         """the kernels write record k at data_ptr + k * prod(inner) elements: anything but a contiguous tensor of
-        this dtype on this device with shape [>= steps, *inner] would be written out of bounds"""
+        this dtype on this device with shape [>= steps, *inner] would be written out of bounds (steps: the records
+        this call writes)"""
         if not isinstance(t, torch.Tensor):
             raise ValueError(f"out {name}: expected a torch.Tensor, got {type(t).__name__}")
         if t.device != self.device:

@@ -2702,11 +2702,13 @@ extern "C" int nascar_step_driven(NascarHandle* h, int32_t policy, uint64_t seed
 }
 // one env step of step-kernel workgroups [P.blk0, P.blk0 + nb) on stream s:
 // model_kernel -> logic_kernel -> sensor_kernel (pass A for every car, pass B for auto-reset cars)
+// obs_in: the observation the device driver reads (the previous step's); obs: where this step's is written
 static int launch_step_range(NascarHandle* h, const Params& P, int nb, const void* actions, int32_t discrete, int policy,
-                             uint64_t seed, int64_t step, float* obs, float* reward, uint8_t* car_flags,
-                             uint8_t* env_flags, int32_t auto_reset, float* terminal_obs, hipStream_t s) {
+                             uint64_t seed, int64_t step, const float* obs_in, float* obs, float* reward,
+                             uint8_t* car_flags, uint8_t* env_flags, int32_t auto_reset, float* terminal_obs,
+                             hipStream_t s) {
   hipLaunchKernelGGL(model_kernel, dim3(nb), dim3(SBLOCK), 0, s, P, actions, discrete, terminal_obs != nullptr,
-                     policy, seed, step, (const float*)obs);
+                     policy, seed, step, obs_in);
   HIPCHK(hipGetLastError());
   if (h->car_contact) {
     hipLaunchKernelGGL(car_contact_kernel, dim3(nb), dim3(SBLOCK), 0, s, P);
@@ -2729,8 +2731,8 @@ static int step_impl(NascarHandle* h, const void* actions, int32_t discrete, int
   // Whole grid on the caller's stream: splitting one step over streams needs a fork and a join per step, and
   // the per-step barrier measured slower than one grid (tools/streams_exp.py: 2 / 4 shards 0.252 / 0.277 ms vs
   // 0.224 ms).  Shards pay off only when they run many steps unsynchronised: the sharded nascar_rollout.
-  return launch_step_range(h, P, h->nblocks, actions, discrete, policy, seed, step, obs, reward, car_flags, env_flags,
-                           auto_reset, terminal_obs, (hipStream_t)stream);
+  return launch_step_range(h, P, h->nblocks, actions, discrete, policy, seed, step, obs, obs, reward, car_flags,
+                           env_flags, auto_reset, terminal_obs, (hipStream_t)stream);
 }
 
 // Sharded rollout: the workgroups split into S contiguous ranges (shards of whole envs), each stepped `steps`
@@ -2778,9 +2780,12 @@ static int rollout_sharded(NascarHandle* h, int S, int32_t policy, uint64_t seed
     for (int s = 1; s < S; ++s) HIPCHK(hipStreamWaitEvent(shard_stream(s), h->ev_fork, 0));
   }
   const size_t NC = (size_t)h->N, E = (size_t)h->E;
+  const bool obs_traj = (traj & NASCAR_TRAJ_OBS) != 0;   // obs = [steps + 1][N][38]: record 0 in, record k + 1 out
   auto enqueue = [&]() -> int {
     for (int k = 0; k < steps; ++k) {
       const size_t ko = traj ? (size_t)k : 0;
+      float* o_in = obs_traj ? obs + (size_t)k * NC * 38 : obs;
+      float* o_out = obs_traj ? obs + (size_t)(k + 1) * NC * 38 : obs;
       for (int s = 0; s < S; ++s) {
         const int b0 = (int)((int64_t)h->nblocks * s / S), b1 = (int)((int64_t)h->nblocks * (s + 1) / S);
         Params P = P0;
@@ -2788,11 +2793,11 @@ static int rollout_sharded(NascarHandle* h, int S, int32_t policy, uint64_t seed
         if (actor) {
           const size_t c0 = S == 1 ? 0 : (size_t)b0 * h->epb * h->C;
           const size_t c1 = S == 1 ? NC : std::min((size_t)b1 * h->epb, E) * h->C;
-          if (c1 > c0) launch_actor(h, (int)(c1 - c0), obs + c0 * 38, h->d_ro_act + c0 * 2, shard_stream(s));
+          if (c1 > c0) launch_actor(h, (int)(c1 - c0), o_in + c0 * 38, h->d_ro_act + c0 * 2, shard_stream(s));
           HIPCHK(hipGetLastError());
         }
         if (launch_step_range(h, P, b1 - b0, actor ? h->d_ro_act : nullptr, 0, actor ? -1 : policy, seed, step0 + k,
-                              obs, reward + ko * NC,
+                              o_in, o_out, reward + ko * NC,
                               car_flags ? car_flags + ko * NC : nullptr, env_flags ? env_flags + ko * E : nullptr,
                               auto_reset, nullptr, shard_stream(s)))
           return -1;
@@ -2826,6 +2831,9 @@ extern "C" int nascar_rollout(NascarHandle* h, int32_t policy, uint64_t seed, in
   if (!h || !obs || !reward) return fail("null argument");
   if (policy < 0 || policy > 3) return fail("rollout policy must be 0, 1, 2 or 3 (got %d)", policy);
   if (policy == 2 && h->ro_streams == 0) return fail("the fused rollout kernel has no actor (policy 2): use the sharded rollout");
+  if (traj & ~(NASCAR_TRAJ_RECORDS | NASCAR_TRAJ_OBS)) return fail("unknown trajectory flags 0x%x", traj);
+  if ((traj & NASCAR_TRAJ_OBS) && !(traj & NASCAR_TRAJ_RECORDS)) return fail("an obs trajectory needs the per-step records (traj bit 0)");
+  if ((traj & NASCAR_TRAJ_OBS) && h->ro_streams == 0) return fail("obs trajectories need the sharded rollout (rollout streams >= 1)");
   if (steps < 0) return fail("steps must be >= 0");
   if (steps == 0) return 0;
   h->pristine = false;

@@ -150,6 +150,15 @@ def test_rollout_out_buffers_rejected():
         assert what
     with pytest.raises(ValueError, match="trajectory=True"):
         env.rollout(3, K, trajectory=False, out=good)
+    with pytest.raises(ValueError, match="trajectory=True"):
+        env.rollout(3, K, obs_trajectory=True)
+    obs_ok = torch.zeros(K + 1, E, C, 38)
+    with pytest.raises(ValueError, match="fewer than"):      # obs records: steps + 1 (record 0 = the entry obs)
+        env.rollout(3, K, trajectory=True, obs_trajectory=True, out=(torch.zeros(K, E, C, 38),) + good)
+    with pytest.raises(ValueError):                          # obs missing from out
+        env.rollout(3, K, trajectory=True, obs_trajectory=True, out=good)
+    with pytest.raises(ValueError):
+        env.rollout(3, K, trajectory=True, obs_trajectory=True, out=(obs_ok[..., :37],) + good)
     if torch.cuda.is_available():
         return
     env.device = torch.device("cuda", 0)          # right shapes, wrong device

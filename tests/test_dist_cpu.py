@@ -53,7 +53,20 @@ def test_bench_reduction_world2():
         assert distinct
 
 
-def _gather_worker(rank, world, port, q):
+def _record(rank, step, E, C, K):
+    """synthetic record of `rank` for pushes step*K .. step*K + K - 1: obs [K, E, C, 38] etc. (K = 1: no step dim)"""
+    import torch
+    ks = torch.arange(K, dtype=torch.float32) + step * K
+    obs = (100.0 * rank + ks).view(K, 1, 1, 1) + torch.arange(38.0) + torch.zeros(K, E, C, 38)
+    rew = (-0.05 * (rank + 1) + ks).view(K, 1, 1) + torch.zeros(K, E, C)
+    cf = (4 * rank + ks.to(torch.uint8)).view(K, 1, 1).expand(K, E, C).contiguous()
+    ef = torch.stack([torch.tensor([rank, int(k), 8 + rank], dtype=torch.uint8) for k in ks.tolist()])
+    if K == 1:
+        return obs[0], rew[0], cf[0], ef[0]
+    return obs, rew, cf, ef
+
+
+def _gather_worker(rank, world, port, q, K):
     import torch
     import torch.distributed as dist
     sys.path.insert(0, ROOT)
@@ -61,29 +74,31 @@ def _gather_worker(rank, world, port, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from nascargymnasium_amd.gather import ObsGather
     E, C = 3, 2
-    g = ObsGather(E, C, torch.device("cpu"))
-    got = []
-    for step in range(2):
-        obs = torch.full((E, C, 38), 100.0 * rank + step) + torch.arange(38.0)
-        rew = torch.full((E, C), -0.05 * (rank + 1) + step)
-        cf = torch.full((E, C), 4 * rank + step, dtype=torch.uint8)
-        ef = torch.tensor([rank, step, 8 + rank], dtype=torch.uint8)
-        g.push(obs, rew, cf, ef)
+    g = ObsGather(E, C, torch.device("cpu"), steps=K)
+    got, held = [], None
+    for step in range(3):
+        g.push(*_record(rank, step, E, C, K))
+        if held is not None:    # the previous record's views survive one more push (double-buffered receive)
+            got.append(("held", step - 1, {k: v.numpy().copy() for k, v in held.items()}))
         r = g.received()
         if r is not None:
             # numpy copies: tensors in an mp queue travel by shared-memory handle, which dies with this process
-            got.append({k: v.numpy().copy() for k, v in r.items()})
+            got.append(("now", step, {k: v.numpy().copy() for k, v in r.items()}))
+        held = r
     q.put((rank, got))
     dist.destroy_process_group()
 
 
-def test_obs_gather_world2():
-    """ObsGather (the optional cfg4 gather of obs/reward/flags to rank 0) over gloo, world size 2."""
+@pytest.mark.parametrize("K", [1, 4])
+def test_obs_gather_world2(K):
+    """ObsGather (the optional cfg4 gather of obs/reward/flags to rank 0) over gloo, world size 2: per-step records
+    (K = 1) and K-step trajectory records; received() returns exactly the last push, and the views of the push before
+    it still hold that record after the next push."""
     import torch
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
-    procs = [ctx.Process(target=_gather_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_gather_worker, args=(r, 2, port, q, K)) for r in range(2)]
     for p in procs:
         p.start()
     res = dict(q.get(timeout=120) for _ in procs)
@@ -91,10 +106,13 @@ def test_obs_gather_world2():
         p.join(timeout=60)
         assert p.exitcode == 0
     assert res[1] == []
-    for step, r in enumerate(res[0]):
-        assert r["obs"].shape == (2, 3, 2, 38)
+    assert [(w, s) for w, s, _ in res[0]] == [("now", 0), ("held", 0), ("now", 1), ("held", 1), ("now", 2)]
+    lead = (K,) if K > 1 else ()
+    for _, step, r in res[0]:
+        assert r["obs"].shape == (2,) + lead + (3, 2, 38)
         for rank in range(2):
-            assert torch.equal(torch.from_numpy(r["obs"][rank]), torch.full((3, 2, 38), 100.0 * rank + step) + torch.arange(38.0))
-            assert torch.equal(torch.from_numpy(r["reward"][rank]), torch.full((3, 2), -0.05 * (rank + 1) + step))
-            assert torch.equal(torch.from_numpy(r["car_flags"][rank]), torch.full((3, 2), 4 * rank + step, dtype=torch.uint8))
-            assert r["env_flags"][rank].tolist() == [rank, step, 8 + rank]
+            obs, rew, cf, ef = _record(rank, step, 3, 2, K)
+            assert torch.equal(torch.from_numpy(r["obs"][rank]), obs)
+            assert torch.equal(torch.from_numpy(r["reward"][rank]), rew)
+            assert torch.equal(torch.from_numpy(r["car_flags"][rank]), cf)
+            assert torch.equal(torch.from_numpy(r["env_flags"][rank]), ef)

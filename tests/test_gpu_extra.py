@@ -20,26 +20,45 @@ def _actions(rng, E, C, k):
 
 
 def test_obs_gather_rccl_world1():
-    """ObsGather over RCCL (torch.distributed "nccl", world size 1, side stream): the gathered record of every
-    step equals the env's own outputs bit for bit."""
+    """ObsGather over RCCL (torch.distributed "nccl", world size 1, side stream): per-step records after every
+    step, then K-step trajectory records of the sharded rollout (obs_trajectory), bit for bit equal to the env's own
+    outputs -- received() read without an explicit wait(), and the previous record's views still intact after the
+    next push (double-buffered receive)."""
     import torch.distributed as dist
     from nascargymnasium_amd.batched import BatchedCarEnv
     from nascargymnasium_amd.gather import ObsGather
     s = socket.socket(); s.bind(("127.0.0.1", 0)); port = s.getsockname()[1]; s.close()
     dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
     try:
-        E, C = 64, 4
+        E, C, K = 64, 4, 25
         env = BatchedCarEnv(E, C, os.path.join(TRACKS, "daytona.track"), device="cuda:0")
         g = ObsGather(E, C, env.device)
         env.reset()
         for k in range(40):
             env.launch_step(env.policy_actions(3, seed=1, step=k).clone(), auto_reset=True)
             g.push(env.obs, env.reward, env.car_flags, env.env_flags)
-            g.wait()
             r = g.received()
             assert torch.equal(r["obs"][0], env.obs) and torch.equal(r["reward"][0], env.reward)
             assert torch.equal(r["car_flags"][0], env.car_flags) and torch.equal(r["env_flags"][0], env.env_flags)
-        env.close()
+        gt = ObsGather(E, C, env.device, steps=K)
+        twin = BatchedCarEnv(E, C, os.path.join(TRACKS, "daytona.track"), device="cuda:0")
+        twin.set_state(env.get_state()); twin.obs.copy_(env.obs)
+        held, want = None, None
+        for j in range(4):
+            ot, rew, cf, ef = env.rollout(3, K, seed=1, step0=40 + j * K, trajectory=True, obs_trajectory=True)
+            # the obs records equal the per-step path's observations step by step
+            for k in range(K):
+                twin.step_driven(3, seed=1, step=40 + j * K + k, auto_reset=True)
+                assert torch.equal(ot[k + 1], twin.obs) and torch.equal(rew[k], twin.reward), (j, k)
+            gt.push(ot[1:], rew, cf, ef)
+            if held is not None:
+                assert torch.equal(held["obs"][0], want[0]) and torch.equal(held["reward"][0], want[1]), j
+            r = gt.received()
+            assert torch.equal(r["obs"][0], ot[1:]) and torch.equal(r["reward"][0], rew)
+            assert torch.equal(r["car_flags"][0], cf) and torch.equal(r["env_flags"][0], ef)
+            held, want = r, (ot[1:].clone(), rew.clone())
+        for x in (env, twin):
+            x.close()
     finally:
         dist.destroy_process_group()
 
