@@ -17,9 +17,12 @@ instead of inside it, since one workgroup never mixes tracks.
 ``return_tensors=False`` (default) returns numpy arrays like an SB3 VecEnv;
 ``return_tensors=True`` keeps obs / rewards / dones on the device and makes no host
 synchronisation per step in single-track mode: actions are validated on the device
-(an invalid action raises at the next point that reads the host: ``infos``, ``reset``
-or ``check_actions()``), and ``infos`` is a list built from device copies the first
-time it is read.
+(an invalid action raises AssertionError, as the reference's ``assert
+self.action_space.contains(action)``, src/car_env.py:694, at the next point that reads
+the host: ``infos``, ``reset``, ``check_actions()``, or at the latest ``check_every``
+steps later -- one small host read per ``check_every`` steps), and ``infos`` is a list
+built from device copies the first time it is read.  The env state after an invalid
+action is undefined (the reference never steps one).
 """
 import random
 import time
@@ -34,7 +37,8 @@ from .track import available_tracks, track_path
 
 
 class _LazyInfos(list):
-    """SB3's per-env info list, materialised from the step's device tensors on first use."""
+    """SB3's per-env info list, materialised from the step's device tensors on first use (any list operation fills
+    it first, so it reads exactly like the eager list)."""
 
     def __init__(self, build):
         super().__init__()
@@ -45,27 +49,33 @@ class _LazyInfos(list):
             b, self._build = self._build, None
             super().extend(b())
 
-    def __getitem__(self, i):
-        self._fill()
-        return super().__getitem__(i)
-
-    def __iter__(self):
-        self._fill()
-        return super().__iter__()
-
-    def __len__(self):
-        self._fill()
-        return super().__len__()
-
     def __reduce__(self):
         self._fill()
         return (list, (list(self),))
 
 
+def _filled(name):
+    base = getattr(list, name)
+
+    def method(self, *args, **kwargs):
+        self._fill()
+        return base(self, *args, **kwargs)
+    method.__name__ = name
+    return method
+
+
+for _name in ("__getitem__", "__iter__", "__len__", "__repr__", "__str__", "__eq__", "__ne__", "__lt__", "__le__",
+              "__gt__", "__ge__", "__contains__", "__reversed__", "__add__", "__mul__", "__rmul__", "__iadd__",
+              "__imul__", "__setitem__", "__delitem__", "copy", "index", "count", "append", "extend", "insert", "pop",
+              "remove", "reverse", "sort", "clear"):
+    setattr(_LazyInfos, _name, _filled(_name))
+_LazyInfos.__hash__ = None
+
+
 class VecCarEnv:
     def __init__(self, num_envs: int, track_file: Optional[Union[str, Sequence[str]]] = "daytona", num_cars: int = 1,
                  discrete_action_space: bool = False, reset_on_lap: bool = False, device="cuda",
-                 return_tensors: bool = False, seed: Optional[int] = None):
+                 return_tensors: bool = False, seed: Optional[int] = None, check_every: int = 64):
         import torch
         from .batched import BatchedCarEnv
         self._torch = torch
@@ -93,6 +103,8 @@ class VecCarEnv:
         self._ep_ret = torch.zeros(self.num_envs, self.num_cars, dtype=torch.float64, device=self.device)
         self._ep_len = torch.zeros(self.num_envs, dtype=torch.int64, device=self.device)
         self._bad = torch.zeros((), dtype=torch.bool, device=self.device)    # invalid action seen (device flag)
+        self.check_every = max(1, int(check_every))   # return_tensors: read the flag at least this often
+        self._unchecked = 0
         self._attrs = [dict() for _ in range(self.num_envs)]
         # per env, the tracks of its last 64 episodes (random-track mode)
         self.episode_tracks = [deque(maxlen=64) for _ in range(self.num_envs)]
@@ -136,12 +148,14 @@ class VecCarEnv:
             bad = (a < -1) | (a > 1) | torch.isnan(a)
         self._bad |= bad.any()             # device-side check, read at the next host synchronisation
         self._actions = a.contiguous()
-        if not self.return_tensors:
+        self._unchecked += 1
+        if not self.return_tensors or self._unchecked >= self.check_every:
             self.check_actions()
 
     def check_actions(self):
         """Raise AssertionError (the reference's `assert self.action_space.contains(action)`, src/car_env.py:694)
         if any action handed to step_async since the last check was outside the action space."""
+        self._unchecked = 0
         if bool(self._bad):
             self._bad.zero_()
             raise AssertionError("Invalid action: continuous actions must be in [-1, 1], discrete in {0..4}")

@@ -164,3 +164,20 @@ def test_rollout_out_buffers_rejected():
     env.device = torch.device("cuda", 0)          # right shapes, wrong device
     with pytest.raises(ValueError, match="on cpu"):
         env.rollout(3, K, trajectory=True, out=good)
+
+
+def test_lazy_infos_fill_on_any_access():
+    """VecCarEnv's lazy info list (return_tensors=True) behaves as the eager list for every list operation."""
+    import pickle
+    from nascargymnasium_amd.vec_env import _LazyInfos
+    want = [{"a": 1}, {}, {"episode": {"r": 1.0}}]
+    mk = lambda: _LazyInfos(lambda: [dict(x) for x in want])   # noqa: E731
+    assert repr(mk()) == repr(want) and str(mk()) == str(want)
+    assert mk() == want and not (mk() != want)
+    assert mk().copy() == want and {"a": 1} in mk()
+    assert mk().index({}) == 1 and mk().count({}) == 1
+    assert list(reversed(mk())) == want[::-1] and mk() + [] == want and [] + list(mk()) == want
+    assert len(mk()) == 3 and mk()[2] == want[2] and list(mk()) == want
+    x = mk(); x.append({"b": 2}); assert len(x) == 4 and x[3] == {"b": 2}
+    assert pickle.loads(pickle.dumps(mk())) == want
+    assert bool(mk()) and mk() * 2 == want * 2

@@ -235,6 +235,14 @@ def test_vec_env_tensor_path_has_lazy_infos_and_device_validation():
     venv.step(torch.full((E, 2, 2), 2.0, device="cuda"))       # invalid: reported at the next host read
     with pytest.raises(AssertionError):
         venv.check_actions()
+    # bounded: a loop that never reads infos still sees the error within check_every steps (or at reset)
+    venv.step(torch.full((E, 2, 2), -3.0, device="cuda"))
+    with pytest.raises(AssertionError):
+        for _ in range(venv.check_every):
+            venv.step(torch.zeros(E, 2, 2, device="cuda"))
+    venv.step(torch.full((E, 2, 2), float("nan"), device="cuda"))
+    with pytest.raises(AssertionError):
+        venv.reset()
     assert venv.get_attr("track_file")[0].endswith("martinsville.track")
     venv.set_attr("foo", 3, indices=[1])
     assert venv.get_attr("foo", indices=[1]) == [3]
