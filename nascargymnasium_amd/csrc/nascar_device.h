@@ -607,7 +607,15 @@ struct VC {
   VCP p[2]; V2 normal; float nm[4]; float K[4]; int pointCount;
   V2 cB; float aB; V2 vB; float wB;
   V2 ln, lp, lps[2]; int pcount, type, ci;
+  Rot qB; uint32_t aB0;   // the static wall's b2Rot (its body transform) and the angle bits it was set from
 };
+// b2Rot::Set(aB) of the static body B inside the solvers: B never moves (mB = iB = 0), so aB keeps the wall's angle
+// bit for bit and its rotation is the wall's body transform (glibc sinf/cosf of that same float, computed when the
+// wall was created) -- no sincosf per solver point.  Any other angle (only possible through non-finite impulses)
+// takes the full b2Rot::Set.
+__device__ __forceinline__ Rot rot_static(float a, uint32_t a0bits, Rot q0) {
+  return __float_as_uint(a) == a0bits ? q0 : rot_set(a);
+}
 struct BodyState { V2 c; float a; V2 v; float w; };
 // unroll count of the per-contact loops below: full for islands of <= 2 contacts (register-resident), else a loop
 #define UNROLL_SMALL NUNR<NMAX>::v
@@ -626,6 +634,7 @@ template <int NMAX> __device__ __forceinline__ void cs_init(VC* vc, int n, const
     v.pointCount = ct.pointCount;
     const LWall& wl = W[ct.wall];
     v.cB = V(wl.px, wl.py); v.aB = wl.ang; v.vB = zero2(); v.wB = 0.0f;
+    v.qB.s = wl.qs; v.qB.c = wl.qc; v.aB0 = __float_as_uint(wl.ang);
     v.ln = V(ct.lnx, ct.lny); v.lp = V(ct.lpx, ct.lpy); v.pcount = ct.pointCount; v.type = ct.mtype;
     v.K[0] = v.K[1] = v.K[2] = v.K[3] = 0.0f; v.nm[0] = v.nm[1] = v.nm[2] = v.nm[3] = 0.0f;
     for (int j = 0; j < 2; ++j) {
@@ -652,7 +661,7 @@ template <int NMAX> __device__ __forceinline__ void cs_init_velocity(VC* vc, int
     V2 cA = A.c; float aA = A.a; V2 vA = A.v; float wA = A.w;
     V2 cB = v.cB; float aB = v.aB; V2 vB = v.vB; float wB = v.wB;
     Xf xfA, xfB;
-    xfA.q = rot_set(aA); xfB.q = rot_set(aB);
+    xfA.q = rot_set(aA); xfB.q = rot_static(aB, v.aB0, v.qB);
     xfA.p = vsub(cA, rmul(xfA.q, zero2()));
     xfB.p = vsub(cB, rmul(xfB.q, zero2()));
     V2 normal = zero2(), pts[2];
@@ -812,7 +821,7 @@ template <int NMAX> __device__ __forceinline__ int cs_solve_position(VC* vc, int
     for (int j = 0; j < 2; ++j) {
       if (j >= v.pcount) break;
       Xf xfA, xfB;
-      xfA.q = rot_set(aA); xfB.q = rot_set(aB);
+      xfA.q = rot_set(aA); xfB.q = rot_static(aB, v.aB0, v.qB);
       xfA.p = vsub(cA, rmul(xfA.q, zero2()));
       xfB.p = vsub(cB, rmul(xfB.q, zero2()));
       V2 normal, point; float sep;
@@ -1337,6 +1346,10 @@ __device__ inline void solve_toi(Car& c, const WallSet& S, float dt, float frict
       total += popc64(b) << bit;
     }
     if (m) { L.sw0[lane] = make_float4(c.c0.x, c.c0.y, c.c.x, c.c.y); L.sw1[lane] = make_float4(c.a0, c.a, c.alpha0, 0.0f); }
+    CCOUNT(c, 14, 1);   // profile builds: scans of this wave
+#ifdef NASCAR_PROFILE
+    const unsigned long long tj0 = __builtin_amdgcn_s_memtime();
+#endif
     for (int r0 = 0; r0 < total; r0 += TOI_JOBCAP) {   // wave-uniform
       {
         uint32_t nb = need; int k = off;
@@ -1365,6 +1378,10 @@ __device__ inline void solve_toi(Car& c, const WallSet& S, float dt, float frict
       }
       wave_lds_sync();   // the next round's pairs overwrite job / res
     }
+#ifdef NASCAR_PROFILE
+    CCOUNT(c, 13, __builtin_amdgcn_s_memtime() - tj0);   // the wave's TOI job rounds of this scan
+    const unsigned long long te0 = __builtin_amdgcn_s_memtime();
+#endif
     // (3) this lane's scan on cached alphas and its event, as Box2D
     if (active) {
       int minC = -1; float minAlpha = 1.0f;
@@ -1430,6 +1447,9 @@ __device__ inline void solve_toi(Car& c, const WallSet& S, float dt, float frict
         }
       }
     }
+#ifdef NASCAR_PROFILE
+    CCOUNT(c, 15, __builtin_amdgcn_s_memtime() - te0);   // the wave's event processing of this scan
+#endif
     if (!__any(active)) break;   // wave-uniform exit
   }
 }

@@ -2382,6 +2382,10 @@ struct NascarHandle {
   hipEvent_t ev_fork = nullptr;
   std::vector<hipEvent_t> ev_join;
   float* d_ro_act = nullptr;        // [N][2] actions of a policy-2 (SAC actor) sharded rollout
+  // prepare(): capacities of the track table / block map buffers, pinned staging of their stream-ordered uploads
+  size_t cap_tracks = 0, cap_blocks = 0;
+  void* h_stage = nullptr; size_t stage_bytes = 0;
+  hipEvent_t ev_stage = nullptr;
 };
 
 static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
@@ -2442,6 +2446,8 @@ extern "C" void nascar_destroy(NascarHandle* h) {
     hipFree(t.beam.d_cell); hipFree(t.beam.d_start); hipFree(t.beam.d_ent); hipFree(t.beam.d_head);
   }
   hipFree(h->d_tracks); hipFree(h->d_blk_track); hipFree(h->d_blk_env);
+  if (h->ev_stage) { hipEventSynchronize(h->ev_stage); hipEventDestroy(h->ev_stage); }
+  if (h->h_stage) hipHostFree(h->h_stage);
   for (auto st : h->sub_stream) hipStreamDestroy(st);
   for (auto ev : h->ev_join) hipEventDestroy(ev);
   if (h->ev_fork) hipEventDestroy(h->ev_fork);
@@ -2584,7 +2590,13 @@ static int apply_pending_tracks(NascarHandle* h, const uint8_t* env_mask, void* 
   return 0;
 }
 
-static int prepare(NascarHandle* h) {
+// Device copies of the track table and the block map, rebuilt when the env -> track assignment changed.
+// Stream-ordered: the tables are uploaded with hipMemcpyAsync on the caller's stream, so the copies land after
+// every earlier launch on that stream (the sharded rollout joins its shard streams into it before returning)
+// and before every later one.  Buffers keep their capacity; only growth (the first call, a newly loaded track)
+// reallocates, and then the old buffers are released after an explicit device synchronisation.  The host
+// source is pinned staging memory owned by the handle, reused only after its previous upload has completed.
+static int prepare(NascarHandle* h, hipStream_t stream) {
   if (h->tracks.empty()) return fail("no track loaded (nascar_add_track)");
   if (!h->dirty_tracks) return 0;
   std::vector<TrackDev> td;
@@ -2596,9 +2608,6 @@ static int prepare(NascarHandle* h) {
     d.beam = t.beam.g;
     td.push_back(d);
   }
-  hipFree(h->d_tracks);
-  HIPCHK(hipMalloc(&h->d_tracks, sizeof(TrackDev) * td.size()));
-  HIPCHK(hipMemcpy(h->d_tracks, td.data(), sizeof(TrackDev) * td.size(), hipMemcpyHostToDevice));
   // workgroups hold whole envs of one track: group envs by track, pad each group to a block
   std::vector<int> blk_track, blk_env;
   for (int tr = 0; tr < (int)h->tracks.size(); ++tr) {
@@ -2609,18 +2618,48 @@ static int prepare(NascarHandle* h) {
       for (int k = 0; k < h->epb; ++k) blk_env.push_back(i + k < envs.size() ? envs[i + k] : -1);
     }
   }
-  h->nblocks = (int)blk_track.size();
+  const size_t nt = td.size(), nb = blk_track.size();
+  if (nt > h->cap_tracks || nb > h->cap_blocks) {   // growth: earlier launches may still read the old buffers
+    HIPCHK(hipDeviceSynchronize());
+    if (nt > h->cap_tracks) {
+      hipFree(h->d_tracks); h->d_tracks = nullptr;
+      const size_t cap = std::max(nt, (size_t)8);
+      HIPCHK(hipMalloc(&h->d_tracks, sizeof(TrackDev) * cap));
+      h->cap_tracks = cap;
+    }
+    if (nb > h->cap_blocks) {
+      hipFree(h->d_blk_track); hipFree(h->d_blk_env); h->d_blk_track = h->d_blk_env = nullptr;
+      const size_t cap = std::max(nb, (size_t)(h->E + h->epb - 1) / h->epb + 8);
+      HIPCHK(hipMalloc(&h->d_blk_track, sizeof(int) * cap));
+      HIPCHK(hipMalloc(&h->d_blk_env, sizeof(int) * cap * h->epb));
+      h->cap_blocks = cap;
+    }
+  }
+  const size_t b_tr = sizeof(TrackDev) * nt, b_bt = sizeof(int) * nb, b_be = sizeof(int) * blk_env.size();
+  const size_t need = b_tr + b_bt + b_be;
+  if (h->ev_stage) HIPCHK(hipEventSynchronize(h->ev_stage));   // the previous upload out of the staging buffer
+  if (need > h->stage_bytes) {
+    if (h->h_stage) hipHostFree(h->h_stage);
+    h->h_stage = nullptr; h->stage_bytes = 0;
+    HIPCHK(hipHostMalloc(&h->h_stage, need));
+    h->stage_bytes = need;
+  }
+  char* st = (char*)h->h_stage;
+  memcpy(st, td.data(), b_tr);
+  memcpy(st + b_tr, blk_track.data(), b_bt);
+  memcpy(st + b_tr + b_bt, blk_env.data(), b_be);
+  HIPCHK(hipMemcpyAsync(h->d_tracks, st, b_tr, hipMemcpyHostToDevice, stream));
+  HIPCHK(hipMemcpyAsync(h->d_blk_track, st + b_tr, b_bt, hipMemcpyHostToDevice, stream));
+  HIPCHK(hipMemcpyAsync(h->d_blk_env, st + b_tr + b_bt, b_be, hipMemcpyHostToDevice, stream));
+  if (!h->ev_stage) HIPCHK(hipEventCreateWithFlags(&h->ev_stage, hipEventDisableTiming));
+  HIPCHK(hipEventRecord(h->ev_stage, stream));
+  h->nblocks = (int)nb;
   h->map_identity = 1;
   for (size_t s = 0; s < blk_env.size(); ++s)
     if (blk_env[s] != ((int)s < h->E ? (int)s : -1)) { h->map_identity = 0; break; }
   h->one_track = blk_track.empty() ? -1 : blk_track[0];
   for (int tr : blk_track) if (tr != h->one_track) { h->one_track = -1; break; }
   if (getenv("NASCAR_NO_MAP_SHORTCUT")) { h->map_identity = 0; h->one_track = -1; }   // A/B and tests
-  hipFree(h->d_blk_track); hipFree(h->d_blk_env);
-  HIPCHK(hipMalloc(&h->d_blk_track, sizeof(int) * blk_track.size()));
-  HIPCHK(hipMalloc(&h->d_blk_env, sizeof(int) * blk_env.size()));
-  HIPCHK(hipMemcpy(h->d_blk_track, blk_track.data(), sizeof(int) * blk_track.size(), hipMemcpyHostToDevice));
-  HIPCHK(hipMemcpy(h->d_blk_env, blk_env.data(), sizeof(int) * blk_env.size(), hipMemcpyHostToDevice));
   h->dirty_tracks = false;
   return 0;
 }
@@ -2676,7 +2715,7 @@ extern "C" int nascar_reset(NascarHandle* h, const uint8_t* env_mask, float* obs
   if (!h || !obs) return fail("null argument");
   h->pristine = false;
   if (apply_pending_tracks(h, env_mask, stream)) return -1;
-  if (prepare(h)) return -1;
+  if (prepare(h, (hipStream_t)stream)) return -1;
   Params P = make_params(h);
   hipLaunchKernelGGL(reset_kernel, dim3(h->nblocks), dim3(SBLOCK), 0, (hipStream_t)stream, P, env_mask, obs);
   HIPCHK(hipGetLastError());
@@ -2726,7 +2765,7 @@ static int step_impl(NascarHandle* h, const void* actions, int32_t discrete, int
                      float* obs, float* reward, uint8_t* car_flags, uint8_t* env_flags, int32_t auto_reset,
                      float* terminal_obs, void* stream) {
   h->pristine = false;
-  if (prepare(h)) return -1;
+  if (prepare(h, (hipStream_t)stream)) return -1;
   Params P = make_params(h);
   // Whole grid on the caller's stream: splitting one step over streams needs a fork and a join per step, and
   // the per-step barrier measured slower than one grid (tools/streams_exp.py: 2 / 4 shards 0.252 / 0.277 ms vs
@@ -2837,7 +2876,7 @@ extern "C" int nascar_rollout(NascarHandle* h, int32_t policy, uint64_t seed, in
   if (steps < 0) return fail("steps must be >= 0");
   if (steps == 0) return 0;
   h->pristine = false;
-  if (prepare(h)) return -1;
+  if (prepare(h, (hipStream_t)stream)) return -1;
   if (h->ro_streams > 0)
     return rollout_sharded(h, h->ro_streams, policy, seed, step0, steps, obs, reward, car_flags, env_flags, auto_reset,
                            traj, (hipStream_t)stream);
@@ -2859,7 +2898,7 @@ extern "C" int nascar_rollout(NascarHandle* h, int32_t policy, uint64_t seed, in
 
 extern "C" int nascar_get_info(NascarHandle* h, double* info, void* stream) {
   if (!h || !info) return fail("null argument");
-  if (prepare(h)) return -1;
+  if (prepare(h, (hipStream_t)stream)) return -1;
   Params P = make_params(h);
   hipLaunchKernelGGL(info_kernel, dim3(h->nblocks), dim3(SBLOCK), 0, (hipStream_t)stream, P, info);
   HIPCHK(hipGetLastError());
@@ -3056,7 +3095,7 @@ __global__ void debug_pose_kernel(Params P, const float* poses) {
 }
 extern "C" int nascar_debug_sensors(NascarHandle* h, const float* poses, float* obs, int32_t impl, void* stream) {
   if (!h || !poses || !obs) return fail("null argument");
-  if (prepare(h)) return -1;
+  if (prepare(h, (hipStream_t)stream)) return -1;
   Params P = make_params(h);
   hipLaunchKernelGGL(debug_pose_kernel, dim3((h->N + 255) / 256), dim3(256), 0, (hipStream_t)stream, P, poses);
   HIPCHK(hipGetLastError());

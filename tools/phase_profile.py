@@ -135,8 +135,12 @@ def main():
                     print("   ", i, *cp[i, [0, 1, 2, 3, 4, 5, 6, 7]].tolist(), f"| bp full scans {cp[i, 8]}, candidates {cp[i, 9]}"
                           f" | x {info[i, F.index('x')]:.1f} y {info[i, F.index('y')]:.1f} v ({info[i, F.index('vx')]:.1f}, "
                           f"{info[i, F.index('vy')]:.1f}) angle {info[i, F.index('angle')]:.2f} disabled {info[i, F.index('disabled')]:.0f} n_contacts {info[i, F.index('n_contacts')]:.0f}")
+            for i in np.argsort(-cyc)[:12]:
+                print(f"    car {i}: wave b2 {cp[i, 0]}, solve_toi scans {cp[i, 14]}, TOI job rounds {cp[i, 13]} cycles, "
+                      f"event processing {cp[i, 15]} cycles, events {cp[i, 4]}, island solve {cp[i, 11]}, "
+                      f"event contact updates {cp[i, 12]}")
             for i in np.argsort(-cyc)[:24]:
-                if cp[i, 10:14].any():
+                if cp[i, 10] or cp[i, 9]:
                     iso = f", isolated single-lane TOI {cp[i, 13] / cp[i, 9]:.0f} cycles/call" if cp[i, 9] else ""
                     print(f"    car {i} solve_toi cycles: TOI calls {cp[i, 10]} (GJK {cp[i, 14]}, separation fn {cp[i, 15]}), "
                           f"island solves {cp[i, 11]}, event contact updates {cp[i, 12]}{iso}")
