@@ -731,6 +731,22 @@ static void collision_data(const ocar *c, double *imp, double *ang) {
     }
 }
 
+/* DistanceSensor.get_sensor_distances (src/distance_sensor.py:71-117) of a car at p1 with body angle ang, as
+   _get_multi_obs stores them (src/car_env.py:946): 16 rays 22.5 deg apart, 250 m, b2World.RayCast closest hit */
+static void sensors16(const oenv *e, ov2 p1, double ang, float *out) {
+    const double px = p1.x, py = p1.y;
+    for (int i = 0; i < 16; ++i) {
+        double sa = -((double)i * (360.0 / 16) * RAD_PER_DEG) + ang;
+        double dx = cos(sa), dy = sin(sa);
+        ov2 p2 = OV(px + dx * 250.0, py + dy * 250.0);
+        float fr = ob_raycast(&e->trk.W, p1, p2);
+        double hd = fr >= 0.0f ? (double)fr * 250.0 : 250.0;
+        float d32 = (float)hd;
+        float v = d32 / 250.0f;
+        out[i] = v < 0.0f ? 0.0f : (v > 1.0f ? 1.0f : v);
+    }
+}
+
 /* CarEnv._get_multi_obs for one car (src/car_env.py:891-956) */
 static void car_obs(oenv *e, ocar *c, float *o) {
     const oworld *w = &c->w;
@@ -748,18 +764,7 @@ static void car_obs(oenv *e, ocar *c, float *o) {
     double imp, ca; collision_data(c, &imp, &ca);
     o[19] = (float)npclip(imp / 50000.0, 0, 1); o[20] = (float)npclip(ca / PI_, -1, 1);
     o[21] = (float)npclip(c->cum_impact / 250000.0, 0, 1);
-    /* DistanceSensor.get_sensor_distances (src/distance_sensor.py:71-117) */
-    ov2 p1 = w->xf.p;
-    for (int i = 0; i < 16; ++i) {
-        double sa = -((double)i * (360.0 / 16) * RAD_PER_DEG) + ang;
-        double dx = cos(sa), dy = sin(sa);
-        ov2 p2 = OV(px + dx * 250.0, py + dy * 250.0);
-        float fr = ob_raycast(&e->trk.W, p1, p2);
-        double hd = fr >= 0.0f ? (double)fr * 250.0 : 250.0;
-        float d32 = (float)hd;
-        float v = d32 / 250.0f;
-        o[22 + i] = v < 0.0f ? 0.0f : (v > 1.0f ? 1.0f : v);
-    }
+    sensors16(e, w->xf.p, ang, o + 22);
 }
 
 static int all_active_completed(oenv *e, int env) {
@@ -1000,6 +1005,12 @@ EXPORT void or_car_info(void *h, int idx, double *o) {
 /* unit hooks */
 EXPORT float or_sinf(float x) { return ob_sinf(x); }
 EXPORT float or_cosf(float x) { return ob_cosf(x); }
+/* the 16 sensor values of n arbitrary poses [n][3] (x, y, angle) float32 -> out [n][16] (sensor parity tests) */
+EXPORT void or_sensors(void *h, const float *poses, int n, float *out) {
+    const oenv *e = h;
+    for (int k = 0; k < n; ++k)
+        sensors16(e, OV(poses[3 * k], poses[3 * k + 1]), (double)poses[3 * k + 2], out + 16 * (size_t)k);
+}
 EXPORT float or_raycast(void *h, float x1, float y1, float x2, float y2) {
     ov2 a = { x1, y1 }, b = { x2, y2 };
     return ob_raycast(&((oenv *)h)->trk.W, a, b);
