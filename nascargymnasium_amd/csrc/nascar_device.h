@@ -1154,13 +1154,15 @@ __device__ inline float sep_eval(const SepFn& f, const Poly* pA, const Poly* pB,
   }
 }
 enum { TOI_UNKNOWN, TOI_FAILED, TOI_OVERLAPPED, TOI_TOUCHING, TOI_SEPARATED };
+// qB0 / aB0: the static body B's rotation and the angle bits it was set from (its body transform): b2Rot::Set of
+// B's normalized sweep angle is that rotation whenever the normalization left the angle unchanged
 __device__ inline float time_of_impact(int* state, const Poly* pA, const Sweep& sweepA, const Poly* pB, const Sweep& sweepB, float tMax,
-                                      int* prof_iters = nullptr, unsigned long long* prof_cyc = nullptr) {
+                                      Rot qB0, uint32_t aB0, int* prof_iters = nullptr, unsigned long long* prof_cyc = nullptr) {
   *state = TOI_UNKNOWN;
   float out_t = tMax;
   Sweep sA = sweepA, sB = sweepB;
   sweep_normalize(sA); sweep_normalize(sB);
-  const Rot qB = rot_set(sB.a0);
+  const Rot qB = rot_static(sB.a0, aB0, qB0);
   float totalRadius = pA->radius + pB->radius;
   float target = fmaxb(LINEAR_SLOP, totalRadius - 3.0f * LINEAR_SLOP);
   float tolerance = 0.25f * LINEAR_SLOP;
@@ -1307,7 +1309,8 @@ __device__ __forceinline__ float toi_alpha(float4 s0, float4 s1, const LWall& wl
   Sweep sA; sA.c0 = V(s0.x, s0.y); sA.c = V(s0.z, s0.w); sA.a0 = s1.x; sA.a = s1.y; sA.alpha0 = s1.z;
   Sweep sB; sB.c0 = V(wl.px, wl.py); sB.c = sB.c0; sB.a0 = wl.ang; sB.a = wl.ang; sB.alpha0 = 0.0f;
   int state;
-  const float beta = time_of_impact(&state, &pa, sA, &pb, sB, 1.0f);
+  Rot qw; qw.s = wl.qs; qw.c = wl.qc;
+  const float beta = time_of_impact(&state, &pa, sA, &pb, sB, 1.0f, qw, __float_as_uint(wl.ang));
   return state == TOI_TOUCHING ? fminb(s1.z + (1.0f - s1.z) * beta, 1.0f) : 1.0f;
 }
 __device__ inline void solve_toi(Car& c, const WallSet& S, float dt, float friction) {
