@@ -214,16 +214,16 @@ __device__ __forceinline__ bool contains(Aabb a, Aabb b) {
   return r;
 }
 
-// wall table in LDS (built on the host from the reference wall builder)
+// wall table (built on the host from the reference wall builder): 32 bytes per wall, so model_kernel can stage a
+// whole track's table in LDS next to its TOI work lists at its occupancy; the broadphase fat AABBs are a separate
+// float4 array (WallSet::fat: read by the contact-list culls only)
 struct LWall {
   float px, py, qs, qc;   // b2Body transform
-  float hx, hy, ang, rad; // half extents, angle, bounding radius (+ culling margin)
-  float flx, fly, fhx, fhy;  // broadphase fat AABB
+  float hx, hy, ang;      // half extents, angle
   int key;                // listener key id (src/car_physics.py:747)
-  int pad0, pad1, pad2;
 };
 __device__ __forceinline__ Xf wall_xf(const LWall& w) { Xf t; t.p = V(w.px, w.py); t.q.s = w.qs; t.q.c = w.qc; return t; }
-__device__ __forceinline__ Aabb wall_fat(const LWall& w) { Aabb a; a.lo = V(w.flx, w.fly); a.hi = V(w.fhx, w.fhy); return a; }
+__device__ __forceinline__ Aabb fat_box(float4 f) { Aabb a; a.lo = V(f.x, f.y); a.hi = V(f.z, f.w); return a; }
 
 // Uniform grid of wall lists over a track (built on the host, nascar_add_track).
 // Cell (ix, iy) covers [ox + ix*cell, ox + (ix+1)*cell) x [...]; its list holds every
@@ -246,6 +246,7 @@ struct WallGrid {
 struct WallSet {
   const LWall* W; int nw;
   WallGrid bp, sn;
+  const float4* fat;      // [nw] broadphase fat AABB (lo.x, lo.y, hi.x, hi.y)
 };
 // list of the cell containing (x, y), or false when outside the grid
 __device__ __forceinline__ bool grid_list(const WallGrid& g, float x, float y, int& beg, int& end) {
@@ -386,8 +387,7 @@ __device__ inline void find_new_contacts(Car& c, const WallSet& S) {
 #endif
   for (int k = beg; k < end; ++k) {
     const int j = list ? (int)list[k] : k;
-    const LWall& wl = W[j];
-    if (!overlap(c.fat, wall_fat(wl))) continue;
+    if (!overlap(c.fat, fat_box(S.fat[j]))) continue;
     bool exists = false;
     for (int i = 0; i < c.nct; ++i) if (c.ct[i].wall == j) { exists = true; break; }
     if (exists) continue;
@@ -585,12 +585,13 @@ __device__ __forceinline__ int rank_in(unsigned long long m) {
   return popc64(m & below);
 }
 
-__device__ inline void collide(Car& c, const LWall* W) {
+__device__ inline void collide(Car& c, const WallSet& S) {
+  const LWall* W = S.W;
   int i = 0;
   while (i < c.nct) {
     if (!c.awake) { ++i; continue; }
     const int wall = c.ct[i].wall;
-    if (!overlap(c.fat, wall_fat(W[wall]))) {
+    if (!overlap(c.fat, fat_box(S.fat[wall]))) {
       bool touching = (c.ct[i].flags & CT_TOUCH) != 0;
       remove_contact(c, i);
       if (touching) lis_end(c, W[wall].key);
@@ -1465,7 +1466,7 @@ __device__ inline void b2_step(Car& c, const WallSet& S, float dt, float frictio
   const unsigned long long t0 = __builtin_amdgcn_s_memtime();
   CCOUNT(c, 1, c.nct);
 #endif
-  collide(c, W);
+  collide(c, S);
   PROFB(11);
   solve(c, S, dt, dtRatio, friction);
   PROFB(13);

@@ -19,6 +19,8 @@
 #include <thread>
 #include <cmath>
 #include <string>
+#include <memory>
+#include <mutex>
 #include <unordered_map>
 #include <vector>
 
@@ -63,16 +65,14 @@ __host__ __device__ __forceinline__ int beam_bin(int slot) { return (slot % 16) 
 struct BeamGrid {
   float ox, oy, inv_cell; int nx, ny;
   const int* cell;          // [nx * ny]: first list of the cell (built cell id * BEAM_NB), -1: not built
-  const uint32_t* start;    // [built cells * BEAM_NB + 1]
-  const uint32_t* ent;
+  const uint32_t* ent;      // list continuations, each closed by a BEAM_PAD sentinel
   // [built cells * BEAM_NB][BEAM_HW] head records: the first BEAM_HEAD entries of each list (padded with
-  // BEAM_PAD) and a tail word -- the ent[] index of the list's next entry (bits 0-27) and how many follow
-  // (bits 28-31, 15 = "15 or more": read start[] for the end) -- so a walk starts with BEAM_HW independent
-  // 16-byte loads and reads the rest of a long list in chunks of 4 entries without a start[] lookup
+  // BEAM_PAD) and a tail word -- the ent[] index of the rest of a longer list (0: none) -- so a walk starts with
+  // BEAM_HW independent 16-byte loads and reads the rest in chunks of RAY_CHUNK entries up to the sentinel
   const uint4* head;
 };
 #ifndef BEAM_HW
-#define BEAM_HW 2
+#define BEAM_HW 1   // 16-byte heads (3 entries + tail): at 1 m cells the median ray walks 2 entries (2-word heads measured slower)
 #endif
 #define BEAM_HEAD (4 * BEAM_HW - 1)
 #ifndef RAY_CHUNK
@@ -86,8 +86,10 @@ __device__ __forceinline__ BeamHead beam_head(const BeamGrid& G, int li) {
   for (int k = 0; k < BEAM_HW; ++k) h.w[k] = G.head[(size_t)li * BEAM_HW + k];
   return h;
 }
+#define MODEL_WALL_LDS_MAX ((size_t)1024 * sizeof(LWall))   // walls per track model_kernel's LDS table holds
 struct TrackDev {
   LWall* walls; int nwall;
+  const float4* wfat;  // [nwall] broadphase fat AABBs
   DSeg* segs; int nseg;
   double* prefix;      // cumulative chord length before segment k (src/car_env.py:1593-1600)
   double total_length; int startline; int has_banking;
@@ -785,8 +787,9 @@ __device__ inline bool query_on_wall(const WallSet& S, double px, double py, dou
     list = S.bp.idx;
   else { beg = 0; end = S.nw; }
   for (int kk = beg; kk < end; ++kk) {
-    const LWall& wl = W[list ? (int)list[kk] : kk];
-    if (!overlap(wall_fat(wl), q)) continue;
+    const int jw = list ? (int)list[kk] : kk;
+    const LWall& wl = W[jw];
+    if (!overlap(fat_box(S.fat[jw]), q)) continue;
     Xf xf = wall_xf(wl);
     Poly p; make_box(&p, wl.hx, wl.hy);
     V2 pl = rmulT(xf.q, vsub(center, xf.p));
@@ -1268,12 +1271,10 @@ __device__ __forceinline__ float ray_walk(const BeamGrid& G, const float4* __res
   }
   const uint32_t tail = hv[BEAM_HEAD];
   if (more && tail != 0u) {
-    const uint32_t s0 = tail & 0x0FFFFFFFu, c = tail >> 28;
-    const uint32_t e0 = c < 15u ? s0 + c : G.start[li + 1];
-    for (uint32_t k = s0; k < e0; k += RAY_CHUNK) {   // RAY_CHUNK entries requested together, walked in order
+    for (uint32_t k = tail;; k += RAY_CHUNK) {   // RAY_CHUNK entries requested together, walked in order to the sentinel
       uint32_t v4[RAY_CHUNK];
 #pragma unroll
-      for (int q = 0; q < RAY_CHUNK; ++q) v4[q] = k + q < e0 ? G.ent[k + q] : BEAM_PAD;
+      for (int q = 0; q < RAY_CHUNK; ++q) v4[q] = G.ent[k + q];
       bool stop = false;
 #pragma unroll
       for (int q = 0; q < RAY_CHUNK; ++q) {
@@ -1519,7 +1520,7 @@ __global__ void policy_kernel(int N, int policy, uint64_t seed, int64_t step, co
 // src/car_physics.py:341-384): BaseEnv._convert_to_internal_action of (tb, st), Car.update_physics, the
 // Box2D step; writes the model / body state back and the sensor pass-A pose.
 __device__ __forceinline__ void model_car(const Params& P, Car& c, int n, const TrackDev& T, float tb, float st, int want_term) {
-  const WallSet S{T.walls, T.nwall, T.bp, T.sn};
+  const WallSet S{T.walls, T.nwall, T.bp, T.sn, T.wfat};
   float a0, a1, a2 = st;
   if (tb >= 0) { a0 = tb; a1 = 0.0f; } else { a0 = 0.0f; a1 = -tb; }
   if (c.disabled) { a0 = 0.0f; a1 = 0.0f; a2 = 0.0f; }
@@ -1539,6 +1540,9 @@ __device__ __forceinline__ void model_car(const Params& P, Car& c, int n, const 
 // The env step as two launches: model_kernel (actions -> Car.update_physics -> Box2D step, one lane
 // per car; its TOI code holds it at one wave per SIMD) hands the body / listener state to logic_kernel
 // (banking, disable logic, lap timer, rewards, termination, obs, auto-reset) through the state arrays.
+#ifndef MODEL_WALLS_LDS
+#define MODEL_WALLS_LDS 1   // model_kernel stages the track's 32-byte wall records in LDS (dynamic shared memory)
+#endif
 #ifndef MODEL_WPE
 #define MODEL_WPE 2   // 256 VGPRs + 40 spilled (vs 256 + 44 AGPRs at 1 wave/SIMD): 103.6 -> 100.6 us/step
 #endif
@@ -1574,8 +1578,17 @@ __global__ void __launch_bounds__(SBLOCK) __attribute__((amdgpu_waves_per_eu(MOD
   }
   TrackDev T = P.tracks[blk_track_of(P, (blockIdx.x + P.blk0))];
   if (tid < T.nseg) s_segs[tid] = T.segs[tid];
+#if MODEL_WALLS_LDS
+  // the track's wall table in LDS: every contact update, TOI pair, island and listener lookup of the Box2D step
+  // reads it (one staging per workgroup instead of a dependent L2 round trip per access)
+  LWall* s_w = (LWall*)smem;
+  for (int k = tid; k < T.nwall; k += SBLOCK) s_w[k] = T.walls[k];
+#endif
   __syncthreads();
   T.segs = s_segs;
+#if MODEL_WALLS_LDS
+  T.walls = s_w;
+#endif
   PROF(1);
   if (env < 0) return;
   PROF(2);
@@ -1629,7 +1642,7 @@ __device__ __forceinline__ void logic_run(const Params& P, const TrackDev& T, co
   const ChordScreen CS{TL.sg, TL.rll, T.nseg};
   float cut = INFINITY;
   const int nw = T.nwall;
-  const WallSet S{T.walls, nw, T.bp, T.sn};
+  const WallSet S{T.walls, nw, T.bp, T.sn, T.wfat};
   bool lapdone = false;
   if (env >= 0) {
     L.dis_old[tid] = c.disabled;
@@ -2009,7 +2022,7 @@ __global__ void __launch_bounds__(SBLOCK) reset_kernel(Params P, const uint8_t* 
   int env = blk_env_of(P, el, slot);
   if (env >= 0 && mask && !mask[env]) { P.pose[env * C + car] = make_float4(0.f, 0.f, 0.f, __int_as_float(0)); env = -1; }
   const TrackDev T = P.tracks[blk_track_of(P, blockIdx.x)];
-  const WallSet S{T.walls, T.nwall, T.bp, T.sn};
+  const WallSet S{T.walls, T.nwall, T.bp, T.sn, T.wfat};
   if (env >= 0) {
     const int n = env * C + car;
     const bool fresh = P.env_i32[E_CREATED * P.E + env] == 0;
@@ -2036,7 +2049,7 @@ __global__ void __launch_bounds__(SBLOCK) info_kernel(Params P, double* info) {
   const int slot = blockIdx.x * P.epb + el;
   const int env = blk_env_of(P, el, slot);
   const TrackDev T = P.tracks[blk_track_of(P, blockIdx.x)];
-  const WallSet S{T.walls, T.nwall, T.bp, T.sn};
+  const WallSet S{T.walls, T.nwall, T.bp, T.sn, T.wfat};
   if (env < 0) return;
   const int n = env * C + car;
   Car c;
@@ -2100,15 +2113,21 @@ struct HostGrid {
   int* d_start = nullptr; uint16_t* d_idx = nullptr;
   std::vector<float4> box; float4* d_box = nullptr;
 };
+// host-side wall record: the device's LWall plus the values only the host builders use
+struct HWall : LWall {
+  float rad;                 // bounding radius + culling margin (sensor wall image)
+  float flx, fly, fhx, fhy;  // broadphase fat AABB
+};
 struct HostTrack {
-  std::vector<LWall> walls; std::vector<DSeg> segs; std::vector<double> prefix;
+  std::vector<HWall> walls; std::vector<DSeg> segs; std::vector<double> prefix;
   double total_length; int startline, has_banking;
-  LWall* d_walls = nullptr; DSeg* d_segs = nullptr; double* d_prefix = nullptr;
+  LWall* d_walls = nullptr; float4* d_wfat = nullptr; DSeg* d_segs = nullptr; double* d_prefix = nullptr;
   HostGrid bp, sn;
   struct {
     BeamGrid g{};
-    std::vector<int> cell; std::vector<uint32_t> start, ent; std::vector<uint4> head;
-    int* d_cell = nullptr; uint32_t* d_start = nullptr; uint32_t* d_ent = nullptr; uint4* d_head = nullptr;
+    std::vector<int> cell; std::vector<uint32_t> ent; std::vector<uint4> head;
+    int* d_cell = nullptr; uint32_t* d_ent = nullptr; uint4* d_head = nullptr;
+    size_t entries = 0, nlist = 0;
     double build_s = 0.0;
   } beam;
   std::vector<float4> groups; float4* d_groups = nullptr;
@@ -2139,7 +2158,7 @@ static void build_grids(HostTrack& t) {
       const double y0 = t.bp.g.oy + (double)cy * BP_CELL - BP_REACH - 0.05, y1 = t.bp.g.oy + (double)(cy + 1) * BP_CELL + BP_REACH + 0.05;
       t.bp.start[(size_t)cy * t.bp.g.nx + cx] = (int)t.bp.idx.size();
       for (int j = 0; j < nw; ++j) {
-        const LWall& w = t.walls[j];
+        const HWall& w = t.walls[j];
         if (w.flx > x1 || w.fhx < x0 || w.fly > y1 || w.fhy < y0) continue;
         t.bp.idx.push_back((uint16_t)j);
         t.bp.box.push_back(make_float4(w.flx, w.fly, w.fhx, w.fhy));
@@ -2215,8 +2234,11 @@ static void build_grids(HostTrack& t) {
 //    B, widened by asin((rr + rc) / dist(c, AB)) (all bins when c is inside the grown capsule), plus a
 //    2e-3 rad guard for the f32 ray end points; every bin that arc touches lists the wall.
 // Both are conservative, so the walk in ray_sensor_kernel visits every wall that can be the first hit.
+// Cell size: the cell's disk widens every wall's angular arc and lowers its distance bound, so smaller cells give
+// shorter walks (steady-state sensor tails; bench step 191 -> 178 / 174 / 168 / 167 us at 2 / 1.5 / 1 / 0.75 m,
+// tools/ab2.sh) at ~0.8 GB of lists per track at 1 m (16-byte heads + sentinel-terminated continuations).
 #ifndef BEAM_CELL_M
-#define BEAM_CELL_M 4.0f
+#define BEAM_CELL_M 1.0f
 #endif
 static const float BEAM_CELL = BEAM_CELL_M;
 static const double BEAM_BAND = 8.0;
@@ -2298,40 +2320,43 @@ static void build_beams(HostTrack& t) {
   std::vector<std::thread> th;
   for (int k = 0; k < nth; ++k) th.emplace_back(work, (int)((long)ncell * k / nth), (int)((long)ncell * (k + 1) / nth));
   for (auto& x : th) x.join();
-  B.start.assign((size_t)ncell * BEAM_NB + 1, 0);
-  B.ent.clear();
-  // lists stored per cell in slot order (beam_slot)
+  // per list (cell-major, slot order, beam_slot): the head record holds its first BEAM_HEAD entries (BEAM_PAD
+  // filled) and, when the list is longer, in its last word the ent[] index of the continuation -- the remaining
+  // entries followed by one BEAM_PAD sentinel (bound 655.35 m stops every walk), so a walk needs no list end.
+  // ent[0] is a sentinel (tail word 0 = no continuation); RAY_CHUNK sentinels close the array (chunk over-read).
+  const size_t nlist = (size_t)ncell * BEAM_NB;
+  B.head.assign(nlist * BEAM_HW, make_uint4(BEAM_PAD, BEAM_PAD, BEAM_PAD, BEAM_PAD));
+  B.ent.assign(1, BEAM_PAD);
+  B.entries = 0;
   for (int ci = 0; ci < ncell; ++ci)
     for (int slot = 0; slot < BEAM_NB; ++slot) {
-      const int bin = beam_bin(slot);
-      const auto& L = lists[(size_t)ci * BEAM_NB + bin];
-      B.start[(size_t)ci * BEAM_NB + slot] = (uint32_t)B.ent.size();
-      B.ent.insert(B.ent.end(), L.begin(), L.end());
+      const auto& L = lists[(size_t)ci * BEAM_NB + beam_bin(slot)];
+      const size_t s = (size_t)ci * BEAM_NB + slot;
+      B.entries += L.size();
+      uint32_t h[4 * BEAM_HW];
+      for (int k = 0; k < BEAM_HEAD; ++k) h[k] = (size_t)k < L.size() ? L[k] : BEAM_PAD;
+      h[BEAM_HEAD] = 0u;
+      if (L.size() > (size_t)BEAM_HEAD) {
+        h[BEAM_HEAD] = (uint32_t)B.ent.size();
+        B.ent.insert(B.ent.end(), L.begin() + BEAM_HEAD, L.end());
+        B.ent.push_back(BEAM_PAD);
+      }
+      for (int k = 0; k < BEAM_HW; ++k) B.head[s * BEAM_HW + k] = make_uint4(h[4 * k], h[4 * k + 1], h[4 * k + 2], h[4 * k + 3]);
     }
-  B.start.back() = (uint32_t)B.ent.size();
-  B.head.assign((size_t)ncell * BEAM_NB * BEAM_HW, make_uint4(BEAM_PAD, BEAM_PAD, BEAM_PAD, BEAM_PAD));
-  for (size_t s = 0; s + 1 < B.start.size(); ++s) {
-    uint32_t h[4 * BEAM_HW];
-    const uint32_t n = B.start[s + 1] - B.start[s];
-    for (int k = 0; k < BEAM_HEAD; ++k) h[k] = (uint32_t)k < n ? B.ent[B.start[s] + k] : BEAM_PAD;
-    const uint32_t rest = n > (uint32_t)BEAM_HEAD ? n - BEAM_HEAD : 0u;
-    h[BEAM_HEAD] = rest ? ((B.start[s] + BEAM_HEAD) | (std::min<uint32_t>(rest, 15u) << 28)) : 0u;
-    for (int k = 0; k < BEAM_HW; ++k) B.head[s * BEAM_HW + k] = make_uint4(h[4 * k], h[4 * k + 1], h[4 * k + 2], h[4 * k + 3]);
-  }
+  for (int k = 0; k < RAY_CHUNK; ++k) B.ent.push_back(BEAM_PAD);
+  B.nlist = nlist;
   B.build_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
 }
 static int upload_beams(HostTrack& t) {
   auto& B = t.beam;
-  if (B.ent.size() >= (1u << 28)) return fail("beam lists hold %zu entries (head tail offsets are 28-bit)", B.ent.size());
+  if (B.ent.size() >= 0xFFFFFFF0u) return fail("beam list continuations hold %zu entries (32-bit offsets)", B.ent.size());
   HIPCHK(hipMalloc(&B.d_cell, sizeof(int) * B.cell.size()));
   HIPCHK(hipMemcpy(B.d_cell, B.cell.data(), sizeof(int) * B.cell.size(), hipMemcpyHostToDevice));
-  HIPCHK(hipMalloc(&B.d_start, sizeof(uint32_t) * B.start.size()));
-  HIPCHK(hipMemcpy(B.d_start, B.start.data(), sizeof(uint32_t) * B.start.size(), hipMemcpyHostToDevice));
   HIPCHK(hipMalloc(&B.d_ent, sizeof(uint32_t) * std::max<size_t>(B.ent.size(), 1)));
   if (!B.ent.empty()) HIPCHK(hipMemcpy(B.d_ent, B.ent.data(), sizeof(uint32_t) * B.ent.size(), hipMemcpyHostToDevice));
   HIPCHK(hipMalloc(&B.d_head, sizeof(uint4) * std::max<size_t>(B.head.size(), 1)));
   if (!B.head.empty()) HIPCHK(hipMemcpy(B.d_head, B.head.data(), sizeof(uint4) * B.head.size(), hipMemcpyHostToDevice));
-  B.g.cell = B.d_cell; B.g.start = B.d_start; B.g.ent = B.d_ent; B.g.head = B.d_head;
+  B.g.cell = B.d_cell; B.g.ent = B.d_ent; B.g.head = B.d_head;
   return 0;
 }
 
@@ -2349,12 +2374,35 @@ static int upload_grid(HostGrid& G) {
   return 0;
 }
 
+// A built track: the device tables of one .track (walls, segments, grids, beam lists, sensor image), read-only
+// once built.  Handles share them through a process-wide cache keyed by the track's input arrays and the device:
+// every env of a batch, every VecEnv sub-engine and every later handle on the same track uses one copy (the beam
+// lists are ~0.8 GB per track at 1 m cells and take ~2 s of host time to build).  The last handle to drop a
+// build frees its device memory.
+struct TrackBuild {
+  int device = 0;
+  HostTrack t;
+  size_t lds = 0;   // model_kernel's LDS wall table
+  ~TrackBuild() {
+    int cur = 0;
+    hipGetDevice(&cur);
+    if (cur != device) hipSetDevice(device);
+    hipFree(t.d_walls); hipFree(t.d_wfat); hipFree(t.d_segs); hipFree(t.d_prefix);
+    hipFree(t.bp.d_start); hipFree(t.bp.d_idx); hipFree(t.bp.d_box); hipFree(t.sn.d_start); hipFree(t.sn.d_idx);
+    hipFree(t.d_groups); hipFree(t.d_swall);
+    hipFree(t.beam.d_cell); hipFree(t.beam.d_ent); hipFree(t.beam.d_head);
+    if (cur != device) hipSetDevice(cur);
+  }
+};
+static std::mutex g_track_mu;
+static std::unordered_map<std::string, std::weak_ptr<TrackBuild>> g_track_cache;
+
 struct NascarHandle {
   NascarConfig cfg;
   int N, E, C, epb;
   void* arena = nullptr; size_t arena_bytes = 0;
   size_t off_f32, off_f64, off_i32, off_acc, off_ct, off_key, off_n, off_time, off_ei32, off_ctl;
-  std::vector<HostTrack> tracks;
+  std::vector<std::shared_ptr<TrackBuild>> tracks;   // shared, read-only track tables (track_cache)
   TrackDev* d_tracks = nullptr;
   int* d_blk_track = nullptr; int* d_blk_env = nullptr; int nblocks = 0;
   int map_identity = 0, one_track = -1;   // Params shortcuts of the block map (prepare)
@@ -2440,10 +2488,9 @@ extern "C" void nascar_destroy(NascarHandle* h) {
   if (!h) return;
   hipFree(h->d_vhist);
   hipFree(h->arena); hipFree(h->d_pose); hipFree(h->d_pose_cs); hipFree(h->d_ray_cs); hipFree(h->d_actor); hipFree(h->d_actor32); hipFree(h->d_params);
-  for (auto& t : h->tracks) {
-    hipFree(t.d_walls); hipFree(t.d_segs); hipFree(t.d_prefix);
-    hipFree(t.bp.d_start); hipFree(t.bp.d_idx); hipFree(t.bp.d_box); hipFree(t.sn.d_start); hipFree(t.sn.d_idx); hipFree(t.d_groups); hipFree(t.d_swall);
-    hipFree(t.beam.d_cell); hipFree(t.beam.d_start); hipFree(t.beam.d_ent); hipFree(t.beam.d_head);
+  {   // the shared track builds are released (and freed by the last holder) under the cache lock
+    std::lock_guard<std::mutex> lk(g_track_mu);
+    h->tracks.clear();
   }
   hipFree(h->d_tracks); hipFree(h->d_blk_track); hipFree(h->d_blk_env);
   if (h->ev_stage) { hipEventSynchronize(h->ev_stage); hipEventDestroy(h->ev_stage); }
@@ -2455,13 +2502,51 @@ extern "C" void nascar_destroy(NascarHandle* h) {
   delete h;
 }
 
+static int build_track(HostTrack& t, size_t& lds_out, const double* segments, int32_t nseg, double total_length,
+                       const double* walls, int32_t nwall);
 // wall table exactly as Box2D sees it (float32 transform via glibc sinf/cosf, fat AABB, key)
 extern "C" int nascar_add_track(NascarHandle* h, const double* segments, int32_t nseg, double total_length,
                                 const double* walls, int32_t nwall) {
   if (!h || !segments || !walls) return fail("null argument");
   if (nseg < 1 || nseg > MAX_SEG) return fail("segment count %d out of range", nseg);
   if (nwall < 1) return fail("track has no walls");
-  HostTrack t;
+  std::string key;
+  {
+    const int32_t dims[3] = {h->cfg.device, nseg, nwall};
+    key.append((const char*)dims, sizeof dims);
+    key.append((const char*)&total_length, sizeof total_length);
+    key.append((const char*)segments, sizeof(double) * 13 * (size_t)nseg);
+    key.append((const char*)walls, sizeof(double) * 4 * (size_t)nwall);
+  }
+  std::lock_guard<std::mutex> lk(g_track_mu);
+  std::shared_ptr<TrackBuild> tb;
+  {
+    auto it = g_track_cache.find(key);
+    if (it != g_track_cache.end()) tb = it->second.lock();
+  }
+  if (!tb) {
+    tb = std::make_shared<TrackBuild>();
+    tb->device = h->cfg.device;
+    int cur = 0;
+    HIPCHK(hipGetDevice(&cur));
+    if (cur != h->cfg.device) HIPCHK(hipSetDevice(h->cfg.device));
+    const int rc = build_track(tb->t, tb->lds, segments, nseg, total_length, walls, nwall);
+    if (cur != h->cfg.device) hipSetDevice(cur);
+    if (rc < 0) return rc;
+    g_track_cache[key] = tb;
+  }
+  const HostTrack& t = tb->t;
+  h->max_sensor_lds = std::max(h->max_sensor_lds, 2 * sizeof(float4) * t.walls.size() + sizeof(float4) * t.groups.size());
+  h->max_sensor_groups_lds = std::max(h->max_sensor_groups_lds, sizeof(float4) * t.groups.size());
+  h->max_lds = std::max(h->max_lds, tb->lds);
+  h->tracks.push_back(tb);
+  h->dirty_tracks = true;
+  return (int)h->tracks.size() - 1;
+}
+
+// the device tables of one track (nascar_add_track, on the current device); lds: model_kernel's wall table bytes
+static int build_track(HostTrack& t, size_t& lds_out, const double* segments, int32_t nseg, double total_length,
+                       const double* walls, int32_t nwall) {
   t.total_length = total_length;
   t.startline = -1; t.has_banking = 0;
   double pre = 0.0;
@@ -2481,7 +2566,7 @@ extern "C" int nascar_add_track(NascarHandle* h, const double* segments, int32_t
   std::unordered_map<std::string, int> keys;
   for (int j = 0; j < nwall; ++j) {
     const double* w = walls + 4 * j;
-    LWall L;
+    HWall L;
     memset(&L, 0, sizeof L);
     L.px = (float)w[0]; L.py = (float)w[1]; L.ang = (float)w[2];
     L.qs = sinf(L.ang); L.qc = cosf(L.ang);
@@ -2505,9 +2590,17 @@ extern "C" int nascar_add_track(NascarHandle* h, const double* segments, int32_t
     t.walls.push_back(L);
   }
   size_t lds = sizeof(LWall) * t.walls.size();
-  if (lds > 150 * 1024) return fail("track has %d walls; LDS staging limit is %zu", nwall, (size_t)(150 * 1024 / sizeof(LWall)));
-  HIPCHK(hipMalloc(&t.d_walls, sizeof(LWall) * t.walls.size()));
-  HIPCHK(hipMemcpy(t.d_walls, t.walls.data(), sizeof(LWall) * t.walls.size(), hipMemcpyHostToDevice));
+  if (lds > MODEL_WALL_LDS_MAX) return fail("track has %d walls; model_kernel's LDS wall table holds %zu", nwall,
+                                            (size_t)(MODEL_WALL_LDS_MAX / sizeof(LWall)));
+  {
+    std::vector<LWall> dw(t.walls.begin(), t.walls.end());
+    std::vector<float4> fat(t.walls.size());
+    for (size_t j = 0; j < t.walls.size(); ++j) fat[j] = make_float4(t.walls[j].flx, t.walls[j].fly, t.walls[j].fhx, t.walls[j].fhy);
+    HIPCHK(hipMalloc(&t.d_walls, sizeof(LWall) * dw.size()));
+    HIPCHK(hipMemcpy(t.d_walls, dw.data(), sizeof(LWall) * dw.size(), hipMemcpyHostToDevice));
+    HIPCHK(hipMalloc(&t.d_wfat, sizeof(float4) * fat.size()));
+    HIPCHK(hipMemcpy(t.d_wfat, fat.data(), sizeof(float4) * fat.size(), hipMemcpyHostToDevice));
+  }
   HIPCHK(hipMalloc(&t.d_segs, sizeof(DSeg) * t.segs.size()));
   HIPCHK(hipMemcpy(t.d_segs, t.segs.data(), sizeof(DSeg) * t.segs.size(), hipMemcpyHostToDevice));
   HIPCHK(hipMalloc(&t.d_prefix, sizeof(double) * t.prefix.size()));
@@ -2522,30 +2615,26 @@ extern "C" int nascar_add_track(NascarHandle* h, const double* segments, int32_t
   {   // the sensor kernel's wall image (same f32 values it would stage: rad + 0.25 rounded once)
     std::vector<float4> sw(2 * t.walls.size());
     for (size_t j = 0; j < t.walls.size(); ++j) {
-      const LWall& w = t.walls[j];
+      const HWall& w = t.walls[j];
       sw[2 * j] = make_float4(w.px, w.py, w.rad + 0.25f, w.hx);
       sw[2 * j + 1] = make_float4(w.qs, w.qc, w.hy, 0.0f);
     }
     HIPCHK(hipMalloc(&t.d_swall, sizeof(float4) * sw.size()));
     HIPCHK(hipMemcpy(t.d_swall, sw.data(), sizeof(float4) * sw.size(), hipMemcpyHostToDevice));
   }
-  h->max_sensor_lds = std::max(h->max_sensor_lds, 2 * sizeof(float4) * t.walls.size() + sizeof(float4) * t.groups.size());
-  h->max_sensor_groups_lds = std::max(h->max_sensor_groups_lds, sizeof(float4) * t.groups.size());
   if (getenv("NASCAR_VERBOSE"))
     fprintf(stderr, "nascar_add_track: %d walls, %zu groups; broadphase grid %dx%d (%zu entries), sensor grid %dx%d "
             "(%zu entries, mean %.1f per cell)\n", nwall, t.groups.size(), t.bp.g.nx, t.bp.g.ny, t.bp.idx.size(),
             t.sn.g.nx, t.sn.g.ny, t.sn.idx.size(), (double)t.sn.idx.size() / ((double)t.sn.g.nx * t.sn.g.ny));
   if (getenv("NASCAR_VERBOSE"))
-    fprintf(stderr, "nascar_add_track: beam grid %dx%d, %zu cells with lists, %zu entries (mean %.2f per list), "
-            "%.1f MB, built in %.2f s\n", t.beam.g.nx, t.beam.g.ny, (t.beam.start.size() - 1) / BEAM_NB, t.beam.ent.size(),
-            (double)t.beam.ent.size() / std::max<size_t>(1, t.beam.start.size() - 1),
-            (4.0 * (t.beam.ent.size() + t.beam.start.size() + t.beam.cell.size())) / 1e6, t.beam.build_s);
-  t.beam.cell.clear(); t.beam.start.clear(); t.beam.ent.clear(); t.beam.head.clear();   // the device copies are all the kernels use
-  t.beam.cell.shrink_to_fit(); t.beam.start.shrink_to_fit(); t.beam.ent.shrink_to_fit(); t.beam.head.shrink_to_fit();
-  h->tracks.push_back(t);
-  h->max_lds = std::max(h->max_lds, lds);
-  h->dirty_tracks = true;
-  return (int)h->tracks.size() - 1;
+    fprintf(stderr, "nascar_add_track: beam grid %dx%d (%.2f m cells), %zu cells with lists, %zu entries (mean %.2f per "
+            "list), heads %.1f MB + continuations %.1f MB + cell map %.1f MB, built in %.2f s\n", t.beam.g.nx, t.beam.g.ny,
+            (double)BEAM_CELL, t.beam.nlist / BEAM_NB, t.beam.entries, (double)t.beam.entries / std::max<size_t>(1, t.beam.nlist),
+            16.0 * t.beam.head.size() / 1e6, 4.0 * t.beam.ent.size() / 1e6, 4.0 * t.beam.cell.size() / 1e6, t.beam.build_s);
+  t.beam.cell.clear(); t.beam.ent.clear(); t.beam.head.clear();   // the device copies are all the kernels use
+  t.beam.cell.shrink_to_fit(); t.beam.ent.shrink_to_fit(); t.beam.head.shrink_to_fit();
+  lds_out = lds;
+  return 0;
 }
 
 extern "C" int nascar_set_env_tracks(NascarHandle* h, const int32_t* env_track) {
@@ -2600,9 +2689,10 @@ static int prepare(NascarHandle* h, hipStream_t stream) {
   if (h->tracks.empty()) return fail("no track loaded (nascar_add_track)");
   if (!h->dirty_tracks) return 0;
   std::vector<TrackDev> td;
-  for (auto& t : h->tracks) {
+  for (auto& tp : h->tracks) {
+    const HostTrack& t = tp->t;
     TrackDev d;
-    d.walls = t.d_walls; d.nwall = (int)t.walls.size(); d.segs = t.d_segs; d.nseg = (int)t.segs.size();
+    d.walls = t.d_walls; d.wfat = t.d_wfat; d.nwall = (int)t.walls.size(); d.segs = t.d_segs; d.nseg = (int)t.segs.size();
     d.prefix = t.d_prefix; d.total_length = t.total_length; d.startline = t.startline; d.has_banking = t.has_banking;
     d.bp = t.bp.g; d.sn = t.sn.g; d.groups = t.d_groups; d.ngroup = (int)t.groups.size(); d.swall = t.d_swall;
     d.beam = t.beam.g;
@@ -2746,8 +2836,8 @@ static int launch_step_range(NascarHandle* h, const Params& P, int nb, const voi
                              uint64_t seed, int64_t step, const float* obs_in, float* obs, float* reward,
                              uint8_t* car_flags, uint8_t* env_flags, int32_t auto_reset, float* terminal_obs,
                              hipStream_t s) {
-  hipLaunchKernelGGL(model_kernel, dim3(nb), dim3(SBLOCK), 0, s, P, actions, discrete, terminal_obs != nullptr,
-                     policy, seed, step, obs_in);
+  hipLaunchKernelGGL(model_kernel, dim3(nb), dim3(SBLOCK), MODEL_WALLS_LDS ? h->max_lds : 0, s, P, actions, discrete,
+                     terminal_obs != nullptr, policy, seed, step, obs_in);
   HIPCHK(hipGetLastError());
   if (h->car_contact) {
     hipLaunchKernelGGL(car_contact_kernel, dim3(nb), dim3(SBLOCK), 0, s, P);
