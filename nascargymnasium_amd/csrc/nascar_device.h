@@ -129,6 +129,32 @@ namespace nascar {
 #define RAD_PER_DEG (PI_D / 180.0)
 #define DEG_PER_RAD (180.0 / PI_D)
 
+// Load through a global-address-space pointer.  Pointers read out of memory (the track tables hang off
+// Params::tracks) are generic to the compiler, which then emits flat loads; a flat load waits on both the vector
+// memory and the LDS counters (and completes out of order), so every one of them serialises against the LDS
+// traffic around it.  The tables are global memory, and saying so gives global_load.
+// Aggregates (float4, DSeg, LWall) are copied as native 16 / 8 / 4-byte vectors: a struct copy through the
+// address-space pointer would become a memcpy that forgets the address space again.
+typedef unsigned int gu4 __attribute__((ext_vector_type(4)));
+typedef unsigned int gu2 __attribute__((ext_vector_type(2)));
+template <typename T> __device__ __forceinline__ T ldg(const T* p) {
+  if constexpr (sizeof(T) % 16 == 0) {
+    T r;
+    const __attribute__((address_space(1))) gu4* q = (const __attribute__((address_space(1))) gu4*)p;
+#pragma unroll
+    for (int i = 0; i < (int)(sizeof(T) / 16); ++i) { const gu4 v = q[i]; __builtin_memcpy((char*)&r + 16 * i, &v, 16); }
+    return r;
+  } else if constexpr (sizeof(T) % 8 == 0) {
+    T r;
+    const __attribute__((address_space(1))) gu2* q = (const __attribute__((address_space(1))) gu2*)p;
+#pragma unroll
+    for (int i = 0; i < (int)(sizeof(T) / 8); ++i) { const gu2 v = q[i]; __builtin_memcpy((char*)&r + 8 * i, &v, 8); }
+    return r;
+  } else {
+    return *(const __attribute__((address_space(1))) T*)p;
+  }
+}
+
 // ------------------------------------------------------------------ vectors
 struct V2 { float x, y; };
 struct Rot { float s, c; };
@@ -254,7 +280,7 @@ __device__ __forceinline__ bool grid_list(const WallGrid& g, float x, float y, i
   const float fx = (x - g.ox) * g.inv_cell, fy = (y - g.oy) * g.inv_cell;
   if (!(fx >= 0.0f && fy >= 0.0f && fx < (float)g.nx && fy < (float)g.ny)) return false;
   const int cell = (int)fy * g.nx + (int)fx;
-  beg = g.start[cell]; end = g.start[cell + 1];
+  beg = ldg(g.start + cell); end = ldg(g.start + cell + 1);
   return true;
 }
 
@@ -374,20 +400,20 @@ __device__ inline void find_new_contacts(Car& c, const WallSet& S) {
     for (int k = beg; k < end; k += BP_BATCH) {
       float4 b[BP_BATCH];
 #pragma unroll
-      for (int u = 0; u < BP_BATCH; ++u) b[u] = box[k + u];   // in bounds: the array is padded by BP_BATCH
+      for (int u = 0; u < BP_BATCH; ++u) b[u] = ldg(box + k + u);   // in bounds: the array is padded by BP_BATCH
 #pragma unroll
       for (int u = 0; u < BP_BATCH; ++u) {
         if (k + u >= end) break;
         Aabb a; a.lo = V(b[u].x, b[u].y); a.hi = V(b[u].z, b[u].w);
-        if (overlap(c.fat, a)) add_pair(c, (int)list[k + u]);
+        if (overlap(c.fat, a)) add_pair(c, (int)ldg(list + k + u));
       }
     }
     return;
   }
 #endif
   for (int k = beg; k < end; ++k) {
-    const int j = list ? (int)list[k] : k;
-    if (!overlap(c.fat, fat_box(S.fat[j]))) continue;
+    const int j = list ? (int)ldg(list + k) : k;
+    if (!overlap(c.fat, fat_box(ldg(S.fat + j)))) continue;
     bool exists = false;
     for (int i = 0; i < c.nct; ++i) if (c.ct[i].wall == j) { exists = true; break; }
     if (exists) continue;
@@ -591,7 +617,7 @@ __device__ inline void collide(Car& c, const WallSet& S) {
   while (i < c.nct) {
     if (!c.awake) { ++i; continue; }
     const int wall = c.ct[i].wall;
-    if (!overlap(c.fat, fat_box(S.fat[wall]))) {
+    if (!overlap(c.fat, fat_box(ldg(S.fat + wall)))) {
       bool touching = (c.ct[i].flags & CT_TOUCH) != 0;
       remove_contact(c, i);
       if (touching) lis_end(c, W[wall].key);

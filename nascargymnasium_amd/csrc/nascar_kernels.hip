@@ -83,7 +83,7 @@ struct BeamHead { uint4 w[BEAM_HW]; };
 __device__ __forceinline__ BeamHead beam_head(const BeamGrid& G, int li) {
   BeamHead h;
 #pragma unroll
-  for (int k = 0; k < BEAM_HW; ++k) h.w[k] = G.head[(size_t)li * BEAM_HW + k];
+  for (int k = 0; k < BEAM_HW; ++k) h.w[k] = ldg(G.head + (size_t)li * BEAM_HW + k);
   return h;
 }
 #define MODEL_WALL_LDS_MAX ((size_t)1024 * sizeof(LWall))   // walls per track model_kernel's LDS table holds
@@ -128,7 +128,7 @@ __device__ __forceinline__ int blk_track_of(const Params& P, int b) { return P.o
 // BeamGrid list base (built cell id * BEAM_NB) of the cell holding (x, y); -1 outside the built cells
 __device__ __forceinline__ int beam_cell_base(const BeamGrid& G, float x, float y) {
   const float fx = (x - G.ox) * G.inv_cell, fy = (y - G.oy) * G.inv_cell;
-  if (fx >= 0.0f && fy >= 0.0f && fx < (float)G.nx && fy < (float)G.ny) return G.cell[(int)fy * G.nx + (int)fx];
+  if (fx >= 0.0f && fy >= 0.0f && fx < (float)G.nx && fy < (float)G.ny) return ldg(G.cell + (int)fy * G.nx + (int)fx);
   return -1;
 }
 
@@ -787,9 +787,9 @@ __device__ inline bool query_on_wall(const WallSet& S, double px, double py, dou
     list = S.bp.idx;
   else { beg = 0; end = S.nw; }
   for (int kk = beg; kk < end; ++kk) {
-    const int jw = list ? (int)list[kk] : kk;
+    const int jw = list ? (int)ldg(list + kk) : kk;
     const LWall& wl = W[jw];
-    if (!overlap(fat_box(S.fat[jw]), q)) continue;
+    if (!overlap(fat_box(ldg(S.fat + jw)), q)) continue;
     Xf xf = wall_xf(wl);
     Poly p; make_box(&p, wl.hx, wl.hy);
     V2 pl = rmulT(xf.q, vsub(center, xf.p));
@@ -1198,7 +1198,7 @@ __device__ inline float ray_fallback(const TrackDev& T, V2 p1, float p2x, float 
   const float4* __restrict__ sw = T.swall;
   float bi = 2.0f;
   for (int kk = beg; kk < end; ++kk) {
-    const float4 G = T.groups[list ? (int)list[kk] : kk];
+    const float4 G = ldg(T.groups + (list ? (int)ldg(list + kk) : kk));
     const float grx = G.x - p1.x, gry = G.y - p1.y;
     const float d2 = grx * grx + gry * gry;
     if (d2 > (250.0f + G.z) * (250.0f + G.z)) continue;
@@ -1207,7 +1207,7 @@ __device__ inline float ray_fallback(const TrackDev& T, V2 p1, float p2x, float 
     float dlo;
     if (G.z > 24.0f) {
       const int j = __float_as_int(G.w) & 0xFFFF;
-      const float4 wa = sw[2 * j], wb = sw[2 * j + 1];
+      const float4 wa = ldg(sw + 2 * j), wb = ldg(sw + 2 * j + 1);
       const float ex = wa.w * wb.y, ey = wa.w * wb.x;
       const float cx = wa.x - p1.x, cy = wa.y - p1.y;
       float dseg;
@@ -1219,7 +1219,7 @@ __device__ inline float ray_fallback(const TrackDev& T, V2 p1, float p2x, float 
     }
     if (!((mask >> i) & 1u) || dlo > bi) continue;
     const int first = __float_as_int(G.w) & 0xFFFF, cnt = __float_as_int(G.w) >> 16;
-    for (int j = first; j < first + cnt; ++j) bi = wall_cast(sw[2 * j], sw[2 * j + 1], p1, p2x, p2y, dx, dy, bi);
+    for (int j = first; j < first + cnt; ++j) bi = wall_cast(ldg(sw + 2 * j), ldg(sw + 2 * j + 1), p1, p2x, p2y, dx, dy, bi);
   }
   return bi;
 }
@@ -1274,7 +1274,7 @@ __device__ __forceinline__ float ray_walk(const BeamGrid& G, const float4* __res
     for (uint32_t k = tail;; k += RAY_CHUNK) {   // RAY_CHUNK entries requested together, walked in order to the sentinel
       uint32_t v4[RAY_CHUNK];
 #pragma unroll
-      for (int q = 0; q < RAY_CHUNK; ++q) v4[q] = G.ent[k + q];
+      for (int q = 0; q < RAY_CHUNK; ++q) v4[q] = ldg(G.ent + k + q);
       bool stop = false;
 #pragma unroll
       for (int q = 0; q < RAY_CHUNK; ++q) {
@@ -1457,7 +1457,7 @@ ray_sensor_kernel(Params P, float* obs, float* terminal_obs, int passes) {
   {
     float4* s_w = (float4*)smem;
     const int nw2 = 2 * T.nwall;
-    for (int k = t; k < nw2; k += BLOCK) s_w[k] = T.swall[k];
+    for (int k = t; k < nw2; k += BLOCK) s_w[k] = ldg(T.swall + k);
     __syncthreads();
   }
   if (env < 0) return;
@@ -1577,12 +1577,12 @@ __global__ void __launch_bounds__(SBLOCK) __attribute__((amdgpu_waves_per_eu(MOD
     }
   }
   TrackDev T = P.tracks[blk_track_of(P, (blockIdx.x + P.blk0))];
-  if (tid < T.nseg) s_segs[tid] = T.segs[tid];
+  if (tid < T.nseg) s_segs[tid] = ldg(T.segs + tid);
 #if MODEL_WALLS_LDS
   // the track's wall table in LDS: every contact update, TOI pair, island and listener lookup of the Box2D step
   // reads it (one staging per workgroup instead of a dependent L2 round trip per access)
   LWall* s_w = (LWall*)smem;
-  for (int k = tid; k < T.nwall; k += SBLOCK) s_w[k] = T.walls[k];
+  for (int k = tid; k < T.nwall; k += SBLOCK) s_w[k] = ldg(T.walls + k);
 #endif
   __syncthreads();
   T.segs = s_segs;
@@ -1608,8 +1608,8 @@ struct LogicLDS {
 struct TrackLDS { DSeg segs[MAX_SEG]; double prefix[MAX_SEG]; float4 sg[MAX_SEG]; float rll[MAX_SEG]; };
 __device__ __forceinline__ void stage_track_lds(const TrackDev& T, TrackLDS& TL, int tid) {
   if (tid < T.nseg) {
-    const DSeg sg = T.segs[tid];
-    TL.segs[tid] = sg; TL.prefix[tid] = T.prefix[tid];
+    const DSeg sg = ldg(T.segs + tid);
+    TL.segs[tid] = sg; TL.prefix[tid] = ldg(T.prefix + tid);
     const double dx = sg.ex - sg.sx, dy = sg.ey - sg.sy, ll = dx * dx + dy * dy;
     TL.sg[tid] = make_float4((float)sg.sx, (float)sg.sy, (float)dx, (float)dy);
     TL.rll[tid] = ll < 1e-6 ? 0.0f : (float)(1.0 / ll);
@@ -1982,7 +1982,7 @@ rollout_kernel(const Params* __restrict__ Pg, int K, int policy, uint64_t seed, 
     const TrackDev T = P.tracks[blk_track_of(P, blockIdx.x)];
     stage_track_lds(T, g_ro_track, threadIdx.x);
     float4* s_w = (float4*)smem;   // [2 * nwall] sensor wall image
-    for (int k = threadIdx.x; k < 2 * T.nwall; k += SBLOCK) s_w[k] = T.swall[k];
+    for (int k = threadIdx.x; k < 2 * T.nwall; k += SBLOCK) s_w[k] = ldg(T.swall + k);
   }
   __syncthreads();
 #pragma unroll 1
