@@ -680,6 +680,7 @@ template <int NMAX> __device__ __forceinline__ void cs_init(VC* vc, int n, const
 template <int NMAX> __device__ __forceinline__ void cs_init_velocity(VC* vc, int n, const Car& c, const BodyState& A) {
   const float mA = CAR_INV_MASS, iA = CAR_INV_I, mB = 0.0f, iB = 0.0f;
   const float friction_unused = 0.0f; (void)friction_unused;
+  const Rot qA = rot_set(A.a);   // b2Rot::Set(aA) of every contact below: A is the same body state for all of them
 #pragma unroll UNROLL_SMALL   // registers for small islands; the general bound stays a loop
   for (int i = 0; i < NMAX; ++i) {
     if (i >= n) break;
@@ -688,7 +689,7 @@ template <int NMAX> __device__ __forceinline__ void cs_init_velocity(VC* vc, int
     V2 cA = A.c; float aA = A.a; V2 vA = A.v; float wA = A.w;
     V2 cB = v.cB; float aB = v.aB; V2 vB = v.vB; float wB = v.wB;
     Xf xfA, xfB;
-    xfA.q = rot_set(aA); xfB.q = rot_static(aB, v.aB0, v.qB);
+    xfA.q = qA; xfB.q = rot_static(aB, v.aB0, v.qB);
     xfA.p = vsub(cA, rmul(xfA.q, zero2()));
     xfB.p = vsub(cB, rmul(xfB.q, zero2()));
     V2 normal = zero2(), pts[2];
@@ -837,7 +838,14 @@ template <int NMAX> __device__ __forceinline__ void cs_store(const VC* vc, int n
   }
 }
 
-template <int NMAX> __device__ __forceinline__ int cs_solve_position(VC* vc, int n, BodyState& A, int toi) {
+// b2Rot::Set of the car's angle, recomputed only when the angle's bits changed since the last call (a point whose
+// position impulse is zero leaves the angle bit for bit as it was: the same input, the same sinf / cosf)
+struct RotCache { uint32_t bits; Rot q; };
+__device__ __forceinline__ Rot rot_cached(RotCache& rc, float a) {
+  if (__float_as_uint(a) != rc.bits) { rc.bits = __float_as_uint(a); rc.q = rot_set(a); }
+  return rc.q;
+}
+template <int NMAX> __device__ __forceinline__ int cs_solve_position(VC* vc, int n, BodyState& A, int toi, RotCache& rcA) {
   float minSep = 0.0f;
   const float mA = CAR_INV_MASS, iA = CAR_INV_I, mB = 0.0f, iB = 0.0f;
 #pragma unroll UNROLL_SMALL   // registers for small islands; the general bound stays a loop
@@ -848,7 +856,7 @@ template <int NMAX> __device__ __forceinline__ int cs_solve_position(VC* vc, int
     for (int j = 0; j < 2; ++j) {
       if (j >= v.pcount) break;
       Xf xfA, xfB;
-      xfA.q = rot_set(aA); xfB.q = rot_static(aB, v.aB0, v.qB);
+      xfA.q = rot_cached(rcA, aA); xfB.q = rot_static(aB, v.aB0, v.qB);
       xfA.p = vsub(cA, rmul(xfA.q, zero2()));
       xfB.p = vsub(cB, rmul(xfB.q, zero2()));
       V2 normal, point; float sep;
@@ -930,9 +938,10 @@ __device__ __forceinline__ int solve_island(Car& c, const LWall* W, const int* c
   cs_store<NMAX>(vc, n, c);
   integrate_positions(A, h);
   int positionSolved = 0;
-  for (int it = 0; it < 4; ++it) { if (cs_solve_position<NMAX>(vc, n, A, 0)) { positionSolved = 1; break; } }
+  RotCache rcA; rcA.bits = __float_as_uint(A.a) ^ 1u; rcA.q.s = 0.0f; rcA.q.c = 1.0f;   // (empty: no angle matches)
+  for (int it = 0; it < 4; ++it) { if (cs_solve_position<NMAX>(vc, n, A, 0, rcA)) { positionSolved = 1; break; } }
   c.c = A.c; c.a = A.a; c.v = A.v; c.w = A.w;
-  sync_transform(c);
+  c.xf.q = rot_cached(rcA, c.a); c.xf.p = vsub(c.c, rmul(c.xf.q, zero2()));   // sync_transform
   report<NMAX>(c, vc, n);
   return positionSolved;
 }
@@ -1260,13 +1269,14 @@ __device__ __forceinline__ void island_solve_toi_n(Car& c, const LWall* W, const
   BodyState A; A.c = c.c; A.a = c.a; A.v = c.v; A.w = c.w;
   VC vc[NMAX];
   cs_init<NMAX>(vc, n, c, cidx, W, false, 1.0f);
-  for (int it = 0; it < 20; ++it) { if (cs_solve_position<NMAX>(vc, n, A, 1)) break; }
+  RotCache rcA; rcA.bits = __float_as_uint(c.a) ^ 1u; rcA.q.s = 0.0f; rcA.q.c = 1.0f;   // (empty: no angle matches)
+  for (int it = 0; it < 20; ++it) { if (cs_solve_position<NMAX>(vc, n, A, 1, rcA)) break; }
   c.c0 = A.c; c.a0 = A.a;
   cs_init_velocity<NMAX>(vc, n, c, A);
   for (int it = 0; it < 6; ++it) cs_solve_velocity<NMAX>(vc, n, A, friction);
   integrate_positions(A, subdt);
   c.c = A.c; c.a = A.a; c.v = A.v; c.w = A.w;
-  sync_transform(c);
+  c.xf.q = rot_cached(rcA, c.a); c.xf.p = vsub(c.c, rmul(c.xf.q, zero2()));   // sync_transform
   report<NMAX>(c, vc, n);
 }
 __device__ inline void island_solve_toi(Car& c, const LWall* W, const int* cidx, int n, float subdt, float friction) {
@@ -1330,14 +1340,15 @@ __device__ __forceinline__ bool toi_far(const Car& c, const Poly* pa, const LWal
 // wall re-scans its 2-5 contacts after each event: sequential on one lane before).  Same alphas, same
 // scan order, same minimum, so the results are Box2D's.
 // b2TimeOfImpact of the car's sweep against static wall wl -> alpha of SolveTOI (1 unless TOUCHING)
-__device__ __forceinline__ float toi_alpha(float4 s0, float4 s1, const LWall& wl) {
+__device__ __forceinline__ float toi_alpha(float4 s0, float4 s1, const LWall& wl, int* iters = nullptr,
+                                           unsigned long long* cyc = nullptr) {
   Poly pa; make_box(&pa, CAR_HX, CAR_HY);
   Poly pb; make_box(&pb, wl.hx, wl.hy);
   Sweep sA; sA.c0 = V(s0.x, s0.y); sA.c = V(s0.z, s0.w); sA.a0 = s1.x; sA.a = s1.y; sA.alpha0 = s1.z;
   Sweep sB; sB.c0 = V(wl.px, wl.py); sB.c = sB.c0; sB.a0 = wl.ang; sB.a = wl.ang; sB.alpha0 = 0.0f;
   int state;
   Rot qw; qw.s = wl.qs; qw.c = wl.qc;
-  const float beta = time_of_impact(&state, &pa, sA, &pb, sB, 1.0f, qw, __float_as_uint(wl.ang));
+  const float beta = time_of_impact(&state, &pa, sA, &pb, sB, 1.0f, qw, __float_as_uint(wl.ang), iters, cyc);
   return state == TOI_TOUCHING ? fminb(s1.z + (1.0f - s1.z) * beta, 1.0f) : 1.0f;
 }
 __device__ inline void solve_toi(Car& c, const WallSet& S, float dt, float friction) {
@@ -1395,7 +1406,13 @@ __device__ inline void solve_toi(Car& c, const WallSet& S, float dt, float frict
         const int2 jb = L.job[j];
         const int owner = jb.x & 0xFF;
         PCOUNT(12, 1); CCOUNT(c, 2, 1);
+#ifdef NASCAR_PROFILE   // per computing lane: TOI outer / root-finder iterations, GJK and separation-function cycles
+        int it2[2] = {0, 0}; unsigned long long cy2[2] = {0ull, 0ull};
+        L.res[j] = toi_alpha(L.sw0[owner], L.sw1[owner], W[jb.y], it2, cy2);
+        CCOUNT(c, 6, it2[0]); CCOUNT(c, 7, it2[1]); CCOUNT(c, 9, cy2[0]); CCOUNT(c, 10, cy2[1]);
+#else
         L.res[j] = toi_alpha(L.sw0[owner], L.sw1[owner], W[jb.y]);
+#endif
       }
       wave_lds_sync();
       {

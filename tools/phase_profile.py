@@ -135,15 +135,18 @@ def main():
                     print("   ", i, *cp[i, [0, 1, 2, 3, 4, 5, 6, 7]].tolist(), f"| bp full scans {cp[i, 8]}, candidates {cp[i, 9]}"
                           f" | x {info[i, F.index('x')]:.1f} y {info[i, F.index('y')]:.1f} v ({info[i, F.index('vx')]:.1f}, "
                           f"{info[i, F.index('vy')]:.1f}) angle {info[i, F.index('angle')]:.2f} disabled {info[i, F.index('disabled')]:.0f} n_contacts {info[i, F.index('n_contacts')]:.0f}")
-            for i in np.argsort(-cyc)[:12]:
-                print(f"    car {i}: wave b2 {cp[i, 0]}, solve_toi scans {cp[i, 14]}, TOI job rounds {cp[i, 13]} cycles, "
-                      f"event processing {cp[i, 15]} cycles, events {cp[i, 4]}, island solve {cp[i, 11]}, "
-                      f"event contact updates {cp[i, 12]}")
-            for i in np.argsort(-cyc)[:24]:
-                if cp[i, 10] or cp[i, 9]:
-                    iso = f", isolated single-lane TOI {cp[i, 13] / cp[i, 9]:.0f} cycles/call" if cp[i, 9] else ""
-                    print(f"    car {i} solve_toi cycles: TOI calls {cp[i, 10]} (GJK {cp[i, 14]}, separation fn {cp[i, 15]}), "
-                          f"island solves {cp[i, 11]}, event contact updates {cp[i, 12]}{iso}")
+            w0 = np.argsort(-cyc)[0] // 64 * 64
+            print(f"  slowest wave (cars {w0}..{w0 + 63}): solve_toi scans {cp[w0, 14]}, TOI job rounds {cp[w0, 13]} cycles, "
+                  f"event processing {cp[w0, 15]} cycles")
+            for i in range(w0, min(w0 + 64, len(cp))):
+                if cp[i, 4] or cp[i, 2]:
+                    print(f"    car {i}: events {cp[i, 4]}, island solve {cp[i, 11]}, event contact updates {cp[i, 12]}, "
+                          f"TOI calls computed by this lane {cp[i, 2]}: outer iters {cp[i, 6]}, root iters {cp[i, 7]}, "
+                          f"GJK cycles {cp[i, 9]}, separation-fn cycles {cp[i, 10]}")
+            tc = cp[:, 2].sum()
+            if tc:
+                print(f"  all TOI calls {tc}: outer iters/call {cp[:, 6].sum() / tc:.2f}, root iters/call {cp[:, 7].sum() / tc:.2f}, "
+                      f"GJK cycles/call {cp[:, 9].sum() / tc:.0f}, separation-fn cycles/call {cp[:, 10].sum() / tc:.0f}")
             ev = np.argsort(-cp[:, 4])[:12]
             print("  cars with the most TOI events: car, wave b2 cycles, events, TOI solved, contacts at start, "
                   "TOI-call cycles, island-solve cycles, event contact-update cycles, outer iterations")
@@ -153,9 +156,6 @@ def main():
             evw = cp[cp[:, 4] > 0, 0]
             if len(evw):
                 print(f"  b2 cycles of cars with TOI events: mean {evw.mean():.0f}, max {evw.max()}; cars with events {len(evw)}")
-            m9 = cp[:, 9] > 0
-            if m9.any():
-                print(f"  isolated single-lane TOI: {cp[m9, 13].sum() / cp[m9, 9].sum():.0f} cycles/call over {cp[m9, 9].sum()} calls")
             wv = m[np.argmax(m[:, 4] - m[:, 3])]
             print("  slowest wave's b2_step phases (cycles): collide", wv[11] - wv[3], "solve", wv[12] - wv[11],
                   "sync+find", wv[13] - wv[12], "toi", wv[4] - wv[13])
