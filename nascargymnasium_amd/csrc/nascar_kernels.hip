@@ -1251,6 +1251,12 @@ __device__ __forceinline__ void quad_transpose(const float v[4], float o[4], int
 #define RSENSOR_WPE 6   // 4 lanes per car at 6 waves/SIMD: 41.5 us (8 lanes 53.7, 2 lanes 44.3; 16 lanes 62.4)
 #endif
 #define RAY_LPC 4     // lanes per car; each lane walks the lists of rays r, r + 4, r + 8, r + 12
+#ifndef RAY_HEADS_AHEAD
+#define RAY_HEADS_AHEAD 0
+#endif
+#ifndef RAY_NO_WALK
+#define RAY_NO_WALK 0
+#endif
 // One ray's walk of its beam list (list index li, head record h = G.head[li]): the first BEAM_HEAD entries from
 // the head, the rest of the list only when all of them were walked; stops at the first entry whose distance
 // bound lies beyond the best hit.  Returns the best b2PolygonShape::RayCast fraction (2 = no hit).
@@ -1331,7 +1337,18 @@ __device__ __forceinline__ void ray_lane(const Params& P, const TrackDev& T, con
     }
     auto slot_of = [&](int i) { return (slot0 & ~15) | ((slot0 - i) & 15); };
     float v[RPL] = {0.0f, 0.0f, 0.0f, 0.0f};
+#if RAY_HEADS_AHEAD
+    // the four rays' list heads requested together (independent 16-byte loads) before the first walk
+    BeamHead hd[RPL];
+#pragma unroll
+    for (int q = 0; q < RPL; ++q) {
+      if (base >= 0) hd[q] = beam_head(G, base + slot_of(r + RAY_LPC * q));
+      else for (int k = 0; k < BEAM_HW; ++k) hd[q].w[k] = make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+#else
 #pragma unroll 1
+#endif
     for (int q = 0; q < RPL; ++q) {
       const int i = r + RAY_LPC * q;
       double dxd, dyd;
@@ -1342,7 +1359,14 @@ __device__ __forceinline__ void ray_lane(const Params& P, const TrackDev& T, con
       float bi = 2.0f;
       if (base >= 0) {
         const int sl = slot_of(i);
+#if RAY_HEADS_AHEAD
+        bi = ray_walk(G, sw, base + sl, hd[q], p1, p2, dx, dy);
+#elif RAY_NO_WALK   // timing probe only (wrong results): the head load without the walk
+        const BeamHead h = beam_head(G, base + sl);
+        bi = __uint_as_float((h.w[0].x & 1u) | 0x3f800000u);
+#else
         bi = ray_walk(G, sw, base + sl, beam_head(G, base + sl), p1, p2, dx, dy);
+#endif
       } else {
         PCOUNT(9, 1);
         bi = ray_fallback(T, p1, p2.x, p2.y, dx, dy, ps.z, i);
@@ -2448,7 +2472,19 @@ extern "C" int nascar_create(const NascarConfig* cfg, NascarHandle** out) {
   NascarHandle* h = new NascarHandle();
   h->cfg = *cfg;
   h->E = cfg->num_envs; h->C = cfg->num_cars; h->N = h->E * h->C;
+  // envs per workgroup of the one-lane-per-car kernels: as many whole envs as fit (SBLOCK / C), unless that leaves
+  // fewer than 2 workgroups per CU -- a small batch (e.g. 4096 envs x 1 car: 32 workgroups) is then spread over
+  // 2 x CUs workgroups with fewer envs each.  Every step kernel lasts as long as its slowest wave, and a wave's
+  // time is the sum over its phases of the slowest lane's: fewer cars per wave shorten the slowest car's wait on
+  // its wave-mates (the chip has room for the extra, partly empty waves).  NASCAR_EPB overrides (A/B).
   h->epb = SBLOCK / h->C;
+  {
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, cfg->device) != hipSuccess || cus <= 0) cus = 256;
+    const long target = 2L * cus;
+    if ((h->E + h->epb - 1) / h->epb < target) h->epb = std::max(1, (int)((h->E + target - 1) / target));
+    if (const char* ev = getenv("NASCAR_EPB")) { const int v = atoi(ev); if (v >= 1 && v <= SBLOCK / h->C) h->epb = v; }
+  }
   size_t N = h->N, E = h->E, o = 0;
   h->off_f32 = o; o = align256(o + sizeof(float) * N_F32 * N);
   h->off_f64 = o; o = align256(o + sizeof(double) * N_F64 * N);
