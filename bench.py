@@ -295,6 +295,21 @@ def stats_pass(env, step, first, KR):
     return kern_ms, tally.tolist(), KR
 
 
+def kernel_pass(env, step, first, KR):
+    """per-kernel durations of the whole-grid step (the per-step path, nascar_step_driven / nascar_step): HIP events
+    recorded by the engine before model_kernel, after it, after logic_kernel and after the sensor launch, on the launch
+    stream (nascar_set_step_events), over KR steps of the same workload.  Returns mean ms per launch of each kernel."""
+    import torch
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(KR)]
+    for i in range(KR):
+        step.env.set_step_events(evs[i])
+        step(first + i)
+    step.env.set_step_events(None)
+    torch.cuda.synchronize()
+    t = [[e[k].elapsed_time(e[k + 1]) for k in range(3)] for e in evs]
+    return {name: sum(r[k] for r in t) / KR for k, name in enumerate(("model_kernel", "logic_kernel", "ray_sensor_kernel"))}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -393,18 +408,24 @@ def main():
     elapsed = timed(step, base + W, K, world)
     KR = min(K, 50)
     kern_ms, tally, KT = stats_pass(env, step, base + W + K, KR)   # KT: the steps the tallies cover
+    ktimes = kernel_pass(env, Stepper(env, args.policy, rank, acts, None, 0), base + W + K + 2 * KR, KR)
     per_step = None
     if step.R:   # the per-step path on the same envs, timed the same way (labelled secondary)
         ps = Stepper(env, args.policy, rank, acts, None, 0)
-        first = base + W + K + 2 * KR
+        first = base + W + K + 3 * KR
         ps.run(first, W)
         per_step = timed(ps, first + W, K, world)
     elapsed, kern_ms = reduce_max([elapsed, kern_ms], dev)
+    kt_names = ("model_kernel", "logic_kernel", "ray_sensor_kernel")
+    ktimes = dict(zip(kt_names, reduce_max([ktimes[k] for k in kt_names], dev)))
     if per_step is not None:
         per_step = reduce_max([per_step], dev)[0]
     tally = reduce_sum(tally, dev)
     value = throughput(world, E, C, K, elapsed)
-    achieved = E * C * ALGO_BYTES_PER_CAR_STEP / (kern_ms * 1e-3) / 1e9
+    # dominant kernel (model_kernel, whole grid): the step's algorithmic bytes per car-step x the cars one launch
+    # processes, over its mean launch duration (HIP events around it on its stream, per-step path)
+    achieved = E * C * ALGO_BYTES_PER_CAR_STEP / (ktimes["model_kernel"] * 1e-3) / 1e9
+    step_achieved = E * C * ALGO_BYTES_PER_CAR_STEP / (elapsed / K) / 1e9      # the timed window itself
     traffic, tnote = None, "no PMC file for this workload"
     tfile = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if os.path.exists(tfile):
@@ -416,9 +437,10 @@ def main():
         elif tj.get("source_sha") != source_sha():
             tnote = f"stale: profiles/pmc_traffic.json ({tj.get('tag')}) was measured on other kernel sources"
         else:
-            traffic = tj["bytes_per_step"]
-            tnote = f"rocprofv3 FETCH_SIZE/WRITE_SIZE passes of this build and workload ({tj.get('tag')}, " \
-                    f"profiles/pmc_traffic.json; not re-measured in this run)"
+            traffic = tj.get("model_kernel_bytes")
+            tnote = f"model_kernel HBM bytes per whole-grid launch from the rocprofv3 FETCH_SIZE/WRITE_SIZE passes of this " \
+                    f"build and workload ({tj.get('tag')}, profiles/pmc_traffic.json; not re-measured in this run); whole " \
+                    f"step {tj.get('bytes_per_step', 0) / 1e6:.1f} MB"
     ncs = world * E * C * KT
     wstats = {"source": POLICY_TEXT[args.policy], "settle_steps": S if not args.load_state else f"state file {args.load_state}",
               "staggered_env_ages": closed and not args.no_stagger, "window_car_steps": ncs,
@@ -456,8 +478,15 @@ def main():
                                    else ", RCCL gather of obs/reward/flags to rank 0 per step)") if gather else ", no collective)")},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": tnote,
-                     "kernel": kernel_txt, "kernel_ms": kern_ms,
-                     "algo_bytes_per_car_step": ALGO_BYTES_PER_CAR_STEP},
+                     "kernel": "model_kernel (dominant kernel; whole-grid launch on the per-step path, HIP events around "
+                               "each launch on its stream)",
+                     "kernel_ms": ktimes["model_kernel"], "units_per_launch": E * C,
+                     "algo_bytes_per_car_step": ALGO_BYTES_PER_CAR_STEP,
+                     "kernel_times_ms": ktimes,
+                     "step": {"achieved": step_achieved, "frac": step_achieved / HBM_PEAK_GBS, "ms": elapsed / K * 1e3,
+                              "note": "the same bytes over the timed window's time per step (" + launch_txt + ")"},
+                     "timed_path_event_ms": kern_ms,
+                     "timed_path_event_note": kernel_txt},
         "workload_stats": wstats,
         "engine_errors": int(tally[5]),
     }

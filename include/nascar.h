@@ -107,6 +107,12 @@ int nascar_rollout(NascarHandle* h, int32_t policy, uint64_t seed, int64_t step0
 int nascar_set_rollout_streams(NascarHandle* h, int32_t streams);
 int nascar_get_rollout_streams(NascarHandle* h);
 
+/* Profiling hook (no reference counterpart; bench.py's per-kernel roofline): events = 4 caller-created timing
+ * events (hipEvent_t), recorded by every following whole-grid step (nascar_step / nascar_step_driven) on its
+ * stream before model_kernel, after model_kernel, after logic_kernel and after the sensor launch; n = 0 stops.
+ * The events stay owned by the caller and must outlive their use. */
+int nascar_set_step_events(NascarHandle* h, void* const* events, int32_t n);
+
 /* Info builder (src/car_env.py:1160-1227, src/lap_timer.py:354-372): per-car float64 [E*C*N_INFO]
  * (field order: nascargymnasium_amd/_lib.py INFO_FIELDS) written to a device buffer. */
 int nascar_get_info(NascarHandle* h, double* info, void* stream);

@@ -104,6 +104,8 @@ def lib():
     L.nascar_set_actor_precision.restype = ctypes.c_int
     L.nascar_actor_forward.argtypes = [vp, vp, i32, vp, vp]
     L.nascar_actor_forward.restype = ctypes.c_int
+    L.nascar_set_step_events.argtypes = [vp, ctypes.POINTER(vp), i32]
+    L.nascar_set_step_events.restype = ctypes.c_int
     L.nascar_debug_sincosf.argtypes = [vp, vp, vp, i32, vp]
     L.nascar_debug_sincosf.restype = ctypes.c_int
     L.nascar_debug_sensors.argtypes = [vp, vp, vp, i32, vp]
@@ -114,7 +116,7 @@ def lib():
 
 EXPORTED = ["nascar_create", "nascar_destroy", "nascar_last_error", "nascar_add_track", "nascar_set_env_tracks",
             "nascar_reset", "nascar_step", "nascar_step_driven", "nascar_rollout", "nascar_get_info", "nascar_set_perf_history", "nascar_set_car_contact", "nascar_set_rollout_streams", "nascar_get_rollout_streams", "nascar_state_bytes", "nascar_get_state",
-            "nascar_set_state", "nascar_policy_actions", "nascar_set_actor", "nascar_set_actor_precision", "nascar_actor_forward",
+            "nascar_set_state", "nascar_policy_actions", "nascar_set_step_events", "nascar_set_actor", "nascar_set_actor_precision", "nascar_actor_forward",
             "nascar_debug_sincosf", "nascar_debug_sensors"]
 
 

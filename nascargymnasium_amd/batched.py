@@ -229,6 +229,24 @@ class BatchedCarEnv:
         if not t.is_contiguous():
             raise ValueError(f"out {name}: must be contiguous")
 
+    def set_step_events(self, events=None):
+        """Profiling hook (nascar_set_step_events): 4 torch.cuda.Event(enable_timing=True) recorded by every following
+        whole-grid step on its stream -- before model_kernel, after model_kernel, after logic_kernel, after the
+        sensor launch -- so their elapsed times are the three kernels' durations; None switches it off."""
+        if events is None:
+            _lib.check(self.L.nascar_set_step_events(self.h, None, 0))
+            self._step_events = None
+            return
+        if len(events) != 4:
+            raise ValueError("need 4 events")
+        with torch.cuda.device(self.device):
+            for e in events:
+                if not e.cuda_event:   # torch creates the HIP event at its first record
+                    e.record()
+            arr = (ctypes.c_void_p * 4)(*[ctypes.c_void_p(e.cuda_event) for e in events])
+            _lib.check(self.L.nascar_set_step_events(self.h, arr, 4))
+        self._step_events = list(events)    # kept alive while the engine may record them
+
     def info_tensor(self) -> torch.Tensor:
         """per-car info [E, C, N_INFO] float64 (fields: _lib.INFO_FIELDS)."""
         with torch.cuda.device(self.device):

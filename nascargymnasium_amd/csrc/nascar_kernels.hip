@@ -2454,6 +2454,7 @@ struct NascarHandle {
   hipEvent_t ev_fork = nullptr;
   std::vector<hipEvent_t> ev_join;
   float* d_ro_act = nullptr;        // [N][2] actions of a policy-2 (SAC actor) sharded rollout
+  hipEvent_t step_ev[4] = {nullptr, nullptr, nullptr, nullptr};   // nascar_set_step_events (profiling)
   // prepare(): capacities of the track table / block map buffers, pinned staging of their stream-ordered uploads
   size_t cap_tracks = 0, cap_blocks = 0;
   void* h_stage = nullptr; size_t stage_bytes = 0;
@@ -2872,6 +2873,8 @@ static int launch_step_range(NascarHandle* h, const Params& P, int nb, const voi
                              uint64_t seed, int64_t step, const float* obs_in, float* obs, float* reward,
                              uint8_t* car_flags, uint8_t* env_flags, int32_t auto_reset, float* terminal_obs,
                              hipStream_t s) {
+  const bool timed = h->step_ev[0] && nb == h->nblocks;   // nascar_set_step_events: whole-grid steps only
+  if (timed) HIPCHK(hipEventRecord(h->step_ev[0], s));
   hipLaunchKernelGGL(model_kernel, dim3(nb), dim3(SBLOCK), MODEL_WALLS_LDS ? h->max_lds : 0, s, P, actions, discrete,
                      terminal_obs != nullptr, policy, seed, step, obs_in);
   HIPCHK(hipGetLastError());
@@ -2879,11 +2882,25 @@ static int launch_step_range(NascarHandle* h, const Params& P, int nb, const voi
     hipLaunchKernelGGL(car_contact_kernel, dim3(nb), dim3(SBLOCK), 0, s, P);
     HIPCHK(hipGetLastError());
   }
+  if (timed) HIPCHK(hipEventRecord(h->step_ev[1], s));
   hipLaunchKernelGGL(logic_kernel, dim3(nb), dim3(SBLOCK), 0, s, P, obs, reward, car_flags,
                      env_flags, auto_reset, terminal_obs);
   HIPCHK(hipGetLastError());
+  if (timed) HIPCHK(hipEventRecord(h->step_ev[2], s));
   launch_sensors_impl(h, P, nb, obs, terminal_obs, auto_reset ? 3 : 1, s, sensor_impl());
   HIPCHK(hipGetLastError());
+  if (timed) HIPCHK(hipEventRecord(h->step_ev[3], s));
+  return 0;
+}
+
+extern "C" int nascar_set_step_events(NascarHandle* h, void* const* events, int32_t n) {
+  if (!h) return fail("null argument");
+  if (n == 0) { for (auto& e : h->step_ev) e = nullptr; return 0; }
+  if (n != 4 || !events) return fail("step events: pass 4 events (or 0 to switch them off), got %d", n);
+  for (int k = 0; k < 4; ++k) {
+    if (!events[k]) return fail("step event %d is null", k);
+    h->step_ev[k] = (hipEvent_t)events[k];
+  }
   return 0;
 }
 

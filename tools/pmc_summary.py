@@ -124,7 +124,7 @@ def main():
     sha = os.path.join(os.path.dirname(os.path.abspath(out)), "prof_source_sha.txt")
     if os.path.exists(sha):
         res["source_sha"] = open(sha).read().strip()
-        res["bench_step_ms_events"] = b["roofline"]["kernel_ms"]
+        res["bench_model_kernel_ms_events"] = b["roofline"]["kernel_ms"]
     f = _find(os.path.join(out, "fetch"), "counter_collection.csv")
     w = _find(os.path.join(out, "write"), "counter_collection.csv")
     if f and w:
@@ -148,7 +148,8 @@ def main():
     json.dump(res, open(os.path.join(prof, f"{tag}_pmc_step.json"), "w"), indent=1)
     if "bytes_per_step" in res and "envs" in res and "source_sha" in res:
         json.dump({k: res[k] for k in ("envs", "cars", "track", "policy", "workload", "source_sha", "bytes_per_step", "bytes_per_step_uncorrected",
-                                       "bytes_per_car_step", "fetch_size_kb", "write_size_kb", "tag")},
+                                       "bytes_per_car_step", "fetch_size_kb", "write_size_kb", "tag",
+                                       "model_kernel_bytes", "logic_kernel_bytes", "ray_sensor_kernel_bytes") if k in res},
                   open(os.path.join(prof, "pmc_traffic.json"), "w"), indent=1)
     print(json.dumps(res, indent=1))
 
