@@ -236,6 +236,85 @@ struct ActorF32 {
   const float* w3;    // [2][256]   mu.weight
   const float* b3;    // [2]
 };
+// ------------------------------------------------------------------ reference-precision actor on the f32 MFMA
+// The float32 actor (SB3 MlpPolicy: ReLU(W2 ReLU(W1 x + b1) + b2), mu = W3 h + b3, tanh, unscale_action) on
+// v_mfma_f32_32x32x2_f32: exact f32 products accumulated as an fmaf chain (bitwise, MI355X_MICROARCH.md
+// "FP32-input MFMA"), so the result is the fp32 kernel's up to summation order.  One wave = 32 observations
+// (batch on the MFMA N dimension, lane r = l & 31 owns observation r, lane half h = l >> 5):
+//   layer 1  H1^T[256 x 32] = W1[256 x 38] . X^T: 8 unit tiles x 19 k-steps; A = W1^T[2s + h][32t + r] (global,
+//            coalesced per half), B = X[row r][2s + h] (global);
+//   layer 2  H2^T = W2 . relu(H1^T + b1): the layer-1 accumulators are the B operands in place -- k-step
+//            (t, q) takes register q of tile t, i.e. hidden unit u = 32t + (q & 3) + 8(q >> 2) + 4h on half h
+//            (the 32x32 C/D map) -- and A = W2^T[u][32t' + r] is read from global (L2-resident, coalesced per
+//            half): 128 k-steps x 8 output tiles;
+//   layer 3  mu_i = W3[i] . relu(H2^T + b2) + b3: per-lane partial sums over the lane's 128 hidden values, the
+//            two lane halves added with a cross-half swap, then tanh / unscale_action in f32.
+// 1024 + 152 MFMAs of 64 cycles per 32 observations: the f32 matrix rate is the f32 vector rate, and
+// the MFMA needs one VGPR per operand where the VALU kernel re-read every activation from LDS.
+#define AM_WAVES 4
+__global__ void __launch_bounds__(64 * AM_WAVES) __attribute__((amdgpu_waves_per_eu(1)))
+actor_mfma32_kernel(int N, const float* __restrict__ obs, float* __restrict__ act, ActorF32 A) {
+  __shared__ float s_b1[ACT_H], s_b2[ACT_H], s_w3[2 * ACT_H];
+  for (int i = threadIdx.x; i < ACT_H; i += 64 * AM_WAVES) { s_b1[i] = A.b1[i]; s_b2[i] = A.b2[i]; }
+  for (int i = threadIdx.x; i < 2 * ACT_H; i += 64 * AM_WAVES) s_w3[i] = A.w3[i];
+  __syncthreads();
+  const int l = threadIdx.x & 63, r = l & 31, h = l >> 5;
+  const int tile = blockIdx.x * AM_WAVES + (threadIdx.x >> 6);
+  const int row0 = tile * 32;
+  if (row0 >= N) return;
+  const int row = row0 + r;
+  const float* xr = obs + (size_t)(row < N ? row : N - 1) * ACT_OBS;
+  f32x16 acc[8];
+#pragma unroll
+  for (int t = 0; t < 8; ++t) acc[t] = (f32x16){};
+  // layer 1
+#pragma unroll
+  for (int s = 0; s < ACT_OBS / 2; ++s) {
+    const float b = xr[2 * s + h];
+    const float* w = A.w1t + (size_t)(2 * s + h) * ACT_H + r;
+#pragma unroll
+    for (int t = 0; t < 8; ++t) acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(w[32 * t], b, acc[t], 0, 0, 0);
+  }
+  f32x16 hid[8];   // relu(H1 + b1) as layer 2's B operands
+#pragma unroll
+  for (int t = 0; t < 8; ++t)
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int u = 32 * t + (q & 3) + 8 * (q >> 2) + 4 * h;
+      hid[t][q] = fmaxf(acc[t][q] + s_b1[u], 0.0f);
+    }
+#pragma unroll
+  for (int t = 0; t < 8; ++t) acc[t] = (f32x16){};
+  // layer 2
+#pragma unroll
+  for (int t = 0; t < 8; ++t)
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int u = 32 * t + (q & 3) + 8 * (q >> 2) + 4 * h;
+      const float* w = A.w2t + (size_t)u * ACT_H + r;
+      const float b = hid[t][q];
+#pragma unroll
+      for (int o = 0; o < 8; ++o) acc[o] = __builtin_amdgcn_mfma_f32_32x32x2f32(w[32 * o], b, acc[o], 0, 0, 0);
+    }
+  // layer 3: partial sums of this lane's half, then the two halves of the observation added
+  float m0 = 0.0f, m1 = 0.0f;
+#pragma unroll
+  for (int t = 0; t < 8; ++t)
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int u = 32 * t + (q & 3) + 8 * (q >> 2) + 4 * h;
+      const float v = fmaxf(acc[t][q] + s_b2[u], 0.0f);
+      m0 = fmaf(s_w3[u], v, m0);
+      m1 = fmaf(s_w3[ACT_H + u], v, m1);
+    }
+  m0 += __shfl_xor(m0, 32);
+  m1 += __shfl_xor(m1, 32);
+  if (h == 0 && row < N) {
+    const float a0 = tanhf(m0 + A.b3[0]), a1 = tanhf(m1 + A.b3[1]);
+    *(f32x2*)&act[2 * (size_t)row] = (f32x2){-1.0f + ((0.5f * (a0 + 1.0f)) * 2.0f), -1.0f + ((0.5f * (a1 + 1.0f)) * 2.0f)};
+  }
+}
+
 #define AF_TILE 32
 __global__ void __launch_bounds__(256) actor_fp32_kernel(int N, const float* __restrict__ obs, float* __restrict__ act,
                                                          ActorF32 A) {

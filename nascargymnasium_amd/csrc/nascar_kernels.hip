@@ -3195,7 +3195,12 @@ extern "C" int nascar_set_actor_precision(NascarHandle* h, int32_t fp32) {
 }
 
 static void launch_actor(NascarHandle* h, int n, const float* obs, float* actions, void* stream) {
-  if (h->actor_fp32) {
+  static const int fp32_valu = getenv("NASCAR_ACTOR_FP32_VALU") != nullptr;   // A/B: the f32 VALU kernel
+  if (h->actor_fp32 && !fp32_valu) {   // reference precision on the f32 MFMA: one wave per 32 observations
+    const int tiles = (n + 31) / 32;
+    hipLaunchKernelGGL(actor_mfma32_kernel, dim3((tiles + AM_WAVES - 1) / AM_WAVES), dim3(64 * AM_WAVES), 0,
+                       (hipStream_t)stream, n, obs, actions, h->actor32);
+  } else if (h->actor_fp32) {
     static int cus = 0;
     if (!cus) { int dev = 0; hipGetDevice(&dev); hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev); if (cus <= 0) cus = 256; }
     const int tiles = (n + AF_TILE - 1) / AF_TILE;
