@@ -60,10 +60,14 @@ __device__ unsigned long long* g_prof = nullptr;
     if (g_prof && (threadIdx.x & 63) == 0) g_prof[LPROF_BASE + ((size_t)blockIdx.x * (SBLOCK / 64) + threadIdx.x / 64) * 16 + (ph)] = _t; } while (0)
 // per-car counters of the Box2D step (model_kernel lane of car c.pid, no atomics): region after logic's
 #define CPROF_BASE (LPROF_BASE + 65536 * 16)
-#define CCOUNT(c, slot, v) do { if (g_prof) g_prof[CPROF_BASE + (size_t)(c).pid * 16 + (slot)] += (unsigned long long)(v); } while (0)
+// per-car slots (CPROF_STRIDE per car): non-returning atomics, so a count does not wait on memory (a read-modify-
+// write here put a dependent global round trip into every counted phase)
+#define CPROF_STRIDE 32
+#define CCOUNT(c, slot, v) do { if (g_prof) (void)atomicAdd(&g_prof[CPROF_BASE + (size_t)(c).pid * CPROF_STRIDE + (slot)], \
+                                                          (unsigned long long)(v)); } while (0)
 #define CTIME_BEGIN() const unsigned long long _ct0 = __builtin_amdgcn_s_memtime()
 // rollout_kernel per-wave phase cycles summed over its steps: region after the per-car counters (N <= 2^20)
-#define RPROF_BASE (CPROF_BASE + (size_t)(1 << 20) * 16)
+#define RPROF_BASE (CPROF_BASE + (size_t)(1 << 19) * CPROF_STRIDE)
 #define RPROF_ADD(slot, v) do { if (g_prof && (threadIdx.x & 63) == 0) \
     g_prof[RPROF_BASE + ((size_t)blockIdx.x * (SBLOCK / 64) + threadIdx.x / 64) * 4 + (slot)] += (v); } while (0)
 #define CTIME_END(c, slot) CCOUNT(c, slot, __builtin_amdgcn_s_memtime() - _ct0)
@@ -1270,7 +1274,13 @@ __device__ __forceinline__ void island_solve_toi_n(Car& c, const LWall* W, const
   VC vc[NMAX];
   cs_init<NMAX>(vc, n, c, cidx, W, false, 1.0f);
   RotCache rcA; rcA.bits = __float_as_uint(c.a) ^ 1u; rcA.q.s = 0.0f; rcA.q.c = 1.0f;   // (empty: no angle matches)
-  for (int it = 0; it < 20; ++it) { if (cs_solve_position<NMAX>(vc, n, A, 1, rcA)) break; }
+  {
+  CTIME_BEGIN();
+  int it = 0;
+  for (; it < 20; ++it) { if (cs_solve_position<NMAX>(vc, n, A, 1, rcA)) break; }
+  CCOUNT(c, 19, it + 1); CCOUNT(c, 18, n);
+  CTIME_END(c, 20);
+  }
   c.c0 = A.c; c.a0 = A.a;
   cs_init_velocity<NMAX>(vc, n, c, A);
   for (int it = 0; it < 6; ++it) cs_solve_velocity<NMAX>(vc, n, A, friction);
@@ -1488,9 +1498,17 @@ __device__ inline void solve_toi(Car& c, const WallSet& S, float dt, float frict
           island_solve_toi(c, W, cidx, n, subdt, friction);
           CTIME_END(c, 11);
           }
+          {
+          CTIME_BEGIN();
           sync_fixtures(c);
           for (int i = 0; i < c.nct; ++i) c.ct[i].flags &= ~(CT_TOI | CT_ISLAND);
+          CTIME_END(c, 17);
+          }
+          {
+          CTIME_BEGIN();
           find_new_contacts(c, S);
+          CTIME_END(c, 16);
+          }
         }
       }
     }

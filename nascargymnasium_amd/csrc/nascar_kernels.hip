@@ -1564,6 +1564,9 @@ __device__ __forceinline__ void model_car(const Params& P, Car& c, int n, const 
 // The env step as two launches: model_kernel (actions -> Car.update_physics -> Box2D step, one lane
 // per car; its TOI code holds it at one wave per SIMD) hands the body / listener state to logic_kernel
 // (banking, disable logic, lap timer, rewards, termination, obs, auto-reset) through the state arrays.
+#ifndef MODEL_CT_PREFETCH
+#define MODEL_CT_PREFETCH 0   // A/B: touch this many of a car's contact records before the staging barrier
+#endif
 #ifndef MODEL_WALLS_LDS
 #define MODEL_WALLS_LDS 1   // model_kernel stages the track's 32-byte wall records in LDS (dynamic shared memory)
 #endif
@@ -1587,6 +1590,17 @@ __global__ void __launch_bounds__(SBLOCK) __attribute__((amdgpu_waves_per_eu(MOD
   // staging's instead of following it: 89 -> 84 us per step)
   if (env >= 0) car_load_phys(P, n, c);
   c.pid = n;
+#if MODEL_CT_PREFETCH
+  // the car's first contact records requested before the staging barrier (they come into L2 while the
+  // segments and walls are staged, instead of at the first dependent access in b2World::Collide)
+  uint32_t ct_touch = 0u;
+  if (env >= 0) {
+    const uint32_t* cw = (const uint32_t*)c.ct;
+#pragma unroll
+    for (int i = 0; i < MODEL_CT_PREFETCH; ++i)
+      if (i < c.nct) ct_touch ^= cw[20 * i] ^ cw[20 * i + 16];
+  }
+#endif
   // actions (BaseEnv._convert_to_internal_action / _discrete_to_continuous, np.float32)
   float tb = 0.0f, st = 0.0f;
   if (env >= 0 && policy >= 0) {
@@ -1609,6 +1623,9 @@ __global__ void __launch_bounds__(SBLOCK) __attribute__((amdgpu_waves_per_eu(MOD
   for (int k = tid; k < T.nwall; k += SBLOCK) s_w[k] = ldg(T.walls + k);
 #endif
   __syncthreads();
+#if MODEL_CT_PREFETCH
+  asm volatile("" :: "v"(ct_touch));
+#endif
   T.segs = s_segs;
 #if MODEL_WALLS_LDS
   T.walls = s_w;
@@ -1908,7 +1925,15 @@ __global__ void __launch_bounds__(SBLOCK) car_contact_kernel(Params P) {
   car_contact_block(P, tid, el, car, env, env >= 0 ? env * C + car : 0);
 }
 
-__global__ void __launch_bounds__(SBLOCK) logic_kernel(Params P, float* obs, float* reward, uint8_t* car_flags,
+#ifndef LOGIC_WPE
+#define LOGIC_WPE 0   // 0: the compiler's choice (182 VGPRs, 2 waves/SIMD)
+#endif
+#if LOGIC_WPE
+#define LOGIC_ATTR __attribute__((amdgpu_waves_per_eu(LOGIC_WPE)))
+#else
+#define LOGIC_ATTR
+#endif
+__global__ void __launch_bounds__(SBLOCK) LOGIC_ATTR logic_kernel(Params P, float* obs, float* reward, uint8_t* car_flags,
                                                       uint8_t* env_flags, int auto_reset, float* terminal_obs) {
   __shared__ LogicLDS L;
   __shared__ TrackLDS TL;

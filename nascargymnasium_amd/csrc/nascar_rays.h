@@ -32,6 +32,15 @@ __host__ __device__ inline bool f32_stable(double xa, double b, float& out) {
 // within 2e-15 of any libm value that is within 1 ulp; the f32 end point is taken from it only when
 // the whole +-bound interval rounds to one float, otherwise (probability ~1e-8 per coordinate) from a
 // direct f64 sincos(sa).  Returns 1 when the fallback was taken.  dx, dy: the f64 direction (cull only).
+// the rare direct evaluation, out of line: inlined, its f64 sincos constants were hoisted out of the sensor
+// kernel's ray loop and spilled to scratch (a reload per ray, 20 B of spill stores per lane)
+__host__ __device__ __attribute__((noinline)) inline void ray_end_direct(double px, double py, double sa, float& fx,
+                                                                         float& fy) {
+  double ey, ex;
+  sincos(sa, &ey, &ex);
+  fx = (float)(px + ex * 250.0);
+  fy = (float)(py + ey * 250.0);
+}
 __host__ __device__ inline int ray_end_f32(double px, double py, double ang, double c0, double s0, int i,
                                            const double (*cs)[2], double& dx, double& dy, float& fx, float& fy) {
   const double k = (double)i * (360.0 / 16) * (3.141592653589793 / 180.0);
@@ -47,9 +56,6 @@ __host__ __device__ inline int ray_end_f32(double px, double py, double ang, dou
   const double bx = 6e-13 + fabs(xa) * 4.5e-16, by = 6e-13 + fabs(ya) * 4.5e-16;
   const bool okx = f32_stable(xa, bx, fx), oky = f32_stable(ya, by, fy);
   if (okx && oky) return 0;
-  double ey, ex;
-  sincos(sa, &ey, &ex);
-  fx = (float)(px + ex * 250.0);
-  fy = (float)(py + ey * 250.0);
+  ray_end_direct(px, py, sa, fx, fy);
   return 1;
 }

@@ -121,7 +121,7 @@ def main():
             st, en = m[:, 14], m[:, 15]
             print(f"    realtime us: last start {(st.max() - st.min()) / 100:.1f}, median end {(np.median(en) - st.min()) / 100:.1f}, "
                   f"last end {(en.max() - st.min()) / 100:.1f}")
-        cp = b[CPROF_BASE:CPROF_BASE + N * 16].reshape(N, 16)
+        cp = b[CPROF_BASE:CPROF_BASE + N * 32].reshape(N, 32)   # CPROF_STRIDE
         if cp[:, 0].any():
             cyc = cp[:, 0]
             print(f"  per-car b2_step cycles: mean {cyc.mean():.0f}, p50 {np.percentile(cyc, 50):.0f}, "
@@ -153,6 +153,19 @@ def main():
             for i in ev:
                 if cp[i, 4]:
                     print("   ", i, cp[i, 0], cp[i, 4], cp[i, 2], cp[i, 1], cp[i, 10], cp[i, 11], cp[i, 12], cp[i, 6])
+            ne = cp[:, 4].sum()
+            if ne:
+                print(f"  per TOI event (all {ne} events): island solve {cp[:, 11].sum() / ne:.0f} cycles (position iterations "
+                      f"{cp[:, 19].sum() / ne:.2f}, {cp[:, 20].sum() / ne:.0f} cycles; island contacts {cp[:, 18].sum() / ne:.2f}), "
+                      f"contact updates {cp[:, 12].sum() / ne:.0f}, sync_fixtures+flags {cp[:, 17].sum() / ne:.0f}, "
+                      f"find_new_contacts {cp[:, 16].sum() / ne:.0f}")
+                per = (128 // a.cars) * a.cars             # cars per workgroup (SBLOCK 128, whole envs)
+                l0 = np.sort(np.concatenate([np.arange(0, N, per), np.arange(64, N, per)]))
+                l0 = l0[l0 < N]                            # lane 0 of each wave
+                w = cp[l0]
+                print(f"  scans per wave: mean {w[:, 14].mean():.2f}, max {w[:, 14].max()}; job-round cycles per scan "
+                      f"{w[:, 13].sum() / max(1, w[:, 14].sum()):.0f}, event-processing cycles per scan "
+                      f"{w[:, 15].sum() / max(1, w[:, 14].sum()):.0f}")
             evw = cp[cp[:, 4] > 0, 0]
             if len(evw):
                 print(f"  b2 cycles of cars with TOI events: mean {evw.mean():.0f}, max {evw.max()}; cars with events {len(evw)}")
