@@ -385,6 +385,9 @@ __device__ inline void add_pair(Car& c, int j) {
 }
 // b2BroadPhase::UpdatePairs + b2ContactManager::AddPair (ascending wall proxy id, prepend)
 __device__ inline void find_new_contacts(Car& c, const WallSet& S) {
+#ifdef NASCAR_KO_FIND
+  c.moved = 0; return;
+#endif
   if (!c.moved) return;
   c.moved = 0;
   const LWall* W = S.W;
@@ -1352,6 +1355,9 @@ __device__ __forceinline__ bool toi_far(const Car& c, const Poly* pa, const LWal
 // b2TimeOfImpact of the car's sweep against static wall wl -> alpha of SolveTOI (1 unless TOUCHING)
 __device__ __forceinline__ float toi_alpha(float4 s0, float4 s1, const LWall& wl, int* iters = nullptr,
                                            unsigned long long* cyc = nullptr) {
+#ifdef NASCAR_KO_TOIJOBS
+  return 1.0f;
+#endif
   Poly pa; make_box(&pa, CAR_HX, CAR_HY);
   Poly pb; make_box(&pb, wl.hx, wl.hy);
   Sweep sA; sA.c0 = V(s0.x, s0.y); sA.c = V(s0.z, s0.w); sA.a0 = s1.x; sA.a = s1.y; sA.alpha0 = s1.z;
@@ -1447,6 +1453,9 @@ __device__ inline void solve_toi(Car& c, const WallSet& S, float dt, float frict
         if (!(ct.flags & CT_ENABLED) || ct.toiCount > MAX_SUBSTEPS || !(ct.flags & CT_TOI)) continue;
         if (ct.toi < minAlpha) { minC = i; minAlpha = ct.toi; }
       }
+#ifdef NASCAR_KO_EVENTS
+      minC = -1;
+#endif
       if (minC < 0 || 1.0f - 10.0f * FLT_EPS < minAlpha) {
         active = false;
       } else {
@@ -1527,14 +1536,21 @@ __device__ inline void b2_step(Car& c, const WallSet& S, float dt, float frictio
   const unsigned long long t0 = __builtin_amdgcn_s_memtime();
   CCOUNT(c, 1, c.nct);
 #endif
+  // NASCAR_KO_*: knockout builds for timing attribution only (a phase skipped: wrong results, never shipped)
+#ifndef NASCAR_KO_COLLIDE
   collide(c, S);
+#endif
   PROFB(11);
+#ifndef NASCAR_KO_SOLVE
   solve(c, S, dt, dtRatio, friction);
+#endif
   PROFB(13);
 #ifdef NASCAR_PROFILE
   const unsigned long long t1 = __builtin_amdgcn_s_memtime();
 #endif
+#ifndef NASCAR_KO_TOI
   solve_toi(c, S, dt, friction);
+#endif
 #ifdef NASCAR_PROFILE
   const unsigned long long t2 = __builtin_amdgcn_s_memtime();
   CCOUNT(c, 0, t2 - t0); (void)t1;

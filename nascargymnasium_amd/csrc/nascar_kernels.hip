@@ -1551,7 +1551,9 @@ __device__ __forceinline__ void model_car(const Params& P, Car& c, int n, const 
   c.thr_in = pymax(0.0, pymin(1.0, (double)a0));
   c.brk_in = pymax(0.0, pymin(1.0, (double)a1));
   c.str_in = pymax(-1.0, pymin(1.0, (double)a2));
+#ifndef NASCAR_KO_UPDATE   // knockout timing builds only (see b2_step)
   car_update_physics(P, c, n, T);
+#endif
   car_store_model(P, n, c);
   asm volatile("" ::: "memory");   // keep the model write-back ahead of the Box2D step (register pressure)
   PROF(3);
@@ -2894,27 +2896,36 @@ extern "C" int nascar_step_driven(NascarHandle* h, int32_t policy, uint64_t seed
 // one env step of step-kernel workgroups [P.blk0, P.blk0 + nb) on stream s:
 // model_kernel -> logic_kernel -> sensor_kernel (pass A for every car, pass B for auto-reset cars)
 // obs_in: the observation the device driver reads (the previous step's); obs: where this step's is written
+// phases: which of the three launches to enqueue (bit 0 model (+ car contact), bit 1 logic, bit 2 sensors), so
+// the sharded rollout can enqueue one phase for every shard before the next phase (see rollout_sharded)
+enum { PH_MODEL = 1, PH_LOGIC = 2, PH_SENSOR = 4, PH_ALL = 7 };
 static int launch_step_range(NascarHandle* h, const Params& P, int nb, const void* actions, int32_t discrete, int policy,
                              uint64_t seed, int64_t step, const float* obs_in, float* obs, float* reward,
                              uint8_t* car_flags, uint8_t* env_flags, int32_t auto_reset, float* terminal_obs,
-                             hipStream_t s) {
+                             hipStream_t s, int phases = PH_ALL) {
   const bool timed = h->step_ev[0] && nb == h->nblocks;   // nascar_set_step_events: whole-grid steps only
-  if (timed) HIPCHK(hipEventRecord(h->step_ev[0], s));
-  hipLaunchKernelGGL(model_kernel, dim3(nb), dim3(SBLOCK), MODEL_WALLS_LDS ? h->max_lds : 0, s, P, actions, discrete,
-                     terminal_obs != nullptr, policy, seed, step, obs_in);
-  HIPCHK(hipGetLastError());
-  if (h->car_contact) {
-    hipLaunchKernelGGL(car_contact_kernel, dim3(nb), dim3(SBLOCK), 0, s, P);
+  if (phases & PH_MODEL) {
+    if (timed) HIPCHK(hipEventRecord(h->step_ev[0], s));
+    hipLaunchKernelGGL(model_kernel, dim3(nb), dim3(SBLOCK), MODEL_WALLS_LDS ? h->max_lds : 0, s, P, actions, discrete,
+                       terminal_obs != nullptr, policy, seed, step, obs_in);
     HIPCHK(hipGetLastError());
+    if (h->car_contact) {
+      hipLaunchKernelGGL(car_contact_kernel, dim3(nb), dim3(SBLOCK), 0, s, P);
+      HIPCHK(hipGetLastError());
+    }
+    if (timed) HIPCHK(hipEventRecord(h->step_ev[1], s));
   }
-  if (timed) HIPCHK(hipEventRecord(h->step_ev[1], s));
-  hipLaunchKernelGGL(logic_kernel, dim3(nb), dim3(SBLOCK), 0, s, P, obs, reward, car_flags,
-                     env_flags, auto_reset, terminal_obs);
-  HIPCHK(hipGetLastError());
-  if (timed) HIPCHK(hipEventRecord(h->step_ev[2], s));
-  launch_sensors_impl(h, P, nb, obs, terminal_obs, auto_reset ? 3 : 1, s, sensor_impl());
-  HIPCHK(hipGetLastError());
-  if (timed) HIPCHK(hipEventRecord(h->step_ev[3], s));
+  if (phases & PH_LOGIC) {
+    hipLaunchKernelGGL(logic_kernel, dim3(nb), dim3(SBLOCK), 0, s, P, obs, reward, car_flags,
+                       env_flags, auto_reset, terminal_obs);
+    HIPCHK(hipGetLastError());
+    if (timed) HIPCHK(hipEventRecord(h->step_ev[2], s));
+  }
+  if (phases & PH_SENSOR) {
+    launch_sensors_impl(h, P, nb, obs, terminal_obs, auto_reset ? 3 : 1, s, sensor_impl());
+    HIPCHK(hipGetLastError());
+    if (timed) HIPCHK(hipEventRecord(h->step_ev[3], s));
+  }
   return 0;
 }
 
@@ -2993,21 +3004,26 @@ static int rollout_sharded(NascarHandle* h, int S, int32_t policy, uint64_t seed
       const size_t ko = traj ? (size_t)k : 0;
       float* o_in = obs_traj ? obs + (size_t)k * NC * 38 : obs;
       float* o_out = obs_traj ? obs + (size_t)(k + 1) * NC * 38 : obs;
-      for (int s = 0; s < S; ++s) {
-        const int b0 = (int)((int64_t)h->nblocks * s / S), b1 = (int)((int64_t)h->nblocks * (s + 1) / S);
-        Params P = P0;
-        P.blk0 = b0;
-        if (actor) {
-          const size_t c0 = S == 1 ? 0 : (size_t)b0 * h->epb * h->C;
-          const size_t c1 = S == 1 ? NC : std::min((size_t)b1 * h->epb, E) * h->C;
-          if (c1 > c0) launch_actor(h, (int)(c1 - c0), o_in + c0 * 38, h->d_ro_act + c0 * 2, shard_stream(s));
-          HIPCHK(hipGetLastError());
+      // phase-major enqueue (every shard's model launch, then every shard's logic, then sensors): each stream's
+      // order is unchanged, but a shard's first launch of the call is queued ~6 us (one launch) after the previous
+      // shard's instead of ~18 us (three), so the shards start together
+      for (int ph = 0; ph < 3; ++ph) {
+        for (int s = 0; s < S; ++s) {
+          const int b0 = (int)((int64_t)h->nblocks * s / S), b1 = (int)((int64_t)h->nblocks * (s + 1) / S);
+          Params P = P0;
+          P.blk0 = b0;
+          if (actor && ph == 0) {
+            const size_t c0 = S == 1 ? 0 : (size_t)b0 * h->epb * h->C;
+            const size_t c1 = S == 1 ? NC : std::min((size_t)b1 * h->epb, E) * h->C;
+            if (c1 > c0) launch_actor(h, (int)(c1 - c0), o_in + c0 * 38, h->d_ro_act + c0 * 2, shard_stream(s));
+            HIPCHK(hipGetLastError());
+          }
+          if (launch_step_range(h, P, b1 - b0, actor ? h->d_ro_act : nullptr, 0, actor ? -1 : policy, seed, step0 + k,
+                                o_in, o_out, reward + ko * NC,
+                                car_flags ? car_flags + ko * NC : nullptr, env_flags ? env_flags + ko * E : nullptr,
+                                auto_reset, nullptr, shard_stream(s), 1 << ph))
+            return -1;
         }
-        if (launch_step_range(h, P, b1 - b0, actor ? h->d_ro_act : nullptr, 0, actor ? -1 : policy, seed, step0 + k,
-                              o_in, o_out, reward + ko * NC,
-                              car_flags ? car_flags + ko * NC : nullptr, env_flags ? env_flags + ko * E : nullptr,
-                              auto_reset, nullptr, shard_stream(s)))
-          return -1;
       }
     }
     return 0;
