@@ -1168,16 +1168,20 @@ __device__ __forceinline__ float wall_cast(const float4 wa, const float4 wb, V2 
   const float hx = wa.w, hy = wb.z;
   if (perp > hx * fabsf(q.c * dy - q.s * dx) + hy * fabsf(q.s * dy + q.c * dx) + 0.02f) return bi;
   const V2 l1 = rmulT(q, V(p1.x - wa.x, p1.y - wa.y));
-  const float n0 = 0.0f * ((-hx) - l1.x) + (-1.0f) * ((-hy) - l1.y);
-  const float n1 = 1.0f * (hx - l1.x) + 0.0f * ((-hy) - l1.y);
-  const float n2 = 0.0f * (hx - l1.x) + 1.0f * (hy - l1.y);
-  const float n3 = (-1.0f) * ((-hx) - l1.x) + 0.0f * (hy - l1.y);
+  // Box2D's num_f = dot(normal_f, vertex_f - l1) and den_f = dot(normal_f, d) with the box normals (0, -1), (1, 0),
+  // (0, 1), (-1, 0): the products by 0 and +-1 are dropped.  The values are the same floats except possibly the sign
+  // of a zero (0 * x + (-y) vs -y), and a zero's sign never reaches the result: den is only compared (== < > 0, a
+  // zero den selects the parallel case), and a zero num can neither lower `lower` (0 < lower * den <= 0 is false
+  // for den < 0) nor reach the returned fraction through `upper` (only compared)
+  const float n0 = l1.y - (-hy);
+  const float n1 = hx - l1.x;
+  const float n2 = hy - l1.y;
+  const float n3 = l1.x - (-hx);
   const V2 l2 = rmulT(q, V(p2x - wa.x, p2y - wa.y));
   const V2 dd = vsub(l2, l1);
   float lower = 0.0f, upper = 1.0f; int index = -1; bool ok = true;
   const float num[4] = {n0, n1, n2, n3};
-  const float den[4] = {0.0f * dd.x + (-1.0f) * dd.y, 1.0f * dd.x + 0.0f * dd.y, 0.0f * dd.x + 1.0f * dd.y,
-                        (-1.0f) * dd.x + 0.0f * dd.y};
+  const float den[4] = {-dd.y, dd.x, dd.y, -dd.x};
 #if WALL_CAST_SELECT
   // the same face loop as selects (no divergent branches): every face's quotient is computed and applied only
   // where the branchy loop would have assigned it; a face after the loop's break (ok false) changes nothing
