@@ -277,7 +277,9 @@ struct WallSet {
   const LWall* W; int nw;
   WallGrid bp, sn;
   const float4* fat;      // [nw] broadphase fat AABB (lo.x, lo.y, hi.x, hi.y)
+  DContact* ct_all = nullptr;   // the global contact records ([N][MAXC]) when a car's may be held in LDS (model_kernel)
 };
+
 // list of the cell containing (x, y), or false when outside the grid
 __device__ __forceinline__ bool grid_list(const WallGrid& g, float x, float y, int& beg, int& end) {
   if (!g.start) return false;
@@ -295,7 +297,7 @@ struct Car {
   V2 force; float torque; V2 c0; float a0; float alpha0;
   Aabb fat; int moved; float invdt0;
   int nct, overflow;
-  int pid;            // car index (profile builds' per-car counters only)
+  int pid;            // car index (its global contact records when they are moved out of LDS; profile counters)
   // Car / TyreManager (float64 like the reference's Python)
   double thr_in, brk_in, str_in, thr, brk, steer;
   double rpm, pvx, pvy, lfm, slip, bank;
@@ -311,11 +313,36 @@ struct Car {
   double cum_impact, stuck_dur, stuck_sx, stuck_sy, prev_px, prev_py, prog_hist, back, prev_back, imp_at_obs;
   float cum_reward, cum_reward_info;
   // per-car global views (AoS lists)
-  DContact* ct;       // [MAXC]
+  DContact* ct;       // [MAXC] (global, or model_kernel's LDS slots)
+  int ct_hw;          // LDS slots: records written this step (live or dead), all copied back to the global ones
   int* act_key;       // [MAXC]
   float* act_n;       // [MAXC][2]
   double* acc;        // [20] ring (long, lat)
 };
+
+// A car's contact records may live in LDS for the Box2D step (model_kernel, CT_LDS_CAP records per lane): every
+// b2Contact access is then an LDS round trip instead of a global one.  A car whose list grows past the LDS slots
+// moves its records back to its global ones first (same records, same order), and model_car writes LDS records
+// back after the step.
+#ifndef CT_LDS_CAP
+#define CT_LDS_CAP 3
+#endif
+__device__ __forceinline__ bool ct_in_lds(const Car& c) {
+  return __builtin_amdgcn_is_shared((const __attribute__((address_space(0))) void*)c.ct);
+}
+// before a contact is prepended: room for one more record where the list lives
+// (the dead records past nct are copied too, so the global image is the one the all-global path leaves)
+__device__ __forceinline__ void ct_make_room(Car& c, const WallSet& S) {
+  if (S.ct_all && ct_in_lds(c)) {
+    if (c.nct >= CT_LDS_CAP) {
+      DContact* g = S.ct_all + (size_t)c.pid * MAXC;
+      for (int i = 0; i < c.nct; ++i) g[i] = c.ct[i];
+      c.ct = g;
+    } else {
+      c.ct_hw = max(c.ct_hw, c.nct + 1);
+    }
+  }
+}
 
 // ------------------------------------------------------------------ listener (src/car_physics.py:693-864)
 __device__ inline void lis_begin(Car& c, int key, V2 n) {
@@ -368,11 +395,12 @@ __device__ __forceinline__ void sync_fixtures(Car& c) {
 }
 
 // b2ContactManager::AddPair for wall j whose fat AABB overlaps the car's (new contacts are prepended)
-__device__ inline void add_pair(Car& c, int j) {
+__device__ inline void add_pair(Car& c, const WallSet& S, int j) {
     bool exists = false;
     for (int i = 0; i < c.nct; ++i) if (c.ct[i].wall == j) { exists = true; break; }
     if (exists) return;
     if (c.nct >= MAXC) { c.overflow = 1; return; }
+    ct_make_room(c, S);
     for (int i = c.nct; i > 0; --i) c.ct[i] = c.ct[i - 1];
     DContact z;
     z.wall = j; z.flags = CT_ENABLED; z.mtype = 0; z.pointCount = 0;
@@ -412,7 +440,7 @@ __device__ inline void find_new_contacts(Car& c, const WallSet& S) {
       for (int u = 0; u < BP_BATCH; ++u) {
         if (k + u >= end) break;
         Aabb a; a.lo = V(b[u].x, b[u].y); a.hi = V(b[u].z, b[u].w);
-        if (overlap(c.fat, a)) add_pair(c, (int)ldg(list + k + u));
+        if (overlap(c.fat, a)) add_pair(c, S, (int)ldg(list + k + u));
       }
     }
     return;
@@ -425,6 +453,7 @@ __device__ inline void find_new_contacts(Car& c, const WallSet& S) {
     for (int i = 0; i < c.nct; ++i) if (c.ct[i].wall == j) { exists = true; break; }
     if (exists) continue;
     if (c.nct >= MAXC) { c.overflow = 1; continue; }
+    ct_make_room(c, S);
     for (int i = c.nct; i > 0; --i) c.ct[i] = c.ct[i - 1];
     DContact z;
     z.wall = j; z.flags = CT_ENABLED; z.mtype = 0; z.pointCount = 0;
@@ -602,7 +631,7 @@ __device__ inline void contact_update(Car& c, int ci, const LWall* W) {
 // Per-car Box2D work whose size varies by car (a car's TOI pairs) is listed per lane and computed by every
 // present lane of the wave, so a wave's time follows its total work rather than its busiest car.  (The same
 // scheme for b2World::Collide's manifolds was parity-green but measured neutral: 118.5 vs 118.8 us.)
-#define TOI_JOBCAP 128    // b2TimeOfImpact pairs per compute round per wave (more pairs: further rounds)
+#define TOI_JOBCAP 64     // b2TimeOfImpact pairs per compute round per wave (more pairs: further rounds)
 struct ToiWaveLDS { float4 sw0[64], sw1[64]; int2 job[TOI_JOBCAP]; float res[TOI_JOBCAP]; };
 union WaveLDS { ToiWaveLDS toi; };
 __shared__ WaveLDS g_wave_lds[SBLOCK / 64];   // model_kernel / rollout_kernel (the Box2D step)
@@ -984,8 +1013,17 @@ __device__ inline void solve(Car& c, const WallSet& S, float dt, float dtRatio, 
     }
   }
   PROFB(12);
+  {
+  CTIME_BEGIN();
   sync_fixtures(c);
+  CTIME_END(c, 22);
+  }
+  {
+  CTIME_BEGIN();
+  if (c.moved) CCOUNT(c, 24, 1);
   find_new_contacts(c, S);
+  CTIME_END(c, 21);
+  }
 }
 
 // ------------------------------------------------------------------ GJK / TOI
@@ -1487,6 +1525,9 @@ __device__ inline void solve_toi(Car& c, const WallSet& S, float dt, float frict
           {
           CTIME_BEGIN();
           for (int i = 0; i < c.nct; ++i) {
+#ifdef NASCAR_KO_EV_CU
+            break;
+#endif
             if (n == MAX_TOI_CONTACTS) break;
             if (n == MAX_ISLAND) {   // more touching contacts than the island buffer: flag, keep going exactly-as-far-as-possible
               if (!(c.ct[i].flags & CT_ISLAND)) { c.overflow = 2; }
@@ -1504,7 +1545,9 @@ __device__ inline void solve_toi(Car& c, const WallSet& S, float dt, float frict
           float subdt = (1.0f - minAlpha) * dt;
           {
           CTIME_BEGIN();
+#ifndef NASCAR_KO_EV_ISLAND
           island_solve_toi(c, W, cidx, n, subdt, friction);
+#endif
           CTIME_END(c, 11);
           }
           {
@@ -1515,7 +1558,9 @@ __device__ inline void solve_toi(Car& c, const WallSet& S, float dt, float frict
           }
           {
           CTIME_BEGIN();
+#ifndef NASCAR_KO_EV_FIND
           find_new_contacts(c, S);
+#endif
           CTIME_END(c, 16);
           }
         }
@@ -1538,7 +1583,11 @@ __device__ inline void b2_step(Car& c, const WallSet& S, float dt, float frictio
 #endif
   // NASCAR_KO_*: knockout builds for timing attribution only (a phase skipped: wrong results, never shipped)
 #ifndef NASCAR_KO_COLLIDE
+  {
+  CTIME_BEGIN();
   collide(c, S);
+  CTIME_END(c, 23);
+  }
 #endif
   PROFB(11);
 #ifndef NASCAR_KO_SOLVE

@@ -1569,7 +1569,7 @@ __global__ void policy_kernel(int N, int policy, uint64_t seed, int64_t step, co
 // src/car_physics.py:341-384): BaseEnv._convert_to_internal_action of (tb, st), Car.update_physics, the
 // Box2D step; writes the model / body state back and the sensor pass-A pose.
 __device__ __forceinline__ void model_car(const Params& P, Car& c, int n, const TrackDev& T, float tb, float st, int want_term) {
-  const WallSet S{T.walls, T.nwall, T.bp, T.sn, T.wfat};
+  const WallSet S{T.walls, T.nwall, T.bp, T.sn, T.wfat, P.ct};
   float a0, a1, a2 = st;
   if (tb >= 0) { a0 = tb; a1 = 0.0f; } else { a0 = 0.0f; a1 = -tb; }
   if (c.disabled) { a0 = 0.0f; a1 = 0.0f; a2 = 0.0f; }
@@ -1584,6 +1584,10 @@ __device__ __forceinline__ void model_car(const Params& P, Car& c, int n, const 
   PROF(3);
   b2_step(c, S, P.dt_f, P.friction);
   PROF(4);
+  if (ct_in_lds(c)) {   // model_kernel's LDS records back to the car's global ones (live and dead, see ct_make_room)
+    DContact* g = P.ct + (size_t)n * MAXC;
+    for (int i = 0; i < c.ct_hw; ++i) g[i] = c.ct[i];
+  }
   car_store_body(P, n, c);
   set_pose(P, n, c, PM_A_OBS | (want_term ? PM_A_TERM : 0));   // sensor pass A
 }
@@ -1591,11 +1595,12 @@ __device__ __forceinline__ void model_car(const Params& P, Car& c, int n, const 
 // The env step as two launches: model_kernel (actions -> Car.update_physics -> Box2D step, one lane
 // per car; its TOI code holds it at one wave per SIMD) hands the body / listener state to logic_kernel
 // (banking, disable logic, lap timer, rewards, termination, obs, auto-reset) through the state arrays.
-#ifndef MODEL_CT_PREFETCH
-#define MODEL_CT_PREFETCH 0   // A/B: touch this many of a car's contact records before the staging barrier
+#ifndef MODEL_CT_LDS
+#define MODEL_CT_LDS 1      // model_kernel holds cars' contact records in LDS (CT_LDS_CAP per lane, dynamic shared memory)
 #endif
+#define MODEL_CT_LDS_BYTES (MODEL_CT_LDS ? (size_t)SBLOCK * CT_LDS_CAP * sizeof(DContact) : (size_t)0)
 #ifndef MODEL_WALLS_LDS
-#define MODEL_WALLS_LDS 1   // model_kernel stages the track's 32-byte wall records in LDS (dynamic shared memory)
+#define MODEL_WALLS_LDS 0   // model_kernel stages the track's 32-byte wall records in LDS (after the contact slots)
 #endif
 #ifndef MODEL_WPE
 #define MODEL_WPE 2   // 256 VGPRs + 40 spilled (vs 256 + 44 AGPRs at 1 wave/SIMD): 103.6 -> 100.6 us/step
@@ -1617,15 +1622,14 @@ __global__ void __launch_bounds__(SBLOCK) __attribute__((amdgpu_waves_per_eu(MOD
   // staging's instead of following it: 89 -> 84 us per step)
   if (env >= 0) car_load_phys(P, n, c);
   c.pid = n;
-#if MODEL_CT_PREFETCH
-  // the car's first contact records requested before the staging barrier (they come into L2 while the
-  // segments and walls are staged, instead of at the first dependent access in b2World::Collide)
-  uint32_t ct_touch = 0u;
-  if (env >= 0) {
-    const uint32_t* cw = (const uint32_t*)c.ct;
-#pragma unroll
-    for (int i = 0; i < MODEL_CT_PREFETCH; ++i)
-      if (i < c.nct) ct_touch ^= cw[20 * i] ^ cw[20 * i + 16];
+#if MODEL_CT_LDS
+  // the car's contact records into its LDS slots (lists of up to CT_LDS_CAP; longer ones stay global): the
+  // loads are issued before the staging barrier, and every b2Contact access of the step is then an LDS one
+  if (env >= 0 && c.nct <= CT_LDS_CAP) {
+    DContact* s_ct = (DContact*)smem + (size_t)tid * CT_LDS_CAP;
+    for (int i = 0; i < c.nct; ++i) s_ct[i] = c.ct[i];
+    c.ct = s_ct;
+    c.ct_hw = c.nct;
   }
 #endif
   // actions (BaseEnv._convert_to_internal_action / _discrete_to_continuous, np.float32)
@@ -1646,13 +1650,10 @@ __global__ void __launch_bounds__(SBLOCK) __attribute__((amdgpu_waves_per_eu(MOD
 #if MODEL_WALLS_LDS
   // the track's wall table in LDS: every contact update, TOI pair, island and listener lookup of the Box2D step
   // reads it (one staging per workgroup instead of a dependent L2 round trip per access)
-  LWall* s_w = (LWall*)smem;
+  LWall* s_w = (LWall*)(smem + MODEL_CT_LDS_BYTES);
   for (int k = tid; k < T.nwall; k += SBLOCK) s_w[k] = ldg(T.walls + k);
 #endif
   __syncthreads();
-#if MODEL_CT_PREFETCH
-  asm volatile("" :: "v"(ct_touch));
-#endif
   T.segs = s_segs;
 #if MODEL_WALLS_LDS
   T.walls = s_w;
@@ -2931,7 +2932,7 @@ static int launch_step_range(NascarHandle* h, const Params& P, int nb, const voi
   const bool timed = h->step_ev[0] && nb == h->nblocks;   // nascar_set_step_events: whole-grid steps only
   if (phases & PH_MODEL) {
     if (timed) HIPCHK(hipEventRecord(h->step_ev[0], s));
-    hipLaunchKernelGGL(model_kernel, dim3(nb), dim3(SBLOCK), MODEL_WALLS_LDS ? h->max_lds : 0, s, P, actions, discrete,
+    hipLaunchKernelGGL(model_kernel, dim3(nb), dim3(SBLOCK), MODEL_CT_LDS_BYTES + (MODEL_WALLS_LDS ? h->max_lds : 0), s, P, actions, discrete,
                        terminal_obs != nullptr, policy, seed, step, obs_in);
     HIPCHK(hipGetLastError());
     if (h->car_contact) {
