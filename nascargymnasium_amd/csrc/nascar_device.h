@@ -603,7 +603,7 @@ __device__ inline void contact_update(Car& c, int ci, const LWall* W) {
   ct.flags |= CT_ENABLED;
   bool was = (ct.flags & CT_TOUCH) != 0;
   Poly pa, pb; make_box(&pa, CAR_HX, CAR_HY);
-  const LWall& wl = W[ct.wall];
+  const LWall wl = ldg(W + ct.wall);   // the wall table is global (ldg: global, not flat, loads)
   make_box(&pb, wl.hx, wl.hy);
   Xf xfB = wall_xf(wl);
   collide_polygons(ct, &pa, c.xf, &pb, xfB);
@@ -656,7 +656,7 @@ __device__ inline void collide(Car& c, const WallSet& S) {
     if (!overlap(c.fat, fat_box(ldg(S.fat + wall)))) {
       bool touching = (c.ct[i].flags & CT_TOUCH) != 0;
       remove_contact(c, i);
-      if (touching) lis_end(c, W[wall].key);
+      if (touching) lis_end(c, ldg(&W[wall].key));
       continue;
     }
     contact_update(c, i, W);
@@ -695,7 +695,7 @@ template <int NMAX> __device__ __forceinline__ void cs_init(VC* vc, int n, const
     VC& v = vc[i];
     v.ci = cidx[i];
     v.pointCount = ct.pointCount;
-    const LWall& wl = W[ct.wall];
+    const LWall wl = ldg(W + ct.wall);
     v.cB = V(wl.px, wl.py); v.aB = wl.ang; v.vB = zero2(); v.wB = 0.0f;
     v.qB.s = wl.qs; v.qB.c = wl.qc; v.aB0 = __float_as_uint(wl.ang);
     v.ln = V(ct.lnx, ct.lny); v.lp = V(ct.lpx, ct.lpy); v.pcount = ct.pointCount; v.type = ct.mtype;
@@ -1423,7 +1423,7 @@ __device__ inline void solve_toi(Car& c, const WallSet& S, float dt, float frict
       for (int i = 0; i < c.nct; ++i) {
         DContact& ct = c.ct[i];
         if (!(ct.flags & CT_ENABLED) || ct.toiCount > MAX_SUBSTEPS || (ct.flags & CT_TOI)) continue;
-        if (toi_far(c, &pa, W[ct.wall])) {
+        if (toi_far(c, &pa, ldg(W + ct.wall))) {
           PCOUNT(13, 1); CCOUNT(c, 3, 1);
           ct.toi = 1.0f; ct.flags |= CT_TOI;
           continue;
@@ -1462,10 +1462,10 @@ __device__ inline void solve_toi(Car& c, const WallSet& S, float dt, float frict
         PCOUNT(12, 1); CCOUNT(c, 2, 1);
 #ifdef NASCAR_PROFILE   // per computing lane: TOI outer / root-finder iterations, GJK and separation-function cycles
         int it2[2] = {0, 0}; unsigned long long cy2[2] = {0ull, 0ull};
-        L.res[j] = toi_alpha(L.sw0[owner], L.sw1[owner], W[jb.y], it2, cy2);
+        L.res[j] = toi_alpha(L.sw0[owner], L.sw1[owner], ldg(W + jb.y), it2, cy2);
         CCOUNT(c, 6, it2[0]); CCOUNT(c, 7, it2[1]); CCOUNT(c, 9, cy2[0]); CCOUNT(c, 10, cy2[1]);
 #else
-        L.res[j] = toi_alpha(L.sw0[owner], L.sw1[owner], W[jb.y]);
+        L.res[j] = toi_alpha(L.sw0[owner], L.sw1[owner], ldg(W + jb.y));
 #endif
       }
       wave_lds_sync();

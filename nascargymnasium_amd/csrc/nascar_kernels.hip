@@ -86,7 +86,7 @@ __device__ __forceinline__ BeamHead beam_head(const BeamGrid& G, int li) {
   for (int k = 0; k < BEAM_HW; ++k) h.w[k] = ldg(G.head + (size_t)li * BEAM_HW + k);
   return h;
 }
-#define MODEL_WALL_LDS_MAX ((size_t)1024 * sizeof(LWall))   // walls per track model_kernel's LDS table holds
+#define WALL_LDS_MAX ((size_t)1024 * sizeof(LWall))   // walls per track the sensor kernels' LDS wall image holds (32 B each)
 struct TrackDev {
   LWall* walls; int nwall;
   const float4* wfat;  // [nwall] broadphase fat AABBs
@@ -788,8 +788,8 @@ __device__ inline bool query_on_wall(const WallSet& S, double px, double py, dou
   else { beg = 0; end = S.nw; }
   for (int kk = beg; kk < end; ++kk) {
     const int jw = list ? (int)ldg(list + kk) : kk;
-    const LWall& wl = W[jw];
     if (!overlap(fat_box(ldg(S.fat + jw)), q)) continue;
+    const LWall wl = ldg(W + jw);
     Xf xf = wall_xf(wl);
     Poly p; make_box(&p, wl.hx, wl.hy);
     V2 pl = rmulT(xf.q, vsub(center, xf.p));
@@ -1599,9 +1599,6 @@ __device__ __forceinline__ void model_car(const Params& P, Car& c, int n, const 
 #define MODEL_CT_LDS 1      // model_kernel holds cars' contact records in LDS (CT_LDS_CAP per lane, dynamic shared memory)
 #endif
 #define MODEL_CT_LDS_BYTES (MODEL_CT_LDS ? (size_t)SBLOCK * CT_LDS_CAP * sizeof(DContact) : (size_t)0)
-#ifndef MODEL_WALLS_LDS
-#define MODEL_WALLS_LDS 0   // model_kernel stages the track's 32-byte wall records in LDS (after the contact slots)
-#endif
 #ifndef MODEL_WPE
 #define MODEL_WPE 2   // 256 VGPRs + 40 spilled (vs 256 + 44 AGPRs at 1 wave/SIMD): 103.6 -> 100.6 us/step
 #endif
@@ -1647,17 +1644,8 @@ __global__ void __launch_bounds__(SBLOCK) __attribute__((amdgpu_waves_per_eu(MOD
   }
   TrackDev T = P.tracks[blk_track_of(P, (blockIdx.x + P.blk0))];
   if (tid < T.nseg) s_segs[tid] = ldg(T.segs + tid);
-#if MODEL_WALLS_LDS
-  // the track's wall table in LDS: every contact update, TOI pair, island and listener lookup of the Box2D step
-  // reads it (one staging per workgroup instead of a dependent L2 round trip per access)
-  LWall* s_w = (LWall*)(smem + MODEL_CT_LDS_BYTES);
-  for (int k = tid; k < T.nwall; k += SBLOCK) s_w[k] = ldg(T.walls + k);
-#endif
   __syncthreads();
-  T.segs = s_segs;
-#if MODEL_WALLS_LDS
-  T.walls = s_w;
-#endif
+  T.segs = s_segs;   // (the wall table stays global: staged in LDS it measured neutral, and the LDS holds the contacts)
   PROF(1);
   if (env < 0) return;
   PROF(2);
@@ -2680,8 +2668,8 @@ static int build_track(HostTrack& t, size_t& lds_out, const double* segments, in
     t.walls.push_back(L);
   }
   size_t lds = sizeof(LWall) * t.walls.size();
-  if (lds > MODEL_WALL_LDS_MAX) return fail("track has %d walls; model_kernel's LDS wall table holds %zu", nwall,
-                                            (size_t)(MODEL_WALL_LDS_MAX / sizeof(LWall)));
+  if (lds > WALL_LDS_MAX) return fail("track has %d walls; the sensor kernels' LDS wall image holds %zu", nwall,
+                                      (size_t)(WALL_LDS_MAX / sizeof(LWall)));
   {
     std::vector<LWall> dw(t.walls.begin(), t.walls.end());
     std::vector<float4> fat(t.walls.size());
@@ -2932,7 +2920,7 @@ static int launch_step_range(NascarHandle* h, const Params& P, int nb, const voi
   const bool timed = h->step_ev[0] && nb == h->nblocks;   // nascar_set_step_events: whole-grid steps only
   if (phases & PH_MODEL) {
     if (timed) HIPCHK(hipEventRecord(h->step_ev[0], s));
-    hipLaunchKernelGGL(model_kernel, dim3(nb), dim3(SBLOCK), MODEL_CT_LDS_BYTES + (MODEL_WALLS_LDS ? h->max_lds : 0), s, P, actions, discrete,
+    hipLaunchKernelGGL(model_kernel, dim3(nb), dim3(SBLOCK), MODEL_CT_LDS_BYTES, s, P, actions, discrete,
                        terminal_obs != nullptr, policy, seed, step, obs_in);
     HIPCHK(hipGetLastError());
     if (h->car_contact) {
