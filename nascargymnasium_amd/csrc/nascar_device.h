@@ -325,7 +325,7 @@ struct Car {
 // moves its records back to its global ones first (same records, same order), and model_car writes LDS records
 // back after the step.
 #ifndef CT_LDS_CAP
-#define CT_LDS_CAP 3
+#define CT_LDS_CAP 4   // 2 / 3 / 4 / 5 / 6 slots: 161 / 156 / 153 / 154 / 155 us/step sharded (5+: 2 workgroups per CU)
 #endif
 __device__ __forceinline__ bool ct_in_lds(const Car& c) {
   return __builtin_amdgcn_is_shared((const __attribute__((address_space(0))) void*)c.ct);
