@@ -1598,7 +1598,9 @@ __device__ __forceinline__ void model_car(const Params& P, Car& c, int n, const 
 #ifndef MODEL_CT_LDS
 #define MODEL_CT_LDS 1      // model_kernel holds cars' contact records in LDS (CT_LDS_CAP per lane, dynamic shared memory)
 #endif
-#define MODEL_CT_LDS_BYTES (MODEL_CT_LDS ? (size_t)SBLOCK * CT_LDS_CAP * sizeof(DContact) : (size_t)0)
+// a lane's slots padded to an odd number of 16-byte units, so the lanes' same-record accesses spread over the banks
+#define CT_LDS_STRIDE ((CT_LDS_CAP * sizeof(DContact) / 16) % 2 ? CT_LDS_CAP * sizeof(DContact) : CT_LDS_CAP * sizeof(DContact) + 16)
+#define MODEL_CT_LDS_BYTES (MODEL_CT_LDS ? (size_t)SBLOCK * CT_LDS_STRIDE : (size_t)0)
 #ifndef MODEL_WPE
 #define MODEL_WPE 2   // 256 VGPRs + 40 spilled (vs 256 + 44 AGPRs at 1 wave/SIMD): 103.6 -> 100.6 us/step
 #endif
@@ -1623,7 +1625,7 @@ __global__ void __launch_bounds__(SBLOCK) __attribute__((amdgpu_waves_per_eu(MOD
   // the car's contact records into its LDS slots (lists of up to CT_LDS_CAP; longer ones stay global): the
   // loads are issued before the staging barrier, and every b2Contact access of the step is then an LDS one
   if (env >= 0 && c.nct <= CT_LDS_CAP) {
-    DContact* s_ct = (DContact*)smem + (size_t)tid * CT_LDS_CAP;
+    DContact* s_ct = (DContact*)(smem + (size_t)tid * CT_LDS_STRIDE);
     for (int i = 0; i < c.nct; ++i) s_ct[i] = c.ct[i];
     c.ct = s_ct;
     c.ct_hw = c.nct;
