@@ -166,6 +166,11 @@ def main():
                 print(f"  scans per wave: mean {w[:, 14].mean():.2f}, max {w[:, 14].max()}; job-round cycles per scan "
                       f"{w[:, 13].sum() / max(1, w[:, 14].sum()):.0f}, event-processing cycles per scan "
                       f"{w[:, 15].sum() / max(1, w[:, 14].sum()):.0f}")
+            nc = cp[:, 1]
+            print(f"  per car (mean over cars): collide {cp[:, 23].mean():.0f} cycles (cars with contacts: "
+                  f"{cp[nc > 0, 23].mean() if (nc > 0).any() else 0:.0f}), sync_fixtures {cp[:, 22].mean():.0f}, "
+                  f"find_new_contacts {cp[:, 21].mean():.0f} (moved cars {cp[:, 24].mean():.3f}; per moved car "
+                  f"{cp[cp[:, 24] > 0, 21].mean() if (cp[:, 24] > 0).any() else 0:.0f}, p99 {np.percentile(cp[:, 21], 99):.0f})")
             evw = cp[cp[:, 4] > 0, 0]
             if len(evw):
                 print(f"  b2 cycles of cars with TOI events: mean {evw.mean():.0f}, max {evw.max()}; cars with events {len(evw)}")
