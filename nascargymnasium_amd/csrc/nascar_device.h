@@ -1364,6 +1364,43 @@ __device__ __forceinline__ float toi_gap_bound(V2 u, V2 d, V2 dc, V2 cx, V2 cy, 
   const float away = s >= 0.0f ? vdot(u, dc) : -vdot(u, dc);   // motion toward +gap during the sweep
   return gap - fmaxb(0.0f, away);
 }
+// Second-order rotation bound (round 3), tried when the bound above fails.  Along a fixed axis u (oriented wall ->
+// car at the end pose), car vertex k's gap g_k(beta) = u . c(beta) + r cos(a(beta) + psi_k) - (wall terms) is a
+// linear function plus a sinusoid of the linear angle a(beta) = a0 + beta (a - a0), so |g_k''| <= r (a - a0)^2 with
+// r = R_car, and g_k(beta) >= min(g_k(0), g_k(1)) - r (a - a0)^2 / 8 on [0, 1].  The box gap is the minimum over
+// the vertices, hence
+//   gap_u(beta) >= min(G_u(start pose), G_u(end pose)) - R_car (a - a0)^2 / 8,
+// G_u the separating-axis gap of the two boxes at that pose measured along the end pose's orientation of u.  The
+// first-order term |a - a0| R_car above is what keeps a car scraping along a wall (core distance ~15 mm, turning a
+// few mrad per step) from being culled; its second-order replacement is ~1e-5 m.  The start pose's rotation is the
+// end pose's b2Rot rotated back by a - a0 (Taylor terms to |a - a0|^5, error < 1e-7 for |a - a0| <= 0.1; larger
+// rotations are not culled here).
+#ifndef TOI_CULL2
+#define TOI_CULL2 1
+#endif
+__device__ __forceinline__ float toi_gap2(V2 u, V2 d1, V2 d0, V2 cx1, V2 cy1, V2 cx0, V2 cy0, float wext) {
+  const float s1 = vdot(u, d1), s0 = vdot(u, d0);
+  const float g1 = fabsf(s1) - (CAR_HX * fabsf(vdot(u, cx1)) + CAR_HY * fabsf(vdot(u, cy1))) - wext;
+  const float g0 = (s1 >= 0.0f ? s0 : -s0) - (CAR_HX * fabsf(vdot(u, cx0)) + CAR_HY * fabsf(vdot(u, cy0))) - wext;
+  return fminb(g0, g1);
+}
+__device__ __forceinline__ bool toi_far_rot2(const Car& c, const LWall& wl, V2 d1, float da, float) {
+  if (!(fabsf(da) <= 0.1f)) return false;
+  const float R_CAR = 2.80389f;
+  const float d2 = da * da;
+  const float cd = 1.0f - 0.5f * d2 + d2 * d2 * (1.0f / 24.0f), sd = da * (1.0f - d2 * (1.0f / 6.0f) + d2 * d2 * (1.0f / 120.0f));
+  const float qc = c.xf.q.c, qs = c.xf.q.s;
+  const float c0c = qc * cd + qs * sd, c0s = qs * cd - qc * sd;   // cos / sin (a - da)
+  const V2 cx1 = V(qc, qs), cy1 = V(-qs, qc), cx0 = V(c0c, c0s), cy0 = V(-c0s, c0c);
+  const V2 wx = V(wl.qc, wl.qs), wy = V(-wl.qs, wl.qc);
+  const V2 d0 = vsub(c.c0, V(wl.px, wl.py));
+  // wall extents along its own axes are hx / hy; along the car's axes hx |u . wx| + hy |u . wy|
+  float b = toi_gap2(wx, d1, d0, cx1, cy1, cx0, cy0, wl.hx);
+  b = fmaxb(b, toi_gap2(wy, d1, d0, cx1, cy1, cx0, cy0, wl.hy));
+  b = fmaxb(b, toi_gap2(cx1, d1, d0, cx1, cy1, cx0, cy0, wl.hx * fabsf(vdot(cx1, wx)) + wl.hy * fabsf(vdot(cx1, wy))));
+  b = fmaxb(b, toi_gap2(cy1, d1, d0, cx1, cy1, cx0, cy0, wl.hx * fabsf(vdot(cy1, wx)) + wl.hy * fabsf(vdot(cy1, wy))));
+  return b - d2 * (R_CAR * 0.125f) > TOI_CULL_DIST;
+}
 __device__ __forceinline__ bool toi_far(const Car& c, const Poly* pa, const LWall& wl) {
 #ifdef NASCAR_NO_TOI_CULL   // A/B and verification builds only
   return false;
@@ -1377,7 +1414,13 @@ __device__ __forceinline__ bool toi_far(const Car& c, const Poly* pa, const LWal
   b = fmaxb(b, toi_gap_bound(wy, d, dc, cx, cy, wx, wy, wl.hx, wl.hy));
   b = fmaxb(b, toi_gap_bound(cx, d, dc, cx, cy, wx, wy, wl.hx, wl.hy));
   b = fmaxb(b, toi_gap_bound(cy, d, dc, cx, cy, wx, wy, wl.hx, wl.hy));
-  return b - fabsf(c.a - c.a0) * R_CAR > TOI_CULL_DIST;
+  const float da = c.a - c.a0;
+  if (b - fabsf(da) * R_CAR > TOI_CULL_DIST) return true;
+#if TOI_CULL2
+  return toi_far_rot2(c, wl, d, da, b);
+#else
+  return false;
+#endif
 }
 
 // b2World::SolveTOI, wave-cooperative.  Box2D's loop per car: scan the contacts (a cached alpha, or a fresh
@@ -1425,6 +1468,10 @@ __device__ inline void solve_toi(Car& c, const WallSet& S, float dt, float frict
         if (!(ct.flags & CT_ENABLED) || ct.toiCount > MAX_SUBSTEPS || (ct.flags & CT_TOI)) continue;
         if (toi_far(c, &pa, ldg(W + ct.wall))) {
           PCOUNT(13, 1); CCOUNT(c, 3, 1);
+#ifdef NASCAR_TOI_CULL_CHECK   // check builds: every culled call run anyway; slot 11 counts culled TOUCHING outcomes
+          if (toi_alpha(make_float4(c.c0.x, c.c0.y, c.c.x, c.c.y), make_float4(c.a0, c.a, c.alpha0, 0.0f),
+                        ldg(W + ct.wall)) < 1.0f) PCOUNT(11, 1);
+#endif
           ct.toi = 1.0f; ct.flags |= CT_TOI;
           continue;
         }

@@ -105,6 +105,9 @@ def main():
         model = b[:NW * 16].reshape(NW, 16)
         sens = b[NW * 16:2 * NW * 16].reshape(NW, 16)
         cnt = b[2 * NW * 16:2 * NW * 16 + 8]
+        tcnt = b[2 * NW * 16 + 11:2 * NW * 16 + 16]
+        print(f"TOI calls computed {tcnt[1]}, culled {tcnt[2]}, culled but TOUCHING (check builds) {tcnt[0]}, "
+              f"events {tcnt[4]}")
         logic = b[LPROF_BASE:LPROF_BASE + NW * 16].reshape(NW, 16)
         print(f"--- step {s}")
         m = phases(model, MODEL, 0, "model_kernel")
