@@ -626,6 +626,62 @@ __device__ inline void contact_update(Car& c, int ci, const LWall* W) {
   if (was && !touching) lis_end(c, wl.key);
 }
 
+// b2Contact::Update split in two for SolveTOI's events (wave-cooperative manifolds, see solve_toi): the manifold
+// b2CollidePolygons computes from the car's transform and the wall (any lane), and the rest of Update on the owner's
+// record.  collide_polygons leaves a record's fields untouched past an early exit, so the packed result says which
+// fields it wrote (stage 0: pointCount only, 1: + type, 2: + local normal / point and the first pc points).
+struct ManiRes { float4 a, b, c; };
+#define MANI_UNSET 0x7fc0deadu   // a NaN collide_polygons never writes to localNormal.x (sentinel: stage 2 not reached)
+__device__ inline ManiRes contact_manifold(Xf xfA, const LWall& wl) {
+  Poly pa, pb; make_box(&pa, CAR_HX, CAR_HY); make_box(&pb, wl.hx, wl.hy);
+  DContact m;
+  m.mtype = -1; m.lnx = __uint_as_float(MANI_UNSET); m.pointCount = 0;
+  m.lny = m.lpx = m.lpy = 0.0f;
+  for (int q = 0; q < 2; ++q) { m.pt[q].lx = m.pt[q].ly = 0.0f; m.pt[q].id = 0u; }
+  collide_polygons(m, &pa, xfA, &pb, wall_xf(wl));
+  const int stage = __float_as_uint(m.lnx) != MANI_UNSET ? 2 : (m.mtype >= 0 ? 1 : 0);
+  ManiRes r;
+  r.a = make_float4(__int_as_float(stage | (m.pointCount << 2) | ((m.mtype & 3) << 4)), m.lnx, m.lny, m.lpx);
+  r.b = make_float4(m.lpy, m.pt[0].lx, m.pt[0].ly, __uint_as_float(m.pt[0].id));
+  r.c = make_float4(m.pt[1].lx, m.pt[1].ly, __uint_as_float(m.pt[1].id), 0.0f);
+  return r;
+}
+// b2Contact::Update of contact ci with its manifold from contact_manifold (the same steps as contact_update)
+__device__ inline void contact_apply(Car& c, int ci, const LWall* W, const ManiRes& r) {
+  PCOUNT(14, 1); CCOUNT(c, 5, 1);
+  DContact ct = c.ct[ci];
+  const DContact old = ct;
+  ct.flags |= CT_ENABLED;
+  bool was = (ct.flags & CT_TOUCH) != 0;
+  const int h = __float_as_int(r.a.x), stage = h & 3, pc = (h >> 2) & 3;
+  ct.pointCount = 0;
+  if (stage >= 1) ct.mtype = (h >> 4) & 3;
+  if (stage == 2) {
+    ct.lnx = r.a.y; ct.lny = r.a.z; ct.lpx = r.a.w; ct.lpy = r.b.x;
+    if (pc > 0) { ct.pt[0].lx = r.b.y; ct.pt[0].ly = r.b.z; ct.pt[0].id = __float_as_uint(r.b.w); ct.pt[0].ni = 0.0f; ct.pt[0].ti = 0.0f; }
+    if (pc > 1) { ct.pt[1].lx = r.c.x; ct.pt[1].ly = r.c.y; ct.pt[1].id = __float_as_uint(r.c.z); ct.pt[1].ni = 0.0f; ct.pt[1].ti = 0.0f; }
+    ct.pointCount = pc;
+  }
+  bool touching = ct.pointCount > 0;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {   // warm-start impulses of the old point with the same feature id (first match)
+    if (i >= ct.pointCount) break;
+    ct.pt[i].ni = 0.0f; ct.pt[i].ti = 0.0f;
+    if (old.pointCount > 0 && old.pt[0].id == ct.pt[i].id) { ct.pt[i].ni = old.pt[0].ni; ct.pt[i].ti = old.pt[0].ti; }
+    else if (old.pointCount > 1 && old.pt[1].id == ct.pt[i].id) { ct.pt[i].ni = old.pt[1].ni; ct.pt[i].ti = old.pt[1].ti; }
+  }
+  if (touching != was) set_awake(c);
+  if (touching) ct.flags |= CT_TOUCH; else ct.flags &= ~CT_TOUCH;
+  c.ct[ci] = ct;
+  if (!was && touching) {
+    const LWall wl = ldg(W + ct.wall);
+    V2 n = zero2(), pts[2];
+    world_manifold(ct, c.xf, wall_xf(wl), &n, pts);
+    lis_begin(c, wl.key, n);
+  }
+  if (was && !touching) lis_end(c, ldg(&W[ct.wall].key));
+}
+
 // b2ContactManager::Collide
 // ------------------------------------------------------------------ wave-cooperative work lists (LDS, per wave)
 // Per-car Box2D work whose size varies by car (a car's TOI pairs) is listed per lane and computed by every
@@ -633,7 +689,11 @@ __device__ inline void contact_update(Car& c, int ci, const LWall* W) {
 // scheme for b2World::Collide's manifolds was parity-green but measured neutral: 118.5 vs 118.8 us.)
 #define TOI_JOBCAP 64     // b2TimeOfImpact pairs per compute round per wave (more pairs: further rounds)
 struct ToiWaveLDS { float4 sw0[64], sw1[64]; int2 job[TOI_JOBCAP]; float res[TOI_JOBCAP]; };
-union WaveLDS { ToiWaveLDS toi; };
+#define MANI_JOBCAP 32    // event manifolds per wave and scan computed cooperatively (the rest by their owners)
+struct ManiWaveLDS { float4 xf[64]; int2 job[MANI_JOBCAP]; ManiRes res[MANI_JOBCAP]; };
+#define BP_JOBCAP 128     // broadphase candidate tests per wave and round
+struct BpWaveLDS { float4 fat[64]; int2 job[BP_JOBCAP]; unsigned int hit[64][2]; };
+union WaveLDS { ToiWaveLDS toi; ManiWaveLDS mani; BpWaveLDS bp; };
 __shared__ WaveLDS g_wave_lds[SBLOCK / 64];   // model_kernel / rollout_kernel (the Box2D step)
 __device__ __forceinline__ void wave_lds_sync() {   // a wave's LDS writes visible to its later LDS reads
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -982,6 +1042,69 @@ __device__ __forceinline__ int solve_island(Car& c, const LWall* W, const int* c
   return positionSolved;
 }
 
+// b2BroadPhase::UpdatePairs of b2World::Solve for every lane of the wave at once (round 3).  A moved car's grid
+// cell lists its candidate walls in ascending proxy id; here every present lane tests any (car, candidate) pair of
+// the wave -- the candidate's fat AABB against the owner's, read from LDS -- and sets the pair's bit in the owner's
+// hit mask, then each owner runs AddPair for its hits in ascending candidate order: the same pairs in the same
+// order as find_new_contacts' own loop, with one round of independent loads per wave instead of a dependent chain
+// per car.  Lists longer than 64 candidates, queries outside the grid or wider than its reach take the car's own scan.
+#ifndef BP_COOP
+#define BP_COOP 1
+#endif
+__device__ inline void find_new_contacts_wave(Car& c, const WallSet& S, bool want) {
+  bool mine = false; int beg = 0, end = 0;
+  if (want && c.moved) {
+    const float hx = 0.5f * (c.fat.hi.x - c.fat.lo.x), hy = 0.5f * (c.fat.hi.y - c.fat.lo.y);
+    const float cx = 0.5f * (c.fat.hi.x + c.fat.lo.x), cy = 0.5f * (c.fat.hi.y + c.fat.lo.y);
+    if (S.bp.box && hx <= S.bp.reach - 0.05f && hy <= S.bp.reach - 0.05f && grid_list(S.bp, cx, cy, beg, end) &&
+        end - beg <= 64) {
+      mine = true;
+      c.moved = 0;
+    } else {
+      find_new_contacts(c, S);
+    }
+  }
+  if (!__ballot(mine)) return;   // wave-uniform
+  BpWaveLDS& B = g_wave_lds[threadIdx.x >> 6].bp;
+  const int lane = (int)__lane_id();
+  const unsigned long long present = __ballot(1);
+  const int prank = rank_in(present), npresent = popc64(present);
+  const int m = mine ? end - beg : 0;
+  int off = 0, total = 0;
+#pragma unroll
+  for (int bit = 0; bit < 7; ++bit) {
+    const unsigned long long b = __ballot((m >> bit) & 1);
+    off += rank_in(b) << bit;
+    total += popc64(b) << bit;
+  }
+  if (mine) { B.fat[lane] = make_float4(c.fat.lo.x, c.fat.lo.y, c.fat.hi.x, c.fat.hi.y); B.hit[lane][0] = 0u; B.hit[lane][1] = 0u; }
+  for (int r0 = 0; r0 < total; r0 += BP_JOBCAP) {   // wave-uniform
+    if (mine) {
+      const int k1 = min(off + m, r0 + BP_JOBCAP);
+      for (int k = max(off, r0); k < k1; ++k) B.job[k - r0] = make_int2(lane | ((k - off) << 8), beg + (k - off));
+    }
+    wave_lds_sync();
+    const int cnt = min(BP_JOBCAP, total - r0);
+    for (int j = prank; j < cnt; j += npresent) {
+      const int2 jb = B.job[j];
+      const int owner = jb.x & 0xFF, q = jb.x >> 8;
+      const float4 f = B.fat[owner], b = ldg(S.bp.box + jb.y);
+      Aabb fa; fa.lo = V(f.x, f.y); fa.hi = V(f.z, f.w);
+      Aabb bb; bb.lo = V(b.x, b.y); bb.hi = V(b.z, b.w);
+      if (overlap(fa, bb)) atomicOr(&B.hit[owner][q >> 5], 1u << (q & 31));
+    }
+    wave_lds_sync();
+  }
+  if (mine) {
+    unsigned long long h = (unsigned long long)B.hit[lane][0] | ((unsigned long long)B.hit[lane][1] << 32);
+    while (h) {
+      const int q = __ffsll((long long)h) - 1; h &= h - 1;
+      add_pair(c, S, (int)ldg(S.bp.idx + beg + q));
+    }
+  }
+  wave_lds_sync();   // hit masks read before the union's next use
+}
+
 // b2World::Solve (single dynamic body island)
 __device__ inline void solve(Car& c, const WallSet& S, float dt, float dtRatio, float friction) {
   const LWall* W = S.W;
@@ -1018,12 +1141,14 @@ __device__ inline void solve(Car& c, const WallSet& S, float dt, float dtRatio, 
   sync_fixtures(c);
   CTIME_END(c, 22);
   }
+#if !BP_COOP   // (else b2_step runs the wave's broadphase updates together: find_new_contacts_wave)
   {
   CTIME_BEGIN();
   if (c.moved) CCOUNT(c, 24, 1);
   find_new_contacts(c, S);
   CTIME_END(c, 21);
   }
+#endif
 }
 
 // ------------------------------------------------------------------ GJK / TOI
@@ -1448,6 +1573,16 @@ __device__ __forceinline__ float toi_alpha(float4 s0, float4 s1, const LWall& wl
   const float beta = time_of_impact(&state, &pa, sA, &pb, sB, 1.0f, qw, __float_as_uint(wl.ang), iters, cyc);
   return state == TOI_TOUCHING ? fminb(s1.z + (1.0f - s1.z) * beta, 1.0f) : 1.0f;
 }
+#ifndef TOI_COOP_MANI
+#define TOI_COOP_MANI 1
+#endif
+// contact ci's b2Contact::Update inside a TOI event: from the wave's cooperative manifold when it has one
+__device__ __forceinline__ void toi_contact_update(Car& c, int ci, const LWall* W, int moff) {
+#if TOI_COOP_MANI
+  if (moff + ci < MANI_JOBCAP) { contact_apply(c, ci, W, g_wave_lds[threadIdx.x >> 6].mani.res[moff + ci]); return; }
+#endif
+  contact_update(c, ci, W);
+}
 __device__ inline void solve_toi(Car& c, const WallSet& S, float dt, float friction) {
   ToiWaveLDS& L = g_wave_lds[threadIdx.x >> 6].toi;
   const LWall* W = S.W;
@@ -1531,8 +1666,10 @@ __device__ inline void solve_toi(Car& c, const WallSet& S, float dt, float frict
     const unsigned long long te0 = __builtin_amdgcn_s_memtime();
 #endif
     // (3) this lane's scan on cached alphas and its event, as Box2D
+    int minC = -1; float minAlpha = 1.0f;
+    bool ev = false;
+    V2 bc0 = c.c0, bc = c.c; float ba0 = c.a0, ba = c.a, balpha0 = c.alpha0;
     if (active) {
-      int minC = -1; float minAlpha = 1.0f;
       for (int i = 0; i < c.nct; ++i) {
         const DContact& ct = c.ct[i];
         if (!(ct.flags & CT_ENABLED) || ct.toiCount > MAX_SUBSTEPS || !(ct.flags & CT_TOI)) continue;
@@ -1544,8 +1681,9 @@ __device__ inline void solve_toi(Car& c, const WallSet& S, float dt, float frict
       if (minC < 0 || 1.0f - 10.0f * FLT_EPS < minAlpha) {
         active = false;
       } else {
+        ev = true;
         PCOUNT(15, 1); CCOUNT(c, 4, 1);
-        V2 bc0 = c.c0, bc = c.c; float ba0 = c.a0, ba = c.a, balpha0 = c.alpha0;
+        bc0 = c.c0; bc = c.c; ba0 = c.a0; ba = c.a; balpha0 = c.alpha0;
         {
           float beta = fdiv_cr(minAlpha - c.alpha0, 1.0f - c.alpha0);
           c.c0 = vadd(c.c0, vmul(beta, vsub(c.c, c.c0)));
@@ -1554,9 +1692,45 @@ __device__ inline void solve_toi(Car& c, const WallSet& S, float dt, float frict
           c.c = c.c0; c.a = c.a0;
           sync_transform(c);
         }
+      }
+    }
+    // (3b) wave-cooperative event manifolds: the event's contact update and the island's updates all see the car
+    // at its TOI pose (the static walls never move), so b2CollidePolygons of every contact of every event lane is
+    // computed up front by any present lane; the owners then apply them in Box2D's order (contact_apply), and
+    // only results they reach are used.  Contacts past the LDS job capacity are updated by their owner.
+    int moff = MANI_JOBCAP;   // this lane's first result slot (contact i -> slot moff + i)
+#if TOI_COOP_MANI
+    if (__ballot(ev)) {   // wave-uniform
+      ManiWaveLDS& M = g_wave_lds[threadIdx.x >> 6].mani;
+      const int mm = ev ? c.nct : 0;
+      int off2 = 0, total2 = 0;
+#pragma unroll
+      for (int bit = 0; bit < 5; ++bit) {
+        const unsigned long long b = __ballot((mm >> bit) & 1);
+        off2 += rank_in(b) << bit;
+        total2 += popc64(b) << bit;
+      }
+      if (ev) {
+        moff = off2;
+        M.xf[lane] = make_float4(c.xf.p.x, c.xf.p.y, c.xf.q.s, c.xf.q.c);
+        for (int i = 0; i < c.nct && off2 + i < MANI_JOBCAP; ++i) M.job[off2 + i] = make_int2(lane | (i << 8), c.ct[i].wall);
+      }
+      wave_lds_sync();
+      const int cnt = min(MANI_JOBCAP, total2);
+      for (int j = prank; j < cnt; j += npresent) {
+        const int2 jb = M.job[j];
+        const float4 x = M.xf[jb.x & 0xFF];
+        Xf xfA; xfA.p = V(x.x, x.y); xfA.q.s = x.z; xfA.q.c = x.w;
+        M.res[j] = contact_manifold(xfA, ldg(W + jb.y));
+      }
+      wave_lds_sync();
+    }
+#endif
+    if (ev) {
+      {
         {
         CTIME_BEGIN();
-        contact_update(c, minC, W);
+        toi_contact_update(c, minC, W, moff);
         CTIME_END(c, 12);
         }
         c.ct[minC].flags &= ~CT_TOI;
@@ -1581,7 +1755,7 @@ __device__ inline void solve_toi(Car& c, const WallSet& S, float dt, float frict
               break;
             }
             if (c.ct[i].flags & CT_ISLAND) continue;
-            contact_update(c, i, W);
+            toi_contact_update(c, i, W, moff);
             if (!(c.ct[i].flags & CT_ENABLED)) continue;
             if (!(c.ct[i].flags & CT_TOUCH)) continue;
             c.ct[i].flags |= CT_ISLAND;
@@ -1613,6 +1787,9 @@ __device__ inline void solve_toi(Car& c, const WallSet& S, float dt, float frict
         }
       }
     }
+#if TOI_COOP_MANI
+    wave_lds_sync();   // every owner's result reads done before the next scan's LDS writes
+#endif
 #ifdef NASCAR_PROFILE
     CCOUNT(c, 15, __builtin_amdgcn_s_memtime() - te0);   // the wave's event processing of this scan
 #endif
@@ -1638,7 +1815,16 @@ __device__ inline void b2_step(Car& c, const WallSet& S, float dt, float frictio
 #endif
   PROFB(11);
 #ifndef NASCAR_KO_SOLVE
+  {
+  const bool awake = c.awake != 0;   // b2World::Solve updates the pairs of awake bodies only
   solve(c, S, dt, dtRatio, friction);
+#if BP_COOP
+  CTIME_BEGIN();
+  if (awake && c.moved) CCOUNT(c, 24, 1);
+  find_new_contacts_wave(c, S, awake);
+  CTIME_END(c, 21);
+#endif
+  }
 #endif
   PROFB(13);
 #ifdef NASCAR_PROFILE
