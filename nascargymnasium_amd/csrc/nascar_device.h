@@ -1049,7 +1049,10 @@ __device__ __forceinline__ int solve_island(Car& c, const LWall* W, const int* c
 // order as find_new_contacts' own loop, with one round of independent loads per wave instead of a dependent chain
 // per car.  Lists longer than 64 candidates, queries outside the grid or wider than its reach take the car's own scan.
 #ifndef BP_COOP
-#define BP_COOP 1
+#define BP_COOP 0   // measured neutral (160.7 vs 159.2 us/step, 3 A/B rounds): the broadphase chain is not its candidate loads
+#endif
+#ifndef MODEL_PRIO
+#define MODEL_PRIO 0   // wave priority experiments (0: off)
 #endif
 __device__ inline void find_new_contacts_wave(Car& c, const WallSet& S, bool want) {
   bool mine = false; int beg = 0, end = 0;
@@ -1831,7 +1834,13 @@ __device__ inline void b2_step(Car& c, const WallSet& S, float dt, float frictio
   const unsigned long long t1 = __builtin_amdgcn_s_memtime();
 #endif
 #ifndef NASCAR_KO_TOI
+#if MODEL_PRIO == 2   // A/B: waves in SolveTOI issue ahead of co-resident waves
+  __builtin_amdgcn_s_setprio(3);
+#endif
   solve_toi(c, S, dt, friction);
+#if MODEL_PRIO == 2
+  __builtin_amdgcn_s_setprio(0);
+#endif
 #endif
 #ifdef NASCAR_PROFILE
   const unsigned long long t2 = __builtin_amdgcn_s_memtime();

@@ -1615,6 +1615,9 @@ __global__ void __launch_bounds__(SBLOCK) __attribute__((amdgpu_waves_per_eu(MOD
   const int n = env >= 0 ? env * C + car : 0;
   PROF_RT(14);
   PROF(0);
+#if MODEL_PRIO == 1   // A/B: model_kernel's waves issue ahead of co-resident logic / sensor waves of other shards
+  __builtin_amdgcn_s_setprio(2);
+#endif
   __shared__ DSeg s_segs[MAX_SEG];
   Car c;
   // car state and action requested before the segment staging barrier (their round trips overlap the
