@@ -138,10 +138,13 @@ def main():
                     print("   ", i, *cp[i, [0, 1, 2, 3, 4, 5, 6, 7]].tolist(), f"| bp full scans {cp[i, 8]}, candidates {cp[i, 9]}"
                           f" | x {info[i, F.index('x')]:.1f} y {info[i, F.index('y')]:.1f} v ({info[i, F.index('vx')]:.1f}, "
                           f"{info[i, F.index('vy')]:.1f}) angle {info[i, F.index('angle')]:.2f} disabled {info[i, F.index('disabled')]:.0f} n_contacts {info[i, F.index('n_contacts')]:.0f}")
-            w0 = np.argsort(-cyc)[0] // 64 * 64
-            print(f"  slowest wave (cars {w0}..{w0 + 63}): solve_toi scans {cp[w0, 14]}, TOI job rounds {cp[w0, 13]} cycles, "
+            per = (128 // a.cars) * a.cars                 # cars per workgroup (SBLOCK 128, whole envs)
+            i0 = np.argsort(-cyc)[0]
+            w0 = i0 // per * per + (i0 % per) // 64 * 64   # first car of the slowest car's wave
+            w1 = min(w0 + 64, i0 // per * per + per, len(cp))
+            print(f"  slowest wave (cars {w0}..{w1 - 1}): solve_toi scans {cp[w0, 14]}, TOI job rounds {cp[w0, 13]} cycles, "
                   f"event processing {cp[w0, 15]} cycles")
-            for i in range(w0, min(w0 + 64, len(cp))):
+            for i in range(w0, w1):
                 if cp[i, 4] or cp[i, 2]:
                     print(f"    car {i}: events {cp[i, 4]}, island solve {cp[i, 11]}, event contact updates {cp[i, 12]}, "
                           f"TOI calls computed by this lane {cp[i, 2]}: outer iters {cp[i, 6]}, root iters {cp[i, 7]}, "
