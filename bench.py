@@ -27,6 +27,9 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 ALGO_BYTES_PER_CAR_STEP = 1221      # 2 x 528 B state + 8 B action + 152 B obs + 4 B reward + 1 B flags
+# model_kernel's own share (the dominant kernel's roofline): the SURVEY Appendix B state it reads and writes -- Box2D
+# body 7 + contacts 56 + listener 4 + car 27 + tyres 12 = 106 words, read + written -- plus the 8 B action
+MODEL_ALGO_BYTES_PER_CAR = 2 * 106 * 4 + 8
 HBM_PEAK_GBS = 8000.0               # MI355X HBM3E spec (MI355X_MICROARCH.md)
 EPISODE_STEPS = 10800               # 180 s time limit at dt = 1/60 (src/car_env.py:1154)
 POLICY_ID = {"uniform": 0, "driver": 1, "sac": 2, "noisy": 3}
@@ -66,16 +69,47 @@ def _oracle_shard(track, cars, E, seed, budget_s, out, slot):
     env.close()
 
 
+def host_cores():
+    """(threads to use, description): every core this process may run on -- its affinity mask, capped by a cgroup
+    CPU quota and by the host's declared CPU share (OMP_NUM_THREADS) when set: on the GPU box the affinity mask lists
+    the whole machine while the job's share is 16 cores, and more threads than the share only time-slice."""
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, -(-int(q) // int(per)))
+    except (OSError, ValueError):
+        pass
+    model = "unknown CPU"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    share = None
+    try:
+        share = int(os.environ["OMP_NUM_THREADS"]) if os.environ.get("OMP_NUM_THREADS") else None
+    except ValueError:
+        pass
+    n = min([aff] + [x for x in (quota, share) if x])
+    return n, (f"{model}; affinity {aff} cores" + (f", cgroup quota {quota} cores" if quota else ", no cgroup quota")
+               + (f", declared CPU share OMP_NUM_THREADS={share}" if share else "") + f"; {n} threads used")
+
+
 def cpu_baseline(track, cars, budget_s=12.0, threads=None):
     """The CPU oracle (C restatement of the reference path) on a bounded sample of the same workload:
     16 envs x C cars per shard, noisy rule driver from reset.  First 1 thread for budget_s / 2, then one shard
-    per host thread (threads = the box's CPU share, at most 16) for budget_s / 2 of wall time; `value` is the
-    multi-thread rate (car-steps over the slowest shard's time), the 1-thread rate is in `sample`."""
+    per host thread (threads = every core the process may use, host_cores()) for budget_s / 2 of wall time;
+    `value` is the multi-thread rate (car-steps over the slowest shard's time), the 1-thread rate is in `sample`."""
     import threading
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     E = 16
+    n_host, host_txt = host_cores()
     if threads is None:
-        threads = max(1, min(16, len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()))
+        threads = n_host
     one = [None]
     _oracle_shard(track, cars, E, 0, budget_s / 2, one, 0)
     rate1 = one[0][0] / one[0][1]
@@ -87,10 +121,11 @@ def cpu_baseline(track, cars, budget_s=12.0, threads=None):
         t.join()
     rate = sum(r[0] for r in res) / max(r[1] for r in res)
     return {"value": rate, "unit": "car-steps/s", "cores": threads, "kind": "port",
+            "host": host_txt,
             "sample": f"oracle (C restatement of the reference path incl. Box2D subset) on {os.path.basename(track)}, "
                       f"noisy rule driver from reset (first ~{min(r[2] for r in res)} steps; the CPU cannot afford "
                       f"the GPU run's 10 800-step settle): {threads} host threads x one shard of {E} envs x {cars} cars, "
-                      f"~{budget_s / 2:.0f} s each; 1 thread alone: {rate1:.0f} car-steps/s"}
+                      f"~{budget_s / 2:.0f} s each; 1 thread alone: {rate1:.0f} car-steps/s; host: {host_txt}"}
 
 
 def reduce_max(values, device):
@@ -113,6 +148,67 @@ def reduce_sum(values, device):
     t = torch.tensor([float(v) for v in values], device=device, dtype=torch.float64)
     dist.all_reduce(t, op=dist.ReduceOp.SUM)
     return [float(x) for x in t.tolist()]
+
+
+def gather_all(value, device):
+    """every rank's value (rank order; [value] at world size 1) -- the per-rank timings the MAX is taken over"""
+    import torch
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return [float(value)]
+    t = torch.tensor([float(value)], device=device, dtype=torch.float64)
+    out = [torch.zeros_like(t) for _ in range(dist.get_world_size())]
+    dist.all_gather(out, t)
+    return [float(x.item()) for x in out]
+
+
+def launch_ranks(n, argv):
+    """`bench.py --gpus N` (N > 1) outside a torchrun environment: start the N ranks as one child
+    `python -m torch.distributed.run --nproc-per-node N ... bench.py <same args>` (the driver's own launch line),
+    rendezvous on 127.0.0.1, and return its exit code.  The parent never initialises the GPU and never execs (a
+    process that has touched the GPU must not replace itself); it only waits.  The reference scales the same way, by
+    processes (learn/ppo.py:77, SubprocVecEnv)."""
+    import socket
+    import subprocess
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.run(cmd, env=env).returncode
+
+
+def plumbing(args, world, rank):
+    """--plumbing: the multi-rank launch and reduction path without a GPU (CPU tests): gloo process group, rank r
+    'steps' by sleeping (r + 1) ms per step, then the same barrier-bracketed timing, MAX over ranks, whole-job value
+    and per-rank record as the measured line.  Not a measurement: the line's metric says so."""
+    import torch
+    import torch.distributed as dist
+    if world > 1:
+        dist.init_process_group("gloo")
+    dev = torch.device("cpu")
+    E, C, K = args.envs, args.cars, args.steps
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(K):
+        time.sleep((rank + 1) * 1e-3)
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    per_rank = gather_all(el, dev)
+    elapsed = reduce_max([el], dev)[0]
+    out = {"metric": "plumbing (no GPU, not a measurement)", "value": throughput(world, E, C, K, elapsed),
+           "unit": "car-steps/s", "n_gpus": world, "steps": K, "warmup": args.warmup, "ms_per_step": elapsed / K * 1e3,
+           "ranks": {"world_size": dist.get_world_size() if world > 1 else 1,
+                     "backend": dist.get_backend() if world > 1 else None, "elapsed_s": per_rank},
+           "config": {"envs_per_gpu": E, "cars_per_env": C}}
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
 
 
 def throughput(world, envs, cars, steps, elapsed_max):
@@ -312,7 +408,9 @@ def kernel_pass(env, step, first, KR):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="GPUs (ranks) of this node; without a torchrun environment N > 1 launches N ranks itself "
+                         "(default: WORLD_SIZE, else 1)")
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--envs", type=int, default=8192)
@@ -343,15 +441,29 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
+    ap.add_argument("--plumbing", action="store_true", help="CPU tests: the multi-rank launch + reduction path only "
+                    "(gloo, no GPU, no engine; not a measurement)")
     args = ap.parse_args()
+
+    if "WORLD_SIZE" not in os.environ:
+        if args.gpus is not None and args.gpus > 1:      # one rank per GPU, started before anything touches a GPU
+            sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+        world = 1
+    else:
+        world = int(os.environ["WORLD_SIZE"])
+        if args.gpus is not None and args.gpus != world:
+            print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world} ranks were launched", file=sys.stderr)
+            sys.exit(2)
+    rank = int(os.environ.get("RANK", "0"))
+    if args.plumbing:
+        plumbing(args, world, rank)
+        return
 
     import torch
     import torch.distributed as dist
     from nascargymnasium_amd.batched import BatchedCarEnv
     from nascargymnasium_amd.track import track_path
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)   # before the process group, so RCCL's barrier binds this rank's GPU
     if world > 1:
@@ -415,6 +527,7 @@ def main():
         first = base + W + K + 3 * KR
         ps.run(first, W)
         per_step = timed(ps, first + W, K, world)
+    rank_elapsed = gather_all(elapsed, dev)
     elapsed, kern_ms = reduce_max([elapsed, kern_ms], dev)
     kt_names = ("model_kernel", "logic_kernel", "ray_sensor_kernel")
     ktimes = dict(zip(kt_names, reduce_max([ktimes[k] for k in kt_names], dev)))
@@ -422,9 +535,10 @@ def main():
         per_step = reduce_max([per_step], dev)[0]
     tally = reduce_sum(tally, dev)
     value = throughput(world, E, C, K, elapsed)
-    # dominant kernel (model_kernel, whole grid): the step's algorithmic bytes per car-step x the cars one launch
-    # processes, over its mean launch duration (HIP events around it on its stream, per-step path)
-    achieved = E * C * ALGO_BYTES_PER_CAR_STEP / (ktimes["model_kernel"] * 1e-3) / 1e9
+    # dominant kernel (model_kernel, whole grid): ITS algorithmic bytes per car (the state it reads and writes + the
+    # action) x the cars one launch processes, over its mean launch duration (HIP events around it on its stream,
+    # per-step path).  The whole step's bytes over the timed window's step time are `roofline.step`.
+    achieved = E * C * MODEL_ALGO_BYTES_PER_CAR / (ktimes["model_kernel"] * 1e-3) / 1e9
     step_achieved = E * C * ALGO_BYTES_PER_CAR_STEP / (elapsed / K) / 1e9      # the timed window itself
     traffic, tnote = None, "no PMC file for this workload"
     tfile = os.path.join(ROOT, "profiles", "pmc_traffic.json")
@@ -481,14 +595,23 @@ def main():
                      "kernel": "model_kernel (dominant kernel; whole-grid launch on the per-step path, HIP events around "
                                "each launch on its stream)",
                      "kernel_ms": ktimes["model_kernel"], "units_per_launch": E * C,
-                     "algo_bytes_per_car_step": ALGO_BYTES_PER_CAR_STEP,
+                     "algo_bytes_per_unit": MODEL_ALGO_BYTES_PER_CAR,
+                     "algo_bytes_note": "model_kernel's share of SURVEY Appendix B: body + contacts + listener + car + "
+                                        "tyre state read and written (848 B) + 8 B action; the whole step's 1221 B per "
+                                        "car-step are used in roofline.step",
                      "kernel_times_ms": ktimes,
                      "step": {"achieved": step_achieved, "frac": step_achieved / HBM_PEAK_GBS, "ms": elapsed / K * 1e3,
-                              "note": "the same bytes over the timed window's time per step (" + launch_txt + ")"},
+                              "algo_bytes_per_car_step": ALGO_BYTES_PER_CAR_STEP,
+                              "note": "the whole step's algorithmic bytes (1221 B per car-step) over the timed window's "
+                                      "time per step (" + launch_txt + ")"},
                      "timed_path_event_ms": kern_ms,
                      "timed_path_event_note": kernel_txt},
         "workload_stats": wstats,
         "engine_errors": int(tally[5]),
+        "ranks": {"world_size": dist.get_world_size() if world > 1 else 1,
+                  "backend": dist.get_backend() if world > 1 else None,
+                  "elapsed_s": rank_elapsed, "envs_per_block": env.envs_per_block,
+                  "note": "one process per GPU; each rank times its own K steps between barriers, value uses the MAX"},
     }
     if per_step is not None:
         out["per_step"] = {"value": throughput(world, E, C, K, per_step), "ms_per_step": per_step / K * 1e3,

@@ -107,6 +107,15 @@ int nascar_rollout(NascarHandle* h, int32_t policy, uint64_t seed, int64_t step0
 int nascar_set_rollout_streams(NascarHandle* h, int32_t streams);
 int nascar_get_rollout_streams(NascarHandle* h);
 
+/* Workgroup layout (no reference counterpart: the reference loops over envs and cars one at a time,
+ * learn/ppo.py:77 SubprocVecEnv and src/car_env.py:567-570; a scheduling choice with identical results).
+ * The one-lane-per-car step kernels run 128-lane workgroups of `epb` whole envs each, epb in [1, 128 / C];
+ * epb = 0 restores the automatic choice (128 / C, or fewer envs per workgroup when that leaves fewer than 2
+ * workgroups per CU).  May be called at any time; the next launch uses the new layout.
+ * nascar_get_envs_per_block returns the current value (-1 for a NULL handle). */
+int nascar_set_envs_per_block(NascarHandle* h, int32_t epb);
+int nascar_get_envs_per_block(NascarHandle* h);
+
 /* Profiling hook (no reference counterpart; bench.py's per-kernel roofline): events = 4 caller-created timing
  * events (hipEvent_t), recorded by every following whole-grid step (nascar_step / nascar_step_driven) on its
  * stream before model_kernel, after model_kernel, after logic_kernel and after the sensor launch; n = 0 stops.

@@ -33,7 +33,8 @@ class BatchedCarEnv:
 
     def __init__(self, num_envs: int, num_cars: int = 1, track_file: Union[str, Sequence[str]] = "daytona",
                  reset_on_lap: bool = False, device: Union[str, int, torch.device] = "cuda",
-                 start_position=None, start_angle: float = 0.0, perf_history: bool = False):
+                 start_position=None, start_angle: float = 0.0, perf_history: bool = False,
+                 envs_per_block: Optional[int] = None):
         if not torch.cuda.is_available():
             raise RuntimeError("BatchedCarEnv needs a HIP device (torch.cuda.is_available() is False); "
                                "the product path has no CPU fallback")
@@ -56,6 +57,8 @@ class BatchedCarEnv:
         with torch.cuda.device(self.device):
             _lib.check(self.L.nascar_create(ctypes.byref(cfg), ctypes.byref(h)))
         self.h = h
+        if envs_per_block is not None:
+            self.set_envs_per_block(envs_per_block)
         self.tracks, self._track_id = [], {}
         for p in uniq:
             self._add_track(p)
@@ -86,6 +89,16 @@ class BatchedCarEnv:
     @property
     def rollout_streams(self) -> int:
         return int(self.L.nascar_get_rollout_streams(self.h))
+
+    def set_envs_per_block(self, epb: int = 0):
+        """Workgroup layout of the one-lane-per-car step kernels: `epb` whole envs per 128-lane workgroup, in
+        [1, 128 // C]; 0 restores the automatic choice.  Results do not depend on it (tests pin every layout the
+        bench runs against the oracle); it changes only which cars share a wave."""
+        _lib.check(self.L.nascar_set_envs_per_block(self.h, int(epb)))
+
+    @property
+    def envs_per_block(self) -> int:
+        return int(self.L.nascar_get_envs_per_block(self.h))
 
     def set_perf_history(self, enable: bool = True):
         """Keep Car.velocity_history on the device so the info's `performance` dict is Car.validate_performance

@@ -336,7 +336,8 @@ __device__ __forceinline__ void ct_make_room(Car& c, const WallSet& S) {
   if (S.ct_all && ct_in_lds(c)) {
     if (c.nct >= CT_LDS_CAP) {
       DContact* g = S.ct_all + (size_t)c.pid * MAXC;
-      for (int i = 0; i < c.nct; ++i) g[i] = c.ct[i];
+      const int nrec = max(c.nct, c.ct_hw);   // live records and the dead ones earlier removals left behind
+      for (int i = 0; i < nrec; ++i) g[i] = c.ct[i];
       c.ct = g;
     } else {
       c.ct_hw = max(c.ct_hw, c.nct + 1);

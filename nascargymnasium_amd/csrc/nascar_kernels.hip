@@ -2502,7 +2502,7 @@ struct NascarHandle {
   float* d_ro_act = nullptr;        // [N][2] actions of a policy-2 (SAC actor) sharded rollout
   hipEvent_t step_ev[4] = {nullptr, nullptr, nullptr, nullptr};   // nascar_set_step_events (profiling)
   // prepare(): capacities of the track table / block map buffers, pinned staging of their stream-ordered uploads
-  size_t cap_tracks = 0, cap_blocks = 0;
+  size_t cap_tracks = 0, cap_blocks = 0, cap_blk_env = 0;
   void* h_stage = nullptr; size_t stage_bytes = 0;
   hipEvent_t ev_stage = nullptr;
 };
@@ -2510,6 +2510,34 @@ struct NascarHandle {
 static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 extern "C" const char* nascar_last_error(void) { return g_err.c_str(); }
+
+// envs per workgroup of the one-lane-per-car kernels: as many whole envs as fit (SBLOCK / C), unless that leaves
+// fewer than 2 workgroups per CU -- a small batch (e.g. 4096 envs x 1 car: 32 workgroups) is then spread over
+// 2 x CUs workgroups with fewer envs each.  Every step kernel lasts as long as its slowest wave, and a wave's
+// time is the sum over its phases of the slowest lane's: fewer cars per wave shorten the slowest car's wait on
+// its wave-mates (the chip has room for the extra, partly empty waves).  NASCAR_EPB overrides (A/B).
+static int auto_epb(int E, int C, int device) {
+  int epb = SBLOCK / C;
+  int cus = 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus <= 0) cus = 256;
+  const long target = 2L * cus;
+  if ((E + epb - 1) / epb < target) epb = std::max(1, (int)((E + target - 1) / target));
+  if (const char* ev = getenv("NASCAR_EPB")) { const int v = atoi(ev); if (v >= 1 && v <= SBLOCK / C) epb = v; }
+  return epb;
+}
+
+// Layout of the envs over the step kernels' workgroups (a scheduling choice: every env's state lives in the
+// env-indexed arena whatever its workgroup, so results do not depend on it; tests pin that against the oracle).
+extern "C" int nascar_set_envs_per_block(NascarHandle* h, int32_t epb) {
+  if (!h) return fail("null argument");
+  const int mx = SBLOCK / h->C;
+  if (epb == 0) epb = auto_epb(h->E, h->C, h->cfg.device);
+  if (epb < 1 || epb > mx) return fail("envs per workgroup must be in [1, %d] for %d cars per env (0: automatic), got %d",
+                                      mx, h->C, epb);
+  if (epb != h->epb) { h->epb = epb; h->dirty_tracks = true; }   // prepare() rebuilds the block map
+  return 0;
+}
+extern "C" int nascar_get_envs_per_block(NascarHandle* h) { return h ? h->epb : -1; }
 
 extern "C" int nascar_create(const NascarConfig* cfg, NascarHandle** out) {
   if (!cfg || !out) return fail("null argument");
@@ -2519,19 +2547,7 @@ extern "C" int nascar_create(const NascarConfig* cfg, NascarHandle** out) {
   NascarHandle* h = new NascarHandle();
   h->cfg = *cfg;
   h->E = cfg->num_envs; h->C = cfg->num_cars; h->N = h->E * h->C;
-  // envs per workgroup of the one-lane-per-car kernels: as many whole envs as fit (SBLOCK / C), unless that leaves
-  // fewer than 2 workgroups per CU -- a small batch (e.g. 4096 envs x 1 car: 32 workgroups) is then spread over
-  // 2 x CUs workgroups with fewer envs each.  Every step kernel lasts as long as its slowest wave, and a wave's
-  // time is the sum over its phases of the slowest lane's: fewer cars per wave shorten the slowest car's wait on
-  // its wave-mates (the chip has room for the extra, partly empty waves).  NASCAR_EPB overrides (A/B).
-  h->epb = SBLOCK / h->C;
-  {
-    int cus = 0;
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, cfg->device) != hipSuccess || cus <= 0) cus = 256;
-    const long target = 2L * cus;
-    if ((h->E + h->epb - 1) / h->epb < target) h->epb = std::max(1, (int)((h->E + target - 1) / target));
-    if (const char* ev = getenv("NASCAR_EPB")) { const int v = atoi(ev); if (v >= 1 && v <= SBLOCK / h->C) h->epb = v; }
-  }
+  h->epb = auto_epb(h->E, h->C, cfg->device);
   size_t N = h->N, E = h->E, o = 0;
   h->off_f32 = o; o = align256(o + sizeof(float) * N_F32 * N);
   h->off_f64 = o; o = align256(o + sizeof(double) * N_F64 * N);
@@ -2792,7 +2808,8 @@ static int prepare(NascarHandle* h, hipStream_t stream) {
     }
   }
   const size_t nt = td.size(), nb = blk_track.size();
-  if (nt > h->cap_tracks || nb > h->cap_blocks) {   // growth: earlier launches may still read the old buffers
+  // growth (a new track, a finer layout from nascar_set_envs_per_block): earlier launches may still read the old buffers
+  if (nt > h->cap_tracks || nb > h->cap_blocks || blk_env.size() > h->cap_blk_env) {
     HIPCHK(hipDeviceSynchronize());
     if (nt > h->cap_tracks) {
       hipFree(h->d_tracks); h->d_tracks = nullptr;
@@ -2800,12 +2817,14 @@ static int prepare(NascarHandle* h, hipStream_t stream) {
       HIPCHK(hipMalloc(&h->d_tracks, sizeof(TrackDev) * cap));
       h->cap_tracks = cap;
     }
-    if (nb > h->cap_blocks) {
+    if (nb > h->cap_blocks || blk_env.size() > h->cap_blk_env) {
       hipFree(h->d_blk_track); hipFree(h->d_blk_env); h->d_blk_track = h->d_blk_env = nullptr;
+      h->cap_blocks = h->cap_blk_env = 0;
       const size_t cap = std::max(nb, (size_t)(h->E + h->epb - 1) / h->epb + 8);
+      const size_t cap_env = std::max(blk_env.size(), cap * h->epb);
       HIPCHK(hipMalloc(&h->d_blk_track, sizeof(int) * cap));
-      HIPCHK(hipMalloc(&h->d_blk_env, sizeof(int) * cap * h->epb));
-      h->cap_blocks = cap;
+      HIPCHK(hipMalloc(&h->d_blk_env, sizeof(int) * cap_env));
+      h->cap_blocks = cap; h->cap_blk_env = cap_env;
     }
   }
   const size_t b_tr = sizeof(TrackDev) * nt, b_bt = sizeof(int) * nb, b_be = sizeof(int) * blk_env.size();

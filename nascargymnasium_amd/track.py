@@ -148,11 +148,10 @@ def load_track(file_path: str) -> Track:
         elif cmd == "STRAIGHT":
             if len(parts) < 2 or len(parts) > 3:
                 raise ValueError(f"STRAIGHT command requires 1-2 arguments (length [, banking]): {line}")
-            try:
-                length = float(parts[1])
-                banking = float(parts[2]) if len(parts) == 3 else 0.0
-            except ValueError:
-                raise ValueError(f"Invalid numeric values for STRAIGHT command: {parts[1:]}")
+            # float() raises Python's own "could not convert string to float: 'X'": the reference's re-wrap looks for
+            # "invalid literal" (an int() message) and so re-raises float()'s error unchanged (track_generator.py:370-374)
+            length = float(parts[1])
+            banking = float(parts[2]) if len(parts) == 3 else 0.0
             if banking < -45 or banking > 45:
                 raise ValueError(f"Banking angle must be between -45 and 45 degrees: {banking}")
             track.add_segment("STRAIGHT", length, banking_angle=banking)
@@ -161,11 +160,8 @@ def load_track(file_path: str) -> Track:
         elif cmd in ("LEFT", "RIGHT"):
             if len(parts) < 3 or len(parts) > 4:
                 raise ValueError(f"{cmd} command requires 2-3 arguments (angle, radius [, banking]): {line}")
-            try:
-                angle, radius = float(parts[1]), float(parts[2])
-                banking = float(parts[3]) if len(parts) == 4 else 0.0
-            except ValueError:
-                raise ValueError(f"Invalid numeric values for {cmd} command: {parts[1:]}")
+            angle, radius = float(parts[1]), float(parts[2])      # float()'s own error, as above (:396-400)
+            banking = float(parts[3]) if len(parts) == 4 else 0.0
             if angle <= 0 or angle > 360:
                 raise ValueError(f"Curve angle must be between 0 and 360 degrees: {angle}")
             if radius <= 0:

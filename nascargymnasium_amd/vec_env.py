@@ -59,6 +59,9 @@ def _filled(name):
 
     def method(self, *args, **kwargs):
         self._fill()
+        for a in args:          # list's C methods read another list's storage directly: fill a lazy operand too
+            if isinstance(a, _LazyInfos):
+                a._fill()
         return base(self, *args, **kwargs)
     method.__name__ = name
     return method

@@ -181,3 +181,8 @@ def test_lazy_infos_fill_on_any_access():
     x = mk(); x.append({"b": 2}); assert len(x) == 4 and x[3] == {"b": 2}
     assert pickle.loads(pickle.dumps(mk())) == want
     assert bool(mk()) and mk() * 2 == want * 2
+    # two lazy operands: the other one is filled too (list's C methods read its storage directly)
+    assert mk() == mk() and not (mk() != mk()) and want == mk()
+    assert mk() + mk() == want * 2
+    y = mk(); y.extend(mk()); assert y == want * 2
+    z = mk(); z += mk(); assert z == want * 2

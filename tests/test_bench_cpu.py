@@ -50,3 +50,44 @@ def test_stagger_schedule_spreads_env_ages():
 
 def test_throughput_is_whole_job():
     assert bench.throughput(8, 8192, 10, 200, 0.02) == 8 * 8192 * 10 * 200 / 0.02
+
+
+def _bench(args, env=None, timeout=240):
+    import os
+    import subprocess
+    import sys
+    e = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        e.pop(k, None)
+    e.update(env or {})
+    return subprocess.run([sys.executable, os.path.join(bench.ROOT, "bench.py")] + args, cwd=bench.ROOT, env=e,
+                          capture_output=True, text=True, timeout=timeout)
+
+
+def test_gpus_n_launches_n_ranks():
+    """`bench.py --gpus 2` outside torchrun starts 2 ranks itself (torch.distributed.run child, gloo in --plumbing);
+    rank 0's line has n_gpus = world = 2, the MAX over the ranks' timings, and the whole-job value from it."""
+    import json
+    K, E, C = 6, 16, 10
+    r = _bench(["--gpus", "2", "--plumbing", "--steps", str(K), "--warmup", "0", "--envs", str(E), "--cars", str(C)])
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout          # rank 0 only
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["ranks"]["world_size"] == 2 and d["ranks"]["backend"] == "gloo"
+    el = d["ranks"]["elapsed_s"]
+    assert len(el) == 2 and max(el) >= K * 2e-3          # rank 1 sleeps 2 ms per step
+    assert np.isclose(d["ms_per_step"], max(el) / K * 1e3)
+    assert np.isclose(d["value"], 2 * E * C * K / max(el))
+
+
+def test_world_size_mismatch_is_an_error():
+    """launched as 2 ranks but told --gpus 1 (or the reverse): exit non-zero before any process group forms"""
+    r = _bench(["--gpus", "1", "--plumbing", "--steps", "1"], env={"WORLD_SIZE": "2", "RANK": "0", "LOCAL_RANK": "0"},
+               timeout=60)
+    assert r.returncode == 2 and "WORLD_SIZE=2" in r.stderr
+
+
+def test_host_cores_reports_the_cpu():
+    n, txt = bench.host_cores()
+    assert n >= 1 and "affinity" in txt and f"{n} threads used" in txt

@@ -3,14 +3,18 @@
 * cfg5 -- mixed batch of all 8 .track files at 10 cars per env: every env equals the oracle on its own track,
   every step, under the bench's closed-loop noisy driver with staggered masked resets and in-launch auto-reset
   (reference: the per-env track of src/car_env.py:243-303 / 375-394).
-* the bench workload over a whole episode: 16 x 10 daytona, noisy driver, >= 10 810 steps, so every env age the
-  bench's steady-state window holds (0 .. 10 800 steps, src/car_env.py:1154) is pinned against the oracle.
+* the bench workload over a whole episode: 48 x 10 daytona at the bench's 12 envs per workgroup (and at 1), noisy
+  driver, >= 10 810 steps, so every env age the bench's steady-state window holds (0 .. 10 800 steps,
+  src/car_env.py:1154) is pinned against the oracle at the layout the bench runs.
+* cfg2's shape (1 car per env) at cfg2's layout (8 envs per workgroup) and at 128 and 1.
 * cfg3's build-only car-car contact extension at its own shape (talladega x 10 cars, >= 256 envs): impulses
   reported, sharded rollout == per-step path, and switched off it equals a reference-behaviour engine from the same
   state.  No reference counterpart exists (src/constants/physics.py:9: every car has its own b2World), so this row
   is property-tested only.
 
-The GPU runs nascar_step_driven (the device driver inside model_kernel, the bench's per-step path; the sharded
+Every oracle comparison runs one GPU engine per workgroup layout (tests/closed_loop.py): the wave-cooperative
+SolveTOI / event manifolds, per-lane LDS contact slots and the logic kernel's LDS env passes then run with several
+envs' cars sharing a wave, as in the bench.  The GPU runs nascar_step_driven (the device driver inside model_kernel, the bench's per-step path; the sharded
 rollout equals it bit for bit, tests/test_gpu_rollout.py); the oracle groups step on host threads.
 """
 import os
@@ -18,94 +22,72 @@ import os
 import numpy as np
 import pytest
 
+from closed_loop import closed_loop_vs_oracle, make_envs
 from golden_replay import TRACKS
 
 pytestmark = pytest.mark.gpu
 torch = pytest.importorskip("torch")
 
 
-def _closed_loop_vs_oracle(env, orc, steps, seed, stagger):
-    """Drive `env` (BatchedCarEnv) with device policy 3 and `orc` (OracleGroups) with the host restatement of the
-    same driver; compare every step.  stagger: {step: env} masked resets.  Returns event tallies."""
-    from drivers import NoisyRuleDriver
-    E, C = env.E, env.C
-    drv = NoisyRuleDriver(E * C, seed=seed)
-    g = env.reset().cpu().numpy()
-    oo = orc.reset()[0]
-    assert np.array_equal(g, oo), "reset obs"
-    t = dict(contact=0, disabled=0, resets=0, laps=0, reasons=set(), max_age=0)
-    age = np.zeros(E, np.int64)
-    for k in range(steps):
-        if k in stagger:
-            e = stagger[k]
-            m = torch.zeros(E, dtype=torch.uint8, device=env.device)
-            m[e] = 1
-            env.reset(m)
-            orc.reset([e])
-            oo = orc.outputs()[0]
-            age[e] = 0
-        env.step_driven(3, seed=seed, step=k, auto_reset=True)
-        oo, orw, ocf, oef = orc.step(drv.actions(oo, k))
-        gr, gcf, gef = env.reward.cpu().numpy(), env.car_flags.cpu().numpy(), env.env_flags.cpu().numpy()
-        assert np.array_equal(gr, orw), f"step {k}: reward mismatch at {np.argwhere(gr != orw)[:5].tolist()}"
-        assert np.array_equal(gcf & 1, ocf & 1), f"step {k}: disabled flags"
-        done = (oef[:, 0] != 0) | (oef[:, 1] != 0)
-        assert np.array_equal((gef & 3) != 0, done), f"step {k}: done flags"
-        assert np.array_equal(((gef >> 4) & 7)[done], oef[done, 2]), f"step {k}: termination reasons"
-        age += 1
-        if done.any():
-            t["reasons"] |= set(oef[done, 2].tolist())
-            t["max_age"] = max(t["max_age"], int(age[done].max()))
-            orc.reset(np.nonzero(done)[0])
-            oo = orc.outputs()[0]
-            t["resets"] += int(done.sum())
-            age[done] = 0
-        go = env.obs.cpu().numpy()
-        bad = np.argwhere(go != oo)
-        assert len(bad) == 0, f"step {k}: obs mismatch at {bad[:5].tolist()} gpu {go[tuple(bad[0])]} oracle {oo[tuple(bad[0])]}"
-        t["contact"] += int(((gcf & 4) != 0).sum())
-        t["disabled"] += int(((gcf & 2) != 0).sum())
-        t["laps"] += int(((gcf & 8) != 0).sum())
-    t["max_age"] = max(t["max_age"], int(age.max()))
-    assert not (env.car_flags.cpu().numpy() & 128).any(), "contact buffer overflow"
-    return t
-
-
 @pytest.mark.timeout(900)
 def test_cfg5_mixed_tracks_10_cars_vs_oracle():
-    """cfg5 at its car count: 64 envs x 10 cars, env e on track e mod 8 (one launch, per-env track index), noisy
-    driver closed loop with staggered resets and in-launch auto-reset, 900 steps; each env == the oracle on its own
-    track every step (obs, rewards, disabled / done flags, termination reasons)."""
-    from nascargymnasium_amd.batched import BatchedCarEnv
+    """cfg5 at its car count: 128 envs x 10 cars, env e on track e mod 8 (one launch, per-env track index: 16 envs
+    per track), noisy driver closed loop with staggered resets and in-launch auto-reset, 900 steps; each env == the
+    oracle on its own track every step (obs, rewards, disabled / done flags, termination reasons), at one env per
+    workgroup and at the bench's 12 envs per workgroup (per track: one full 12-env workgroup and one of 4)."""
     from oracle_lib import OracleGroups
     tracks = sorted(f for f in os.listdir(TRACKS) if f.endswith(".track"))
-    E, C, S = 64, 10, 900
+    E, C, S = 128, 10, 900
     files = [os.path.join(TRACKS, tracks[e % 8]) for e in range(E)]
-    env = BatchedCarEnv(E, C, files, device="cuda:0")
+    envs = make_envs(E, C, files, [1, 12])
     orc = OracleGroups(files, C)
-    stagger = {11 * e: e for e in range(8, E)}        # envs 8.. reset at staggered steps (ages spread)
-    t = _closed_loop_vs_oracle(env, orc, S, seed=23, stagger=stagger)
-    env.close(); orc.close()
+    stagger = {7 * e: e for e in range(8, E)}        # envs 8.. reset at staggered steps (ages spread)
+    t = closed_loop_vs_oracle(envs, orc, S, seed=23, stagger=stagger)
+    for env in envs:
+        env.close()
+    orc.close()
     assert t["contact"] > 0 and t["disabled"] > 0, t
 
 
 @pytest.mark.timeout(1200)
 def test_bench_workload_full_episode_vs_oracle():
-    """The bench's steady-state workload over a whole episode: 16 x 10 daytona, noisy driver closed loop, staggered
-    resets (env e reset at step 600 e), in-launch auto-reset, 10 830 steps.  Env 0 is never reset by the schedule,
-    so unless an earlier termination ends it, it runs to the 10 800-step time limit (src/car_env.py:1154): every
-    env age the bench's window holds is compared with the oracle every step."""
-    from nascargymnasium_amd.batched import BatchedCarEnv
+    """The bench's steady-state workload over a whole episode at the bench's layout: 48 x 10 daytona at 12 envs per
+    workgroup (4 full workgroups, 120 live lanes in two waves each, as the bench's 8192 x 10 runs) and at one env per
+    workgroup, noisy driver closed loop inside model_kernel, staggered resets (env e reset at step 225 e, so the env
+    ages of every step spread over the episode as in the bench's settled window), in-launch auto-reset, 10 830 steps.
+    Env 0 is never reset by the schedule, so unless an earlier termination ends it, it runs to the 10 800-step time
+    limit (src/car_env.py:1154): every env age the bench's window holds is compared with the oracle every step."""
     from oracle_lib import OracleGroups
-    E, C, S = 16, 10, 10830
+    E, C, S = 48, 10, 10830
     path = os.path.join(TRACKS, "daytona.track")
-    env = BatchedCarEnv(E, C, path, device="cuda:0")
+    envs = make_envs(E, C, path, [12, 1])
     orc = OracleGroups([path] * E, C, shards=8)
-    stagger = {600 * e: e for e in range(1, E)}
-    t = _closed_loop_vs_oracle(env, orc, S, seed=31, stagger=stagger)
-    env.close(); orc.close()
+    stagger = {225 * e: e for e in range(1, E)}
+    t = closed_loop_vs_oracle(envs, orc, S, seed=31, stagger=stagger)
+    for env in envs:
+        env.close()
+    orc.close()
     assert t["contact"] > 0 and t["disabled"] > 0 and t["laps"] > 0, t
     assert 4 in t["reasons"] and t["max_age"] >= 10800, t      # an episode ran to the 10 800-step truncation
+
+
+@pytest.mark.timeout(600)
+def test_cfg2_one_car_layouts_vs_oracle():
+    """cfg2's shape (1 car per env) at cfg2's own layout: 256 envs x 1 car daytona at 8 envs per workgroup (what the
+    engine picks for 4096 x 1: 512 workgroups of 8 cars), at 128 envs per workgroup (two full waves per workgroup)
+    and at one env per workgroup; noisy driver closed loop, staggered resets, auto-reset, 2500 steps, == the oracle
+    every step."""
+    from oracle_lib import OracleGroups
+    E, C, S = 256, 1, 2500
+    path = os.path.join(TRACKS, "daytona.track")
+    envs = make_envs(E, C, path, [8, 128, 1])
+    orc = OracleGroups([path] * E, C, shards=4)
+    stagger = {9 * e: e for e in range(1, E)}
+    t = closed_loop_vs_oracle(envs, orc, S, seed=41, stagger=stagger)
+    for env in envs:
+        env.close()
+    orc.close()
+    assert t["contact"] > 0, t
 
 
 @pytest.mark.timeout(600)

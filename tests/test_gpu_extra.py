@@ -223,3 +223,31 @@ def test_full_size_batch_independence_and_determinism():
     assert torch.equal(full.get_state(), end)
     assert contacts > 0
     full.close(); sub.close()
+
+
+def test_envs_per_block_switch_mid_run():
+    """nascar_set_envs_per_block may change the workgroup layout between launches: an engine whose layout changes
+    every 100 steps (12 -> 5 -> 1 -> automatic) stays bit-identical to one at a fixed layout, per step and in its
+    final state; out-of-range layouts are rejected."""
+    from nascargymnasium_amd.batched import BatchedCarEnv
+    E, C = 60, 10
+    path = os.path.join(TRACKS, "daytona.track")
+    a = BatchedCarEnv(E, C, path, device="cuda:0", envs_per_block=12)
+    b = BatchedCarEnv(E, C, path, device="cuda:0", envs_per_block=3)
+    with pytest.raises(RuntimeError):
+        a.set_envs_per_block(13)          # 13 x 10 cars > 128 lanes
+    with pytest.raises(RuntimeError):
+        a.set_envs_per_block(-1)
+    assert a.envs_per_block == 12
+    a.reset(); b.reset()
+    for k in range(400):
+        if k % 100 == 0 and k:
+            a.set_envs_per_block({1: 5, 2: 1, 3: 0}[k // 100])
+        a.step_driven(3, seed=9, step=k, auto_reset=True)
+        b.step_driven(3, seed=9, step=k, auto_reset=True)
+        assert torch.equal(a.obs, b.obs) and torch.equal(a.reward, b.reward), k
+        assert torch.equal(a.env_flags, b.env_flags), k
+    assert a.envs_per_block == 1     # automatic for 60 envs: spread to one env per workgroup
+    a.rollout(3, 100, seed=9, step0=400); b.rollout(3, 100, seed=9, step0=400)
+    assert torch.equal(a.obs, b.obs) and torch.equal(a.get_state(), b.get_state())
+    a.close(); b.close()

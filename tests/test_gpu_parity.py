@@ -55,11 +55,12 @@ INFO_MAP = [(0, "lap_count"), (1, "last_lap_time"), (2, "best_lap_time"), (3, "i
 
 @pytest.mark.parametrize("name", scenarios())
 def test_golden_trace_gpu(name):
-    """Reference golden trace replayed on the GPU; 4 identical env copies (exercises the block map)."""
+    """Reference golden trace replayed on the GPU; 4 identical env copies in 2 workgroups of 2 envs each
+    (exercises the block map and envs sharing a workgroup)."""
     from nascargymnasium_amd import _lib
     d = load(name)
     C = int(d["C"]); E = 4
-    env = _env(str(d["track"]), E, C, bool(d["reset_on_lap"]), **start_kwargs(d))
+    env = _env(str(d["track"]), E, C, bool(d["reset_on_lap"]), envs_per_block=2, **start_kwargs(d))
     env.set_perf_history(True)
     obs0 = env.reset().cpu().numpy()
     for e in range(E):
@@ -119,29 +120,35 @@ def _random_actions(rng, E, C, k):
                                               ("talladega.track", 16, 10, 600), ("michigan.track", 40, 1, 1200),
                                               ("daytona.track", 64, 4, 1000)])   # cfg4's car count
 def test_random_batch_vs_oracle(track, E, C, steps):
-    """Seeded random driving (crashes, disables, stuck cars) on E x C cars: GPU == CPU oracle, every step."""
+    """Seeded random driving (crashes, disables, stuck cars) on E x C cars: GPU == CPU oracle, every step, at one
+    env per workgroup and at the most envs a workgroup holds (128 // C: e.g. daytona 64 x 4 at 32 envs per
+    workgroup), the same actions into both engines."""
     from oracle_lib import OracleEnv
     rng = np.random.default_rng(hash(track) % 2**32)
-    env = _env(track, E, C)
+    envs = [_env(track, E, C, envs_per_block=epb) for epb in (1, 128 // C)]
     orc = OracleEnv(os.path.join(TRACKS, track), E, C)
-    g = env.reset().cpu().numpy()
     o = orc.reset()[0]
-    assert np.array_equal(g, o)
+    for env in envs:
+        assert np.array_equal(env.reset().cpu().numpy(), o)
     n_collide = 0
     for k in range(steps):
         a = _random_actions(rng, E, C, k)
-        go, gr, gt, gtr = env.step(torch.from_numpy(a).cuda())
+        ta = torch.from_numpy(a).cuda()
         oo, orw, ocf, oef = orc.step(a)
-        go, gr = go.cpu().numpy(), gr.cpu().numpy()
-        bad = np.argwhere(~((go == oo) | (np.isnan(go) & np.isnan(oo))))
-        assert len(bad) == 0, f"step {k}: obs mismatch at {bad[:5].tolist()}: gpu {go[tuple(bad[0])]} oracle {oo[tuple(bad[0])]}"
-        assert np.array_equal(gr, orw), f"step {k}: reward mismatch"
-        assert np.array_equal(gt.cpu().numpy(), oef[:, 0] != 0) and np.array_equal(gtr.cpu().numpy(), oef[:, 1] != 0)
-        assert np.array_equal((env.car_flags.cpu().numpy() & 1), ocf & 1)
-        n_collide += int(((env.car_flags & 4) != 0).sum())
+        for env in envs:
+            go, gr, gt, gtr = env.step(ta)
+            lay = f"envs per block {env.envs_per_block}"
+            go, gr = go.cpu().numpy(), gr.cpu().numpy()
+            bad = np.argwhere(~((go == oo) | (np.isnan(go) & np.isnan(oo))))
+            assert len(bad) == 0, f"step {k} ({lay}): obs mismatch at {bad[:5].tolist()}: gpu {go[tuple(bad[0])]} oracle {oo[tuple(bad[0])]}"
+            assert np.array_equal(gr, orw), f"step {k} ({lay}): reward mismatch"
+            assert np.array_equal(gt.cpu().numpy(), oef[:, 0] != 0) and np.array_equal(gtr.cpu().numpy(), oef[:, 1] != 0)
+            assert np.array_equal((env.car_flags.cpu().numpy() & 1), ocf & 1)
+        n_collide += int(((envs[0].car_flags & 4) != 0).sum())
     assert n_collide > 0, "scenario exercised no wall contact"
-    assert not (env.car_flags.cpu().numpy() & 128).any(), "contact buffer overflow"
-    env.close()
+    for env in envs:
+        assert not (env.car_flags.cpu().numpy() & 128).any(), "contact buffer overflow"
+        env.close()
 
 
 def test_auto_reset_and_terminal_obs():
@@ -229,47 +236,19 @@ def test_device_rule_driver_matches_reference_controller(name, car):
 
 
 def test_noisy_driver_closed_loop_vs_oracle():
-    """The bench's steady-state workload in miniature: device noisy rule driver (policy 3) in closed loop with
-    in-launch auto-reset and staggered masked resets, 16 envs x 10 cars on daytona for 2400 steps.  Every
-    step: device actions == the host restatement (tests/drivers.py), and obs / rewards / flags == the oracle
-    (which resets the same envs).  Asserts that wall contact, a disable and an env reset all happened."""
-    from drivers import NoisyRuleDriver
-    from oracle_lib import OracleEnv
-    E, C, S = 16, 10, 2400
-    env = _env("daytona.track", E, C)
-    orc = OracleEnv(os.path.join(TRACKS, "daytona.track"), E, C)
-    env.reset()
-    oo = orc.reset()[0]
-    drv = NoisyRuleDriver(E * C, seed=7)
-    stagger = {150 * e: e for e in range(1, E)}        # env e reset at step 150 e (ages spread)
-    n_contact = n_disabled = n_reset = 0
-    for k in range(S):
-        if k in stagger:
-            e = stagger[k]
-            m = torch.zeros(E, dtype=torch.uint8, device="cuda"); m[e] = 1
-            env.reset(m)
-            orc.reset(e)
-            oo = orc.outputs()[0]
-        ga = env.policy_actions(3, seed=7, step=k).clone()
-        ha = drv.actions(oo, k)
-        assert np.array_equal(ga.cpu().numpy().reshape(-1, 2), ha), f"step {k}: driver actions differ"
-        env.launch_step(ga, auto_reset=True)
-        oo, orw, ocf, oef = orc.step(ha)
-        gr, gcf, gef = env.reward.cpu().numpy(), env.car_flags.cpu().numpy(), env.env_flags.cpu().numpy()
-        assert np.array_equal(gr, orw), f"step {k}: reward mismatch"
-        assert np.array_equal(gcf & 1, ocf & 1), f"step {k}: disabled flags"
-        done = (oef[:, 0] != 0) | (oef[:, 1] != 0)
-        assert np.array_equal((gef & 3) != 0, done), f"step {k}: done flags"
-        for e in np.nonzero(done)[0]:
-            orc.reset(int(e))
-        if done.any():
-            oo = orc.outputs()[0]
-            n_reset += int(done.sum())
-        go = env.obs.cpu().numpy()
-        bad = np.argwhere(go != oo)
-        assert len(bad) == 0, f"step {k}: obs mismatch at {bad[:5].tolist()}"
-        n_contact += int((gcf & 4).astype(bool).sum())
-        n_disabled += int((gcf & 2).astype(bool).sum())
-    assert n_contact > 0 and n_disabled > 0, (n_contact, n_disabled)
-    assert not (env.car_flags.cpu().numpy() & 128).any()
-    env.close()
+    """The bench's steady-state workload in miniature at the bench's layout: device noisy rule driver (policy 3) in
+    closed loop with in-launch auto-reset and staggered masked resets, 48 envs x 10 cars on daytona for 2400 steps,
+    at 12 envs per workgroup (4 full workgroups, as the bench's 8192 x 10) and at 1.  Every step: device actions ==
+    the host restatement (tests/drivers.py), and obs / rewards / flags == the oracle (which resets the same envs).
+    Asserts that wall contact, a disable and an env reset all happened."""
+    from closed_loop import closed_loop_vs_oracle
+    from oracle_lib import OracleGroups
+    E, C, S = 48, 10, 2400
+    envs = [_env("daytona.track", E, C, envs_per_block=epb) for epb in (12, 1)]
+    orc = OracleGroups([os.path.join(TRACKS, "daytona.track")] * E, C, shards=8)
+    stagger = {50 * e: e for e in range(1, E)}        # env e reset at step 50 e (ages spread)
+    t = closed_loop_vs_oracle(envs, orc, S, seed=7, stagger=stagger, check_actions=True)
+    for env in envs:
+        env.close()
+    orc.close()
+    assert t["contact"] > 0 and t["disabled"] > 0 and t["resets"] > 0, t

@@ -12,10 +12,10 @@ pytestmark = pytest.mark.gpu
 torch = pytest.importorskip("torch")
 
 
-def _engine(tracks, E, C, reset_on_lap=False):
+def _engine(tracks, E, C, reset_on_lap=False, envs_per_block=None):
     from nascargymnasium_amd.batched import BatchedCarEnv
     files = [os.path.join(TRACKS, tracks[e % len(tracks)]) for e in range(E)]
-    return BatchedCarEnv(E, C, files, reset_on_lap=reset_on_lap, device="cuda:0")
+    return BatchedCarEnv(E, C, files, reset_on_lap=reset_on_lap, device="cuda:0", envs_per_block=envs_per_block)
 
 
 def _per_step(env, policy, seed, step0, K):
@@ -28,16 +28,20 @@ def _per_step(env, policy, seed, step0, K):
 
 
 @pytest.mark.parametrize("streams", [4, 0])        # sharded rollout (default) / fused rollout kernel
-@pytest.mark.parametrize("tracks,E,C,policy,warm,K", [
-    (["daytona.track"], 48, 10, 3, 600, 900),          # the bench workload: noisy driver, contacts
-    (["daytona.track"], 16, 2, 1, 0, 400),             # rule driver from reset
-    (["martinsville.track"], 32, 4, 0, 3500, 300),     # uniform, reset_on_lap: the t > 60 s termination + auto-reset
-    (["talladega.track", "michigan.track", "nascar2.track", "trioval.track"], 40, 3, 3, 900, 600),   # mixed tracks
-    (["daytona.track", "nascar.track"], 500, 10, 3, 1200, 200),   # 42 workgroups: uneven shards, 2 track groups
+@pytest.mark.parametrize("tracks,E,C,policy,warm,K,epb", [
+    (["daytona.track"], 48, 10, 3, 600, 900, 12),      # the bench workload and layout: noisy driver, contacts
+    (["daytona.track"], 16, 2, 1, 0, 400, None),       # rule driver from reset
+    (["martinsville.track"], 32, 4, 0, 3500, 300, 8),  # uniform, reset_on_lap: the t > 60 s termination + auto-reset
+    (["talladega.track", "michigan.track", "nascar2.track", "trioval.track"], 40, 3, 3, 900, 600, None),   # mixed tracks
+    # 12 envs per workgroup: 2 track groups of 250 envs = 2 x 21 workgroups (the last of each with 10 envs), 3 uneven
+    # shards of 14 workgroups
+    (["daytona.track", "nascar.track"], 500, 10, 3, 1200, 200, 12),
 ])
-def test_rollout_equals_per_step(tracks, E, C, policy, warm, K, streams):
+def test_rollout_equals_per_step(tracks, E, C, policy, warm, K, epb, streams):
+    """the per-step path at the automatic layout (one env per workgroup for these batch sizes) against the
+    rollout at `epb` envs per workgroup: the same results whatever the schedule and the layout"""
     rol = policy == 0
-    a, b = _engine(tracks, E, C, rol), _engine(tracks, E, C, rol)
+    a, b = _engine(tracks, E, C, rol), _engine(tracks, E, C, rol, envs_per_block=epb)
     b.set_rollout_streams(streams if E < 500 or streams == 0 else 3)
     a.reset()
     if warm:                                    # leave the reset state first (cars spread, contacts active)
@@ -78,7 +82,7 @@ def test_rollout_last_step_outputs_and_errors():
 
 
 @pytest.mark.parametrize("tracks,E,precision", [
-    (["daytona.track"], 480, "fp32"),            # 40 workgroups: 4 shards, each its own actor launch
+    (["daytona.track"], 480, "fp32"),            # 40 workgroups of 12 envs: 4 shards, each its own actor launch
     (["daytona.track"], 480, "bf16"),
     (["daytona.track", "nascar.track"], 96, "fp32"),   # non-identity block map: one shard
 ])
@@ -87,7 +91,7 @@ def test_sharded_rollout_sac_equals_per_step(tracks, E, precision):
     batch (nascar_policy_actions) + nascar_step."""
     from nascargymnasium_amd.policy import random_actor
     C, warm, K = 10, 300, 150
-    a, b = _engine(tracks, E, C), _engine(tracks, E, C)
+    a, b = _engine(tracks, E, C), _engine(tracks, E, C, envs_per_block=12)
     for e in (a, b):
         e.set_actor(random_actor(3), precision=precision)
     a.reset()

@@ -33,6 +33,17 @@ def test_loader_errors(tmp_path):
     p.write_text("GRID\nLEFT 400 100\n")
     with pytest.raises(ValueError, match="Curve angle"):
         load_track(str(p))
+    # non-numeric arguments: Python's own float() message, as the reference re-raises it (its "invalid literal"
+    # re-wrap never matches a float() error; src/track_generator.py:370-374, 396-400); upper-cased like the line
+    p.write_text("GRID\nSTRAIGHT ten\n")
+    with pytest.raises(ValueError, match=r"^could not convert string to float: 'TEN'$"):
+        load_track(str(p))
+    p.write_text("GRID\nRIGHT 90 wide 3\n")
+    with pytest.raises(ValueError, match=r"^could not convert string to float: 'WIDE'$"):
+        load_track(str(p))
+    p.write_text("GRID\nSTRAIGHT 100 60\n")
+    with pytest.raises(ValueError, match="Banking angle must be between -45 and 45 degrees: 60.0"):
+        load_track(str(p))
     p.write_text("grid  # comment\nstartline\nstraight 10 5 # banked\n")
     t = load_track(str(p))
     assert [s.segment_type for s in t.segments] == ["GRID", "STARTLINE", "STRAIGHT"]
