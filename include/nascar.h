@@ -116,6 +116,18 @@ int nascar_get_rollout_streams(NascarHandle* h);
 int nascar_set_envs_per_block(NascarHandle* h, int32_t epb);
 int nascar_get_envs_per_block(NascarHandle* h);
 
+/* Lanes per car of the distance-sensor kernel (no reference counterpart: DistanceSensor casts its 16 rays one after
+ * another, src/distance_sensor.py:93-115): 4 (each lane walks rays r, r + 4, r + 8, r + 12) or 16 (one ray per
+ * lane, for small batches that leave most of the chip idle); 0 = automatic (16 up to 16 384 cars, else 4).
+ * Identical results either way. */
+int nascar_set_sensor_lanes(NascarHandle* h, int32_t lanes);
+
+/* Cell size (m) of the distance sensors' beam lists for the tracks added to this handle AFTER the call (host-built
+ * per track in nascar_add_track; no reference counterpart -- DistanceSensor ray-casts against every wall,
+ * src/distance_sensor.py:93-115).  Default 1 m (or NASCAR_BEAM_CELL): ~0.8 GB of device lists and ~2 s of host build
+ * per track; 2 m quarters both for slightly longer list walks.  Range [0.5, 8].  Identical results at any size. */
+int nascar_set_beam_cell(NascarHandle* h, float meters);
+
 /* Profiling hook (no reference counterpart; bench.py's per-kernel roofline): events = 4 caller-created timing
  * events (hipEvent_t), recorded by every following whole-grid step (nascar_step / nascar_step_driven) on its
  * stream before model_kernel, after model_kernel, after logic_kernel and after the sensor launch; n = 0 stops.
@@ -162,7 +174,8 @@ int nascar_set_actor(NascarHandle* h, const float* w1, const float* b1, const fl
                      const float* w3, const float* b3, int32_t obs_dim, int32_t hidden, int32_t act_dim);
 /* Actor arithmetic for policy 2 and nascar_actor_forward: 1 (default) = float32 throughout (the reference's
  * model.predict precision; <= 1e-5 on the reference's sac_1235 checkpoint, tests/test_gpu_actor.py), 0 = the
- * bf16-operand MFMA kernel (fp32 accumulation; ~5x faster, max |delta action| 0.40 on sac_1235). */
+ * bf16-operand MFMA kernel (fp32 accumulation; ~8x faster: 16.2 vs 135 us at 81 920 observations, max |delta action|
+ * 0.40 on sac_1235). */
 int nascar_set_actor_precision(NascarHandle* h, int32_t fp32);
 /* The loaded actor on any device batch: obs [n][38] float32 -> actions [n][2] float32 (both 8-byte aligned). */
 int nascar_actor_forward(NascarHandle* h, const float* obs, int32_t n, float* actions, void* stream);

@@ -29,12 +29,14 @@ class BatchedCarEnv:
 
     track_file: one track (name or path) for all envs, or a sequence of E tracks
     (per-env track index; envs are grouped per track into workgroups).
+    envs_per_block / beam_cell: scheduling and memory choices with identical results (set_envs_per_block;
+    nascar_set_beam_cell: the distance sensors' beam-list cell size in m, default 1).
     """
 
     def __init__(self, num_envs: int, num_cars: int = 1, track_file: Union[str, Sequence[str]] = "daytona",
                  reset_on_lap: bool = False, device: Union[str, int, torch.device] = "cuda",
                  start_position=None, start_angle: float = 0.0, perf_history: bool = False,
-                 envs_per_block: Optional[int] = None):
+                 envs_per_block: Optional[int] = None, beam_cell: Optional[float] = None):
         if not torch.cuda.is_available():
             raise RuntimeError("BatchedCarEnv needs a HIP device (torch.cuda.is_available() is False); "
                                "the product path has no CPU fallback")
@@ -59,6 +61,8 @@ class BatchedCarEnv:
         self.h = h
         if envs_per_block is not None:
             self.set_envs_per_block(envs_per_block)
+        if beam_cell is not None:     # before the tracks are added: their beam lists are built at this cell size
+            _lib.check(self.L.nascar_set_beam_cell(self.h, float(beam_cell)))
         self.tracks, self._track_id = [], {}
         for p in uniq:
             self._add_track(p)
@@ -99,6 +103,11 @@ class BatchedCarEnv:
     @property
     def envs_per_block(self) -> int:
         return int(self.L.nascar_get_envs_per_block(self.h))
+
+    def set_sensor_lanes(self, lanes: int = 0):
+        """Lanes per car of the distance-sensor kernel: 4 or 16 (one ray per lane), 0 automatic (16 for batches of
+        up to 16 384 cars).  Identical results; a scheduling choice."""
+        _lib.check(self.L.nascar_set_sensor_lanes(self.h, int(lanes)))
 
     def set_perf_history(self, enable: bool = True):
         """Keep Car.velocity_history on the device so the info's `performance` dict is Car.validate_performance
@@ -272,7 +281,7 @@ class BatchedCarEnv:
     def set_actor(self, weights, precision: str = "fp32"):
         """Load an SB3 SAC MlpPolicy actor: a dict from nascargymnasium_amd.policy.load_sb3_actor / random_actor.
         precision "fp32" (default): float32 throughout, the reference's model.predict precision (<= 1e-5 on the
-        reference's sac_1235 checkpoint); "bf16": the MFMA kernel (bf16 operands, fp32 accumulation), ~5x faster but
+        reference's sac_1235 checkpoint); "bf16": the MFMA kernel (bf16 operands, fp32 accumulation), ~8x faster but
         NOT faithful for trained policies (max |delta action| 0.40 on sac_1235)."""
         from .policy import actor_arrays
         if precision not in ("bf16", "fp32"):

@@ -694,7 +694,18 @@ struct ToiWaveLDS { float4 sw0[64], sw1[64]; int2 job[TOI_JOBCAP]; float res[TOI
 struct ManiWaveLDS { float4 xf[64]; int2 job[MANI_JOBCAP]; ManiRes res[MANI_JOBCAP]; };
 #define BP_JOBCAP 128     // broadphase candidate tests per wave and round
 struct BpWaveLDS { float4 fat[64]; int2 job[BP_JOBCAP]; unsigned int hit[64][2]; };
-union WaveLDS { ToiWaveLDS toi; ManiWaveLDS mani; BpWaveLDS bp; };
+// b2ContactSolver constraint of one (car, wall) contact (register-resident for small islands; see solve_island)
+struct VCP { V2 rA, rB; float ni, ti, nm, tm, vb; };
+struct VC {
+  VCP p[2]; V2 normal; float nm[4]; float K[4]; int pointCount;
+  V2 cB; float aB; V2 vB; float wB;
+  V2 ln, lp, lps[2]; int pcount, type, ci;
+  Rot qB; uint32_t aB0;   // the static wall's b2Rot (its body transform) and the angle bits it was set from
+};
+// the general (more than ISLAND_MID contacts) island's constraints, one lane at a time (solve_island_general)
+struct IslandWaveLDS { VC vc[MAX_ISLAND]; };
+union WaveLDS { ToiWaveLDS toi; ManiWaveLDS mani; BpWaveLDS bp; IslandWaveLDS island; };
+static_assert(sizeof(IslandWaveLDS) <= sizeof(ToiWaveLDS), "the island area must not grow the wave's LDS work area");
 __shared__ WaveLDS g_wave_lds[SBLOCK / 64];   // model_kernel / rollout_kernel (the Box2D step)
 __device__ __forceinline__ void wave_lds_sync() {   // a wave's LDS writes visible to its later LDS reads
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -726,13 +737,6 @@ __device__ inline void collide(Car& c, const WallSet& S) {
 }
 
 // ------------------------------------------------------------------ b2ContactSolver
-struct VCP { V2 rA, rB; float ni, ti, nm, tm, vb; };
-struct VC {
-  VCP p[2]; V2 normal; float nm[4]; float K[4]; int pointCount;
-  V2 cB; float aB; V2 vB; float wB;
-  V2 ln, lp, lps[2]; int pcount, type, ci;
-  Rot qB; uint32_t aB0;   // the static wall's b2Rot (its body transform) and the angle bits it was set from
-};
 // b2Rot::Set(aB) of the static body B inside the solvers: B never moves (mB = iB = 0), so aB keeps the wall's angle
 // bit for bit and its rotation is the wall's body transform (glibc sinf/cosf of that same float, computed when the
 // wall was created) -- no sincosf per solver point.  Any other angle (only possible through non-finite impulses)
@@ -1033,8 +1037,8 @@ __device__ __forceinline__ void island_push(int cidx[MAX_ISLAND], int& n, int i)
 // the island solve of b2World::Solve for n touching contacts; NMAX >= n contact constraints in registers (the
 // common islands of 1-2 contacts; a larger bound would sit in scratch memory)
 template <int NMAX>
-__device__ __forceinline__ int solve_island(Car& c, const LWall* W, const int* cidx, int n, float dt, float dtRatio,
-                                            float friction) {
+__device__ __forceinline__ int solve_island_buf(Car& c, const LWall* W, const int* cidx, int n, float dt, float dtRatio,
+                                                float friction, VC* vc) {
   float h = dt;
   BodyState A;
   c.c0 = c.c; c.a0 = c.a;
@@ -1045,7 +1049,6 @@ __device__ __forceinline__ int solve_island(Car& c, const LWall* W, const int* c
     wv += h * CAR_INV_I * c.torque;
     A.c = c.c; A.a = c.a; A.v = v; A.w = wv;
   }
-  VC vc[NMAX];
   cs_init<NMAX>(vc, n, c, cidx, W, true, dtRatio);
   cs_init_velocity<NMAX>(vc, n, c, A);
   cs_warm_start<NMAX>(vc, n, A);
@@ -1059,6 +1062,41 @@ __device__ __forceinline__ int solve_island(Car& c, const LWall* W, const int* c
   c.xf.q = rot_cached(rcA, c.a); c.xf.p = vsub(c.c, rmul(c.xf.q, zero2()));   // sync_transform
   report<NMAX>(c, vc, n);
   return positionSolved;
+}
+template <int NMAX>
+__device__ __forceinline__ int solve_island(Car& c, const LWall* W, const int* cidx, int n, float dt, float dtRatio,
+                                            float friction) {
+  VC vc[NMAX];   // small islands: fully unrolled, register-resident
+  return solve_island_buf<NMAX>(c, W, cidx, n, dt, dtRatio, friction, vc);
+}
+// The general island (more than ISLAND_MID touching contacts) indexes its constraints dynamically; as a private
+// array they would live in scratch memory (1.6 KB per lane, a vector-memory round trip per field use).  Instead
+// the wave's LDS work area (free during b2World::Solve and an event's island solve) holds them, one lane at a time
+// -- the lowest lane of the wave still waiting goes next.  Divergent lanes of a wave run one after another anyway,
+// so serialising them costs nothing over the private-array form; every access is an LDS round trip.
+#ifndef ISLAND_LDS
+#define ISLAND_LDS 1
+#endif
+template <typename F>
+__device__ __forceinline__ void wave_lds_one_at_a_time(F&& body) {
+  unsigned long long pending = __ballot(1);   // the lanes of this wave executing this call
+  wave_lds_sync();                            // earlier LDS reads of the work area (any lane) done before its reuse
+  while (pending) {                           // wave-uniform
+    const int leader = __ffsll((long long)pending) - 1;
+    if ((int)__lane_id() == leader) body((VC*)g_wave_lds[threadIdx.x >> 6].island.vc);
+    pending &= pending - 1;
+    wave_lds_sync();
+  }
+}
+__device__ __forceinline__ int solve_island_general(Car& c, const LWall* W, const int* cidx, int n, float dt,
+                                                   float dtRatio, float friction) {
+#if ISLAND_LDS
+  int r = 0;
+  wave_lds_one_at_a_time([&](VC* vc) { r = solve_island_buf<MAX_ISLAND>(c, W, cidx, n, dt, dtRatio, friction, vc); });
+  return r;
+#else
+  return solve_island<MAX_ISLAND>(c, W, cidx, n, dt, dtRatio, friction);
+#endif
 }
 
 // b2BroadPhase::UpdatePairs of b2World::Solve for every lane of the wave at once (round 3).  A moved car's grid
@@ -1139,14 +1177,17 @@ __device__ inline void solve(Car& c, const WallSet& S, float dt, float dtRatio, 
     island_push(cidx, n, i);
   }
   const float h = dt;
+  CCOUNT(c, 26, n);   // profile builds: the island's touching contacts and its solve cycles (slot 25)
+  CTIME_BEGIN();
 #if ISLAND_MID
   const int positionSolved = n <= 2 ? solve_island<2>(c, W, cidx, n, dt, dtRatio, friction)
                            : n <= ISLAND_MID ? solve_island<ISLAND_MID>(c, W, cidx, n, dt, dtRatio, friction)
-                                             : solve_island<MAX_ISLAND>(c, W, cidx, n, dt, dtRatio, friction);
+                                             : solve_island_general(c, W, cidx, n, dt, dtRatio, friction);
 #else
   const int positionSolved = n <= 2 ? solve_island<2>(c, W, cidx, n, dt, dtRatio, friction)
                                     : solve_island<MAX_ISLAND>(c, W, cidx, n, dt, dtRatio, friction);
 #endif
+  CTIME_END(c, 25);
   {
     float minSleepTime = FLT_BIG;
     const float linTolSqr = LINEAR_SLEEP_TOL * LINEAR_SLEEP_TOL;
@@ -1457,9 +1498,9 @@ __device__ inline float time_of_impact(int* state, const Poly* pA, const Sweep& 
 }
 
 template <int NMAX>
-__device__ __forceinline__ void island_solve_toi_n(Car& c, const LWall* W, const int* cidx, int n, float subdt, float friction) {
+__device__ __forceinline__ void island_solve_toi_buf(Car& c, const LWall* W, const int* cidx, int n, float subdt, float friction,
+                                                     VC* vc) {
   BodyState A; A.c = c.c; A.a = c.a; A.v = c.v; A.w = c.w;
-  VC vc[NMAX];
   cs_init<NMAX>(vc, n, c, cidx, W, false, 1.0f);
   RotCache rcA; rcA.bits = __float_as_uint(c.a) ^ 1u; rcA.q.s = 0.0f; rcA.q.c = 1.0f;   // (empty: no angle matches)
   {
@@ -1477,12 +1518,21 @@ __device__ __forceinline__ void island_solve_toi_n(Car& c, const LWall* W, const
   c.xf.q = rot_cached(rcA, c.a); c.xf.p = vsub(c.c, rmul(c.xf.q, zero2()));   // sync_transform
   report<NMAX>(c, vc, n);
 }
+template <int NMAX>
+__device__ __forceinline__ void island_solve_toi_n(Car& c, const LWall* W, const int* cidx, int n, float subdt, float friction) {
+  VC vc[NMAX];
+  island_solve_toi_buf<NMAX>(c, W, cidx, n, subdt, friction, vc);
+}
 __device__ inline void island_solve_toi(Car& c, const LWall* W, const int* cidx, int n, float subdt, float friction) {
   if (n <= 2) island_solve_toi_n<2>(c, W, cidx, n, subdt, friction);
 #if ISLAND_MID
   else if (n <= ISLAND_MID) island_solve_toi_n<ISLAND_MID>(c, W, cidx, n, subdt, friction);
 #endif
+#if ISLAND_LDS   // the general TOI island in the wave's LDS work area, one lane at a time (see solve_island_general)
+  else wave_lds_one_at_a_time([&](VC* vc) { island_solve_toi_buf<MAX_ISLAND>(c, W, cidx, n, subdt, friction, vc); });
+#else
   else island_solve_toi_n<MAX_ISLAND>(c, W, cidx, n, subdt, friction);
+#endif
 }
 
 // Exact shortcut for b2TimeOfImpact on a (car, static wall) pair.  The root finder can only report

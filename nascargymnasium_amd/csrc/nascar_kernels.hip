@@ -48,7 +48,7 @@ __device__ int g_dbg_car = -1;
 struct DSeg {   // per segment, float64 (src/track_generator.py TrackSegment)
   double sx, sy, ex, ey, width, banking, la, chord;  // la: banking lateral assist (src/car.py:527-533)
 };
-// Ray-candidate lists ("beams"), built on the host (build_beams): for every BEAM_CELL-sized cell near the
+// Ray-candidate lists ("beams"), built on the host (build_beams): for every cell (nascar_set_beam_cell) near the
 // walls and every one of BEAM_NB direction bins, the walls that a ray starting anywhere in the cell with a
 // direction in the bin can reach within 250 m, sorted by a lower bound of their distance from the cell.
 // Entry = (lower bound in cm, floored) << 16 | wall index.  A ray walks its list and stops at the first
@@ -1329,9 +1329,13 @@ __device__ __forceinline__ int beam_slot0(double ang) {   // list slot of ray 0'
 // The 4-lane work of car n, lane r (rays r, r + 4, r + 8, r + 12) in ray_sensor_kernel / rollout_kernel: both
 // passes, the beam-list walks against the wall image sw (LDS), the quad transpose and the obs stores.
 // All 4 lanes of a car are consecutive lanes of one quad and call this together.
+// LPC = 16 (small batches, see launch_sensors_impl): one ray per lane, the 16 lanes of a car store its 16 values
+// directly (64 contiguous bytes per car).
+template <int LPC = RAY_LPC>
 __device__ __forceinline__ void ray_lane(const Params& P, const TrackDev& T, const float4* __restrict__ sw, int n, int r,
                                          float* obs, float* terminal_obs, int passes) {
-  constexpr int RPL = 16 / RAY_LPC;
+  static_assert(LPC == 4 || LPC == 16, "lanes per car");
+  constexpr int RPL = 16 / LPC;
   // pose loads after the staging barrier: issuing them (and pass A's cos/sin) before it, or the beam-cell
   // lookup too, measured 2.5 / 9 us slower (registers held across the staging)
   // each pass loads its own pose (pass B's only for auto-reset cars): no pose is held across the other pass's
@@ -1361,13 +1365,15 @@ __device__ __forceinline__ void ray_lane(const Params& P, const TrackDev& T, con
       slot0 = beam_slot(min(BEAM_NB - 1, max(0, (int)u)));
     }
     auto slot_of = [&](int i) { return (slot0 & ~15) | ((slot0 - i) & 15); };
-    float v[RPL] = {0.0f, 0.0f, 0.0f, 0.0f};
+    float v[RPL];
+#pragma unroll
+    for (int q = 0; q < RPL; ++q) v[q] = 0.0f;
 #if RAY_HEADS_AHEAD
     // the four rays' list heads requested together (independent 16-byte loads) before the first walk
     BeamHead hd[RPL];
 #pragma unroll
     for (int q = 0; q < RPL; ++q) {
-      if (base >= 0) hd[q] = beam_head(G, base + slot_of(r + RAY_LPC * q));
+      if (base >= 0) hd[q] = beam_head(G, base + slot_of(r + LPC * q));
       else for (int k = 0; k < BEAM_HW; ++k) hd[q].w[k] = make_uint4(0, 0, 0, 0);
     }
 #pragma unroll
@@ -1375,7 +1381,7 @@ __device__ __forceinline__ void ray_lane(const Params& P, const TrackDev& T, con
 #pragma unroll 1
 #endif
     for (int q = 0; q < RPL; ++q) {
-      const int i = r + RAY_LPC * q;
+      const int i = r + LPC * q;
       double dxd, dyd;
       float fx = ps.x, fy = ps.y, fa = ps.z;   // widened per ray: three floats live across the walks, not three doubles
       asm volatile("" : "+v"(fx), "+v"(fy), "+v"(fa));
@@ -1397,18 +1403,25 @@ __device__ __forceinline__ void ray_lane(const Params& P, const TrackDev& T, con
         bi = ray_fallback(T, p1, p2.x, p2.y, dx, dy, ps.z, i);
       }
       PCOUNT(8, 1);
-      put4(v, q, sensor_value(bi));
+      if constexpr (RPL == 4) put4(v, q, sensor_value(bi));
+      else v[q] = sensor_value(bi);
     }
     // lane index and car index made opaque here, so the transpose indices and the store addresses derived from
     // them are computed now rather than held (spilled) across the walks
     int rq = r, nq = n;
     asm volatile("" : "+v"(rq), "+v"(nq));
-    float o[4];
-    quad_transpose(v, o, rq);
-    const size_t at = (size_t)nq * 38 + 22 + 4 * rq;   // 8-byte aligned (rows are 152 B)
-    const float2 lo = make_float2(o[0], o[1]), hi = make_float2(o[2], o[3]);
-    if (pass == 1 || (mode & PM_A_OBS)) { *(float2*)(obs + at) = lo; *(float2*)(obs + at + 2) = hi; }
-    if (pass == 0 && (mode & PM_A_TERM)) { *(float2*)(terminal_obs + at) = lo; *(float2*)(terminal_obs + at + 2) = hi; }
+    if constexpr (RPL == 4) {
+      float o[4];
+      quad_transpose(v, o, rq);
+      const size_t at = (size_t)nq * 38 + 22 + 4 * rq;   // 8-byte aligned (rows are 152 B)
+      const float2 lo = make_float2(o[0], o[1]), hi = make_float2(o[2], o[3]);
+      if (pass == 1 || (mode & PM_A_OBS)) { *(float2*)(obs + at) = lo; *(float2*)(obs + at + 2) = hi; }
+      if (pass == 0 && (mode & PM_A_TERM)) { *(float2*)(terminal_obs + at) = lo; *(float2*)(terminal_obs + at + 2) = hi; }
+    } else {
+      const size_t at = (size_t)nq * 38 + 22 + rq;
+      if (pass == 1 || (mode & PM_A_OBS)) obs[at] = v[0];
+      if (pass == 0 && (mode & PM_A_TERM)) terminal_obs[at] = v[0];
+    }
   }
 }
 
@@ -1492,12 +1505,14 @@ __device__ __forceinline__ void ray_block_batched(const Params& P, const TrackDe
     }
   }
 }
+// LPC lanes per car, BLOCK / LPC cars per workgroup; `sub` sensor workgroups per step-kernel workgroup (enough for
+// its epb * C cars)
+template <int LPC>
 __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(RSENSOR_WPE)))
-ray_sensor_kernel(Params P, float* obs, float* terminal_obs, int passes) {
-  constexpr int CPW = BLOCK / RAY_LPC;
-  constexpr int SUB = (SBLOCK + CPW - 1) / CPW;   // sensor workgroups per step-kernel workgroup
+ray_sensor_kernel(Params P, float* obs, float* terminal_obs, int passes, int SUB) {
+  constexpr int CPW = BLOCK / LPC;
   const int bx = blockIdx.x, b = bx / SUB + P.blk0, sub = bx % SUB;
-  const int t = threadIdx.x, lc = t / RAY_LPC, r = t - lc * RAY_LPC;
+  const int t = threadIdx.x, lc = t / LPC, r = t - lc * LPC;
   const int C = P.C;
   const int slot = sub * CPW + lc;
   const int el = slot / C, car = slot - el * C;
@@ -1510,7 +1525,7 @@ ray_sensor_kernel(Params P, float* obs, float* terminal_obs, int passes) {
     __syncthreads();
   }
   if (env < 0) return;
-  ray_lane(P, T, (const float4*)smem, env * C + car, r, obs, terminal_obs, passes);
+  ray_lane<LPC>(P, T, (const float4*)smem, env * C + car, r, obs, terminal_obs, passes);
 }
 
 __device__ __forceinline__ uint32_t mix32(uint64_t x) {   // splitmix64 finaliser
@@ -1602,7 +1617,8 @@ __device__ __forceinline__ void model_car(const Params& P, Car& c, int n, const 
 #define CT_LDS_STRIDE ((CT_LDS_CAP * sizeof(DContact) / 16) % 2 ? CT_LDS_CAP * sizeof(DContact) : CT_LDS_CAP * sizeof(DContact) + 16)
 #define MODEL_CT_LDS_BYTES (MODEL_CT_LDS ? (size_t)SBLOCK * CT_LDS_STRIDE : (size_t)0)
 #ifndef MODEL_WPE
-#define MODEL_WPE 2   // 256 VGPRs + 40 spilled (vs 256 + 44 AGPRs at 1 wave/SIMD): 103.6 -> 100.6 us/step
+#define MODEL_WPE 2   // 2 waves/SIMD (248 VGPRs, no spills, no scratch since the LDS general island; round 1: 1 wave/SIMD
+                      // with 256 + 44 AGPRs measured 103.6 vs 100.6 us/step)
 #endif
 // policy >= 0: the actions come from device action source `policy` (policy_car, nascar_step_driven) on the
 // current obs instead of the actions buffer -- the closed-loop driver's step without a policy_kernel launch
@@ -2294,7 +2310,7 @@ static void build_grids(HostTrack& t) {
     }
   t.sn.start.back() = (int)t.sn.idx.size();
 }
-// Beam lists (BeamGrid).  Cells of BEAM_CELL m over the walls' extent; a cell gets lists when its centre is
+// Beam lists (BeamGrid).  Cells of `cell` m (BEAM_CELL_M by default) over the walls' extent; a cell gets lists when its centre is
 // within (largest half width + BEAM_BAND) of a wall centre line -- the corridor and a band outside each wall.
 // Per cell (centre c, disk radius rc = half diagonal + 5 cm) and wall j (centre line AB, capsule radius
 // rr = half thickness + 10 cm, which holds the box and the f32 rounding of the device's ray cast):
@@ -2310,9 +2326,10 @@ static void build_grids(HostTrack& t) {
 #ifndef BEAM_CELL_M
 #define BEAM_CELL_M 1.0f
 #endif
-static const float BEAM_CELL = BEAM_CELL_M;
+#define BEAM_CELL_MIN 0.5f    // nascar_set_beam_cell range (heads: cell count x 4 KB; walks: longer above ~2 m)
+#define BEAM_CELL_MAX 8.0f
 static const double BEAM_BAND = 8.0;
-static void build_beams(HostTrack& t) {
+static void build_beams(HostTrack& t, const float cell) {
   auto t0 = std::chrono::steady_clock::now();
   auto& B = t.beam;
   const int nw = (int)t.walls.size();
@@ -2327,10 +2344,10 @@ static void build_beams(HostTrack& t) {
     ly = std::min({ly, ay[j], by[j]}); uy = std::max({uy, ay[j], by[j]});
   }
   for (auto& s : t.segs) hwmax = std::max(hwmax, s.width / 2.0);
-  const double D = hwmax + BEAM_BAND, pad = D + 2.0 * BEAM_CELL;
-  B.g.ox = (float)(lx - pad); B.g.oy = (float)(ly - pad); B.g.inv_cell = 1.0f / BEAM_CELL;
-  B.g.nx = (int)std::ceil((ux + pad - B.g.ox) / BEAM_CELL) + 1;
-  B.g.ny = (int)std::ceil((uy + pad - B.g.oy) / BEAM_CELL) + 1;
+  const double D = hwmax + BEAM_BAND, pad = D + 2.0 * cell;
+  B.g.ox = (float)(lx - pad); B.g.oy = (float)(ly - pad); B.g.inv_cell = 1.0f / cell;
+  B.g.nx = (int)std::ceil((ux + pad - B.g.ox) / cell) + 1;
+  B.g.ny = (int)std::ceil((uy + pad - B.g.oy) / cell) + 1;
   const int nx = B.g.nx, ny = B.g.ny;
   auto segdist = [&](int j, double x, double y) {
     const double sx = bx[j] - ax[j], sy = by[j] - ay[j], ll = sx * sx + sy * sy;
@@ -2339,15 +2356,15 @@ static void build_beams(HostTrack& t) {
     return std::hypot(x - (ax[j] + tt * sx), y - (ay[j] + tt * sy));
   };
   auto centre = [&](int cx, int cy, double& x, double& y) {
-    x = (double)B.g.ox + (cx + 0.5) * (double)BEAM_CELL; y = (double)B.g.oy + (cy + 0.5) * (double)BEAM_CELL;
+    x = (double)B.g.ox + (cx + 0.5) * (double)cell; y = (double)B.g.oy + (cy + 0.5) * (double)cell;
   };
   // cells near a wall
   std::vector<uint8_t> mark((size_t)nx * ny, 0);
   for (int j = 0; j < nw; ++j) {
-    const int x0 = std::max(0, (int)std::floor((std::min(ax[j], bx[j]) - D - B.g.ox) / BEAM_CELL) - 1);
-    const int x1 = std::min(nx - 1, (int)std::floor((std::max(ax[j], bx[j]) + D - B.g.ox) / BEAM_CELL) + 1);
-    const int y0 = std::max(0, (int)std::floor((std::min(ay[j], by[j]) - D - B.g.oy) / BEAM_CELL) - 1);
-    const int y1 = std::min(ny - 1, (int)std::floor((std::max(ay[j], by[j]) + D - B.g.oy) / BEAM_CELL) + 1);
+    const int x0 = std::max(0, (int)std::floor((std::min(ax[j], bx[j]) - D - B.g.ox) / cell) - 1);
+    const int x1 = std::min(nx - 1, (int)std::floor((std::max(ax[j], bx[j]) + D - B.g.ox) / cell) + 1);
+    const int y0 = std::max(0, (int)std::floor((std::min(ay[j], by[j]) - D - B.g.oy) / cell) - 1);
+    const int y1 = std::min(ny - 1, (int)std::floor((std::max(ay[j], by[j]) + D - B.g.oy) / cell) + 1);
     for (int cy = y0; cy <= y1; ++cy)
       for (int cx = x0; cx <= x1; ++cx) {
         double x, y;
@@ -2360,7 +2377,7 @@ static void build_beams(HostTrack& t) {
   for (size_t k = 0; k < mark.size(); ++k)
     if (mark[k]) { B.cell[k] = (int)cells.size() * BEAM_NB; cells.push_back((int)k); }
   const int ncell = (int)cells.size();
-  const double rc = BEAM_CELL * 0.70710678 + 0.05, two_pi = 2.0 * M_PI, dbin = two_pi / BEAM_NB;
+  const double rc = cell * 0.70710678 + 0.05, two_pi = 2.0 * M_PI, dbin = two_pi / BEAM_NB;
   std::vector<std::vector<uint32_t>> lists((size_t)ncell * BEAM_NB);
   auto work = [&](int c0, int c1) {
     for (int ci = c0; ci < c1; ++ci) {
@@ -2480,6 +2497,8 @@ struct NascarHandle {
   std::vector<int> pending_track;   // nascar_set_env_tracks, applied per env by its next nascar_reset
   bool pristine = true;             // no reset / step / rollout / set_state yet: track changes apply at once
   int car_contact = 0;              // nascar_set_car_contact (build-only extension)
+  int ray_lanes = 0;                // nascar_set_sensor_lanes: 0 automatic, 4 or 16 lanes per car
+  float beam_cell = BEAM_CELL_M;    // nascar_set_beam_cell: cell size (m) of the beam lists of tracks added later
   float* d_vhist = nullptr;  // [VH_RING][N] speed history (nascar_set_perf_history), outside the snapshot arena
   double* d_ctl = nullptr;   // rule-driver state for nascar_policy_actions (inside the arena: snapshots keep it)
   float4* d_pose = nullptr;  // [2][N] step/reset -> sensor_kernel hand-off
@@ -2538,6 +2557,19 @@ extern "C" int nascar_set_envs_per_block(NascarHandle* h, int32_t epb) {
   return 0;
 }
 extern "C" int nascar_get_envs_per_block(NascarHandle* h) { return h ? h->epb : -1; }
+extern "C" int nascar_set_beam_cell(NascarHandle* h, float meters) {
+  if (!h) return fail("null argument");
+  if (!(meters >= BEAM_CELL_MIN && meters <= BEAM_CELL_MAX))
+    return fail("beam cell size must be in [%.1f, %.1f] m, got %g", (double)BEAM_CELL_MIN, (double)BEAM_CELL_MAX, (double)meters);
+  h->beam_cell = meters;
+  return 0;
+}
+extern "C" int nascar_set_sensor_lanes(NascarHandle* h, int32_t lanes) {
+  if (!h) return fail("null argument");
+  if (lanes != 0 && lanes != 4 && lanes != 16) return fail("sensor lanes per car must be 0 (automatic), 4 or 16, got %d", lanes);
+  h->ray_lanes = lanes;
+  return 0;
+}
 
 extern "C" int nascar_create(const NascarConfig* cfg, NascarHandle** out) {
   if (!cfg || !out) return fail("null argument");
@@ -2548,6 +2580,11 @@ extern "C" int nascar_create(const NascarConfig* cfg, NascarHandle** out) {
   h->cfg = *cfg;
   h->E = cfg->num_envs; h->C = cfg->num_cars; h->N = h->E * h->C;
   h->epb = auto_epb(h->E, h->C, cfg->device);
+  if (const char* ev = getenv("NASCAR_RAY_LPC")) h->ray_lanes = atoi(ev);   // A/B
+  if (const char* ev = getenv("NASCAR_BEAM_CELL")) {
+    const float v = (float)atof(ev);
+    if (v >= BEAM_CELL_MIN && v <= BEAM_CELL_MAX) h->beam_cell = v;
+  }
   size_t N = h->N, E = h->E, o = 0;
   h->off_f32 = o; o = align256(o + sizeof(float) * N_F32 * N);
   h->off_f64 = o; o = align256(o + sizeof(double) * N_F64 * N);
@@ -2602,7 +2639,7 @@ extern "C" void nascar_destroy(NascarHandle* h) {
 }
 
 static int build_track(HostTrack& t, size_t& lds_out, const double* segments, int32_t nseg, double total_length,
-                       const double* walls, int32_t nwall);
+                       const double* walls, int32_t nwall, float beam_cell);
 // wall table exactly as Box2D sees it (float32 transform via glibc sinf/cosf, fat AABB, key)
 extern "C" int nascar_add_track(NascarHandle* h, const double* segments, int32_t nseg, double total_length,
                                 const double* walls, int32_t nwall) {
@@ -2614,6 +2651,7 @@ extern "C" int nascar_add_track(NascarHandle* h, const double* segments, int32_t
     const int32_t dims[3] = {h->cfg.device, nseg, nwall};
     key.append((const char*)dims, sizeof dims);
     key.append((const char*)&total_length, sizeof total_length);
+    key.append((const char*)&h->beam_cell, sizeof h->beam_cell);   // builds at different cell sizes differ
     key.append((const char*)segments, sizeof(double) * 13 * (size_t)nseg);
     key.append((const char*)walls, sizeof(double) * 4 * (size_t)nwall);
   }
@@ -2629,7 +2667,7 @@ extern "C" int nascar_add_track(NascarHandle* h, const double* segments, int32_t
     int cur = 0;
     HIPCHK(hipGetDevice(&cur));
     if (cur != h->cfg.device) HIPCHK(hipSetDevice(h->cfg.device));
-    const int rc = build_track(tb->t, tb->lds, segments, nseg, total_length, walls, nwall);
+    const int rc = build_track(tb->t, tb->lds, segments, nseg, total_length, walls, nwall, h->beam_cell);
     if (cur != h->cfg.device) hipSetDevice(cur);
     if (rc < 0) return rc;
     g_track_cache[key] = tb;
@@ -2645,7 +2683,7 @@ extern "C" int nascar_add_track(NascarHandle* h, const double* segments, int32_t
 
 // the device tables of one track (nascar_add_track, on the current device); lds: model_kernel's wall table bytes
 static int build_track(HostTrack& t, size_t& lds_out, const double* segments, int32_t nseg, double total_length,
-                       const double* walls, int32_t nwall) {
+                       const double* walls, int32_t nwall, float beam_cell) {
   t.total_length = total_length;
   t.startline = -1; t.has_banking = 0;
   double pre = 0.0;
@@ -2707,7 +2745,7 @@ static int build_track(HostTrack& t, size_t& lds_out, const double* segments, in
   if (nwall > 65535) return fail("track has %d walls (grid indices are 16-bit)", nwall);
   build_grids(t);
   if (upload_grid(t.bp) < 0 || upload_grid(t.sn) < 0) return -1;
-  build_beams(t);
+  build_beams(t, beam_cell);
   if (upload_beams(t) < 0) return -1;
   HIPCHK(hipMalloc(&t.d_groups, sizeof(float4) * t.groups.size()));
   HIPCHK(hipMemcpy(t.d_groups, t.groups.data(), sizeof(float4) * t.groups.size(), hipMemcpyHostToDevice));
@@ -2728,7 +2766,7 @@ static int build_track(HostTrack& t, size_t& lds_out, const double* segments, in
   if (getenv("NASCAR_VERBOSE"))
     fprintf(stderr, "nascar_add_track: beam grid %dx%d (%.2f m cells), %zu cells with lists, %zu entries (mean %.2f per "
             "list), heads %.1f MB + continuations %.1f MB + cell map %.1f MB, built in %.2f s\n", t.beam.g.nx, t.beam.g.ny,
-            (double)BEAM_CELL, t.beam.nlist / BEAM_NB, t.beam.entries, (double)t.beam.entries / std::max<size_t>(1, t.beam.nlist),
+            (double)beam_cell, t.beam.nlist / BEAM_NB, t.beam.entries, (double)t.beam.entries / std::max<size_t>(1, t.beam.nlist),
             16.0 * t.beam.head.size() / 1e6, 4.0 * t.beam.ent.size() / 1e6, 4.0 * t.beam.cell.size() / 1e6, t.beam.build_s);
   t.beam.cell.clear(); t.beam.ent.clear(); t.beam.head.clear();   // the device copies are all the kernels use
   t.beam.cell.shrink_to_fit(); t.beam.ent.shrink_to_fit(); t.beam.head.shrink_to_fit();
@@ -2883,15 +2921,31 @@ static int sensor_impl() {
   if (m < 0) { const char* e = getenv("NASCAR_SENSOR"); m = (e && !strcmp(e, "groups")) ? 0 : 1; }
   return m;
 }
-// nb step-kernel workgroups from P.blk0 (each is SUB sensor workgroups)
+// Lanes per car of the beam-list sensor kernel.  4 (rays r, r + 4, r + 8, r + 12 per lane) fills the chip at the
+// headline's 81 920 cars (16 measured 62 vs 41.5 us there); a small batch leaves most of the chip idle, and then one
+// ray per lane (16 lanes per car) cuts each car's four sequential walks to one.  NASCAR_RAY_LPC = 4 / 16 overrides.
+#ifndef RAY_LPC16_MAX_CARS
+#define RAY_LPC16_MAX_CARS 16384
+#endif
+static int ray_lpc(const NascarHandle* h) {
+  if (h->ray_lanes == 4 || h->ray_lanes == 16) return h->ray_lanes;   // nascar_set_sensor_lanes / NASCAR_RAY_LPC
+  return h->N <= RAY_LPC16_MAX_CARS ? 16 : 4;
+}
+// nb step-kernel workgroups from P.blk0 (each is `sub` sensor workgroups)
 static void launch_sensors_impl(NascarHandle* h, const Params& P, int nb, float* obs, float* terminal_obs, int passes,
                                 void* stream, int impl) {
   if (impl == 1) {
-    constexpr int CPW = BLOCK / RAY_LPC;
-    const int sub = (SBLOCK + CPW - 1) / CPW;
     const size_t rlds = h->max_sensor_lds;   // >= 2 float4 per wall
-    hipLaunchKernelGGL(ray_sensor_kernel, dim3(nb * sub), dim3(BLOCK), rlds, (hipStream_t)stream, P, obs,
-                       terminal_obs, passes);
+    const int cars = h->epb * h->C;          // cars per step-kernel workgroup
+    if (ray_lpc(h) == 16) {
+      const int sub = (cars + BLOCK / 16 - 1) / (BLOCK / 16);
+      hipLaunchKernelGGL(ray_sensor_kernel<16>, dim3(nb * sub), dim3(BLOCK), rlds, (hipStream_t)stream, P, obs,
+                         terminal_obs, passes, sub);
+    } else {
+      const int sub = (cars + BLOCK / RAY_LPC - 1) / (BLOCK / RAY_LPC);
+      hipLaunchKernelGGL(ray_sensor_kernel<RAY_LPC>, dim3(nb * sub), dim3(BLOCK), rlds, (hipStream_t)stream, P, obs,
+                         terminal_obs, passes, sub);
+    }
     return;
   }
   const size_t lds = h->max_sensor_groups_lds;

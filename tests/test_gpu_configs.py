@@ -75,12 +75,13 @@ def test_bench_workload_full_episode_vs_oracle():
 def test_cfg2_one_car_layouts_vs_oracle():
     """cfg2's shape (1 car per env) at cfg2's own layout: 256 envs x 1 car daytona at 8 envs per workgroup (what the
     engine picks for 4096 x 1: 512 workgroups of 8 cars), at 128 envs per workgroup (two full waves per workgroup)
-    and at one env per workgroup; noisy driver closed loop, staggered resets, auto-reset, 2500 steps, == the oracle
-    every step."""
+    and at one env per workgroup (there with 4 distance-sensor lanes per car instead of the small batch's 16); noisy
+    driver closed loop, staggered resets, auto-reset, 2500 steps, == the oracle every step."""
     from oracle_lib import OracleGroups
     E, C, S = 256, 1, 2500
     path = os.path.join(TRACKS, "daytona.track")
     envs = make_envs(E, C, path, [8, 128, 1])
+    envs[2].set_sensor_lanes(4)          # the small batch's default is 16 sensor lanes per car; pin 4 too
     orc = OracleGroups([path] * E, C, shards=4)
     stagger = {9 * e: e for e in range(1, E)}
     t = closed_loop_vs_oracle(envs, orc, S, seed=41, stagger=stagger)

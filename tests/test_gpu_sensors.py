@@ -88,7 +88,8 @@ def _oracle_sensors(orc, pose):
                                        ("michigan.track", 512, 4), ("nascar.track", 512, 4),
                                        ("nascar2.track", 512, 4), ("trioval.track", 512, 4)])
 def test_sensors_on_random_poses(track, E, C):
-    """every pose: beam-list kernel == wall-group kernel == the oracle's brute-force cast, bit for bit"""
+    """every pose: beam-list kernel (4 and 16 lanes per car) == wall-group kernel == the oracle's brute-force
+    cast, bit for bit"""
     from nascargymnasium_amd.batched import BatchedCarEnv
     from nascargymnasium_amd.track import build_walls, load_track
     from oracle_lib import OracleEnv
@@ -97,9 +98,14 @@ def test_sensors_on_random_poses(track, E, C):
     walls = build_walls(load_track(path))
     env = BatchedCarEnv(E, C, path, device="cuda:0")
     poses = _poses(rng, walls, E * C)
+    env.set_sensor_lanes(4)
     beams = _device_sensors(env, poses, 1)
+    env.set_sensor_lanes(16)
+    beams16 = _device_sensors(env, poses, 1)
     groups = _device_sensors(env, poses, 0)
     env.close()
+    bad = np.argwhere(beams16.view(np.uint32) != beams.view(np.uint32))
+    assert len(bad) == 0, f"16 vs 4 lanes per car differ at {bad[:5].tolist()}"
     assert (beams[:, :22] == -7.0).all(), "sensor launch wrote outside obs[22:38]"
     bad = np.argwhere(beams[:, 22:].view(np.uint32) != groups[:, 22:].view(np.uint32))
     assert len(bad) == 0, f"beam vs group sensors differ at {bad[:5].tolist()}"
@@ -112,3 +118,23 @@ def test_sensors_on_random_poses(track, E, C):
     for n in rng.integers(0, E * C, 40):
         assert np.array_equal(_oracle_sensors(orc, poses[n]).view(np.uint32), ref[n].view(np.uint32)), n
     orc.close()
+
+
+def test_beam_cell_size_changes_nothing():
+    """nascar_set_beam_cell: beam lists built at 2 m and 4 m cells give the 1 m default's sensor values on every pose
+    (the lists are conservative at any cell size); a 2 m build takes a quarter of the 1 m build's list memory."""
+    from nascargymnasium_amd.batched import BatchedCarEnv
+    from nascargymnasium_amd.track import build_walls, load_track
+    path = os.path.join(TRACKS, "daytona.track")
+    rng = np.random.default_rng(77)
+    poses = _poses(rng, build_walls(load_track(path)), 4096)
+    out = {}
+    for cell in (None, 2.0, 4.0):
+        env = BatchedCarEnv(1024, 4, path, device="cuda:0", beam_cell=cell)
+        out[cell] = _device_sensors(env, poses, 1)
+        env.close()
+    for cell in (2.0, 4.0):
+        bad = np.argwhere(out[cell].view(np.uint32) != out[None].view(np.uint32))
+        assert len(bad) == 0, f"{cell} m cells differ from 1 m at {bad[:5].tolist()}"
+    with pytest.raises(RuntimeError):
+        BatchedCarEnv(4, 1, path, device="cuda:0", beam_cell=0.1)

@@ -145,6 +145,9 @@ def main():
             print(f"  slowest wave (cars {w0}..{w1 - 1}): solve_toi scans {cp[w0, 14]}, TOI job rounds {cp[w0, 13]} cycles, "
                   f"event processing {cp[w0, 15]} cycles")
             for i in range(w0, w1):
+                if cp[i, 26]:
+                    print(f"    car {i}: island of {cp[i, 26]} touching contacts, island solve {cp[i, 25]} cycles")
+            for i in range(w0, w1):
                 if cp[i, 4] or cp[i, 2]:
                     print(f"    car {i}: events {cp[i, 4]}, island solve {cp[i, 11]}, event contact updates {cp[i, 12]}, "
                           f"TOI calls computed by this lane {cp[i, 2]}: outer iters {cp[i, 6]}, root iters {cp[i, 7]}, "
@@ -183,6 +186,22 @@ def main():
             wv = m[np.argmax(m[:, 4] - m[:, 3])]
             print("  slowest wave's b2_step phases (cycles): collide", wv[11] - wv[3], "solve", wv[12] - wv[11],
                   "sync+find", wv[13] - wv[12], "toi", wv[4] - wv[13])
+            # the wave with the longest solve phase and its islands (stamp rows: blockIdx.x * 4 + wave of the block)
+            ok = (model[:, 12] != 0) & (model[:, 11] != 0)
+            sol = np.where(ok, model[:, 12] - model[:, 11], -1)
+            ws = int(np.argmax(sol))
+            per_w = (128 // a.cars) * a.cars
+            blk, wi = divmod(ws, 4)
+            c0 = blk * per_w + wi * 64
+            lanes = [i for i in range(c0, min(c0 + 64, blk * per_w + per_w, len(cp))) if cp[i, 26]]
+            print(f"  longest solve phase {sol[ws]} cycles (block {blk} wave {wi}); its islands (touching contacts: "
+                  f"solve cycles): " + ", ".join(f"{cp[i, 26]}: {cp[i, 25]}" for i in lanes))
+            isl = cp[:, 26]
+            for lo, hi in [(1, 3), (3, 4), (4, 9)]:
+                sel = (isl >= lo) & (isl < hi)
+                if sel.any():
+                    print(f"  islands of {lo}-{hi - 1} contacts: {sel.sum()} cars, solve cycles mean {cp[sel, 25].mean():.0f} "
+                          f"max {cp[sel, 25].max()}")
             print(f"  broadphase full scans per car-step {cp[:, 8].mean():.4f}, cars with a full scan {(cp[:, 8] > 0).sum()}")
             it = cp[:, 7]
             print(f"  root-finder iterations per car-step: mean {it.mean():.2f}, max {it.max()}, cars > 100: {(it > 100).sum()}, "
