@@ -764,6 +764,17 @@ struct BodyState { V2 c; float a; V2 v; float w; };
 #define ISLAND_MID 3     // islands of 3 .. ISLAND_MID contacts also solved register-resident (0: off; 4 measured slower)
 #endif
 template <int NMAX> struct NUNR { static constexpr int v = NMAX <= 2 || NMAX == ISLAND_MID ? NMAX : 1; };
+// The solvers' iteration loops (6 velocity, 4 / 20 position iterations) index nothing per iteration, so rolled
+// loops keep the constraints in the same registers; unrolled, each island size's solver was copied six times over
+// (cs_solve_velocity alone was 34 KB of model_kernel's 295 KB of code, a kernel far beyond the instruction cache).
+#ifndef SOLVER_ITER_UNROLL
+#define SOLVER_ITER_UNROLL 0
+#endif
+#if SOLVER_ITER_UNROLL
+#define SOLVER_ITER_LOOP
+#else
+#define SOLVER_ITER_LOOP _Pragma("unroll 1")
+#endif
 
 template <int NMAX> __device__ __forceinline__ void cs_init(VC* vc, int n, const Car& c, const int* cidx, const LWall* W, bool warm, float dtRatio) {
 #pragma unroll UNROLL_SMALL   // registers for small islands; the general bound stays a loop
@@ -1052,11 +1063,13 @@ __device__ __forceinline__ int solve_island_buf(Car& c, const LWall* W, const in
   cs_init<NMAX>(vc, n, c, cidx, W, true, dtRatio);
   cs_init_velocity<NMAX>(vc, n, c, A);
   cs_warm_start<NMAX>(vc, n, A);
+  SOLVER_ITER_LOOP
   for (int it = 0; it < 6; ++it) cs_solve_velocity<NMAX>(vc, n, A, friction);
   cs_store<NMAX>(vc, n, c);
   integrate_positions(A, h);
   int positionSolved = 0;
   RotCache rcA; rcA.bits = __float_as_uint(A.a) ^ 1u; rcA.q.s = 0.0f; rcA.q.c = 1.0f;   // (empty: no angle matches)
+  SOLVER_ITER_LOOP
   for (int it = 0; it < 4; ++it) { if (cs_solve_position<NMAX>(vc, n, A, 0, rcA)) { positionSolved = 1; break; } }
   c.c = A.c; c.a = A.a; c.v = A.v; c.w = A.w;
   c.xf.q = rot_cached(rcA, c.a); c.xf.p = vsub(c.c, rmul(c.xf.q, zero2()));   // sync_transform
@@ -1512,6 +1525,7 @@ __device__ __forceinline__ void island_solve_toi_buf(Car& c, const LWall* W, con
   }
   c.c0 = A.c; c.a0 = A.a;
   cs_init_velocity<NMAX>(vc, n, c, A);
+  SOLVER_ITER_LOOP
   for (int it = 0; it < 6; ++it) cs_solve_velocity<NMAX>(vc, n, A, friction);
   integrate_positions(A, subdt);
   c.c = A.c; c.a = A.a; c.v = A.v; c.w = A.w;

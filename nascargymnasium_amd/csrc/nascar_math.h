@@ -79,7 +79,15 @@ __host__ __device__ __forceinline__ uint32_t inv_pio4(int i) {
   return kInvPio4Host[i];
 #endif
 }
-__host__ __device__ inline double reduce_large(uint32_t xi, int* np) {   // |y| >= 120: rare (wound-up angles)
+// |y| >= 120: rare (wound-up angles).  Out of line on the device: inlined into every b2Rot::Set it was ~15 KB of
+// model_kernel's code for a path almost never taken.
+#ifndef SINCOS_LARGE_INLINE
+#define SINCOS_LARGE_INLINE 0
+#endif
+#if defined(__HIP_DEVICE_COMPILE__) && !SINCOS_LARGE_INLINE
+__attribute__((noinline))
+#endif
+__host__ __device__ inline double reduce_large(uint32_t xi, int* np) {
   const int k = (xi >> 26) & 15;
   int shift = (xi >> 23) & 7;
   uint64_t n, res0, res1, res2;
