@@ -128,6 +128,12 @@ int nascar_set_sensor_lanes(NascarHandle* h, int32_t lanes);
  * per track; 2 m quarters both for slightly longer list walks.  Range [0.5, 8].  Identical results at any size. */
 int nascar_set_beam_cell(NascarHandle* h, float meters);
 
+/* Step kernels (no reference counterpart; identical results): enable != 0 runs the vehicle model + Box2D step and
+ * the env logic (disable rules, lap timer, obs[0:22], rewards, termination, auto-reset; src/car_env.py:537-803,
+ * 805-1158) as one launch per step, each workgroup starting its envs' logic when its own cars' Box2D steps are done;
+ * 0 (default) runs them as two launches. */
+int nascar_set_fused_logic(NascarHandle* h, int32_t enable);
+
 /* Profiling hook (no reference counterpart; bench.py's per-kernel roofline): events = 4 caller-created timing
  * events (hipEvent_t), recorded by every following whole-grid step (nascar_step / nascar_step_driven) on its
  * stream before model_kernel, after model_kernel, after logic_kernel and after the sensor launch; n = 0 stops.

@@ -104,6 +104,12 @@ class BatchedCarEnv:
     def envs_per_block(self) -> int:
         return int(self.L.nascar_get_envs_per_block(self.h))
 
+    def set_fused_logic(self, enable: bool = True):
+        """One launch per step for the vehicle model + Box2D step and the env logic (each workgroup runs its envs'
+        logic once its own cars' physics is done) instead of two; identical results."""
+        _lib.check(self.L.nascar_set_fused_logic(self.h, int(bool(enable))))
+        self.fused_logic = bool(enable)
+
     def set_sensor_lanes(self, lanes: int = 0):
         """Lanes per car of the distance-sensor kernel: 4 or 16 (one ray per lane), 0 automatic (16 for batches of
         up to 16 384 cars).  Identical results; a scheduling choice."""

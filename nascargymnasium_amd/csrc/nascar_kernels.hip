@@ -1621,14 +1621,12 @@ __device__ __forceinline__ void model_car(const Params& P, Car& c, int n, const 
                       // with 256 + 44 AGPRs measured 103.6 vs 100.6 us/step)
 #endif
 // policy >= 0: the actions come from device action source `policy` (policy_car, nascar_step_driven) on the
-// current obs instead of the actions buffer -- the closed-loop driver's step without a policy_kernel launch
-__global__ void __launch_bounds__(SBLOCK) __attribute__((amdgpu_waves_per_eu(MODEL_WPE))) model_kernel(Params P, const void* actions, int discrete, int want_term,
-                                                                                                    int policy, uint64_t seed, int64_t step, const float* pobs) {
-  const int tid = threadIdx.x, C = P.C;
-  const int el = tid / C, car = tid - el * C;
-  const int slot = (blockIdx.x + P.blk0) * P.epb + el;
-  const int env = blk_env_of(P, el, slot);
-  const int n = env >= 0 ? env * C + car : 0;
+// current obs instead of the actions buffer -- the closed-loop driver's step without a policy_kernel launch.
+// Every thread of the block calls it (it holds the segment staging barrier); lanes without a car (env < 0) skip
+// the step (model_kernel: they return; FUSED, the model_logic_kernel, keeps them for the barriers after it).
+template <bool FUSED>
+__device__ __forceinline__ void model_block(const Params& P, const void* actions, int discrete, int want_term, int policy,
+                                            uint64_t seed, int64_t step, const float* pobs, int tid, int env, int n) {
   PROF_RT(14);
   PROF(0);
 #if MODEL_PRIO == 1   // A/B: model_kernel's waves issue ahead of co-resident logic / sensor waves of other shards
@@ -1668,11 +1666,21 @@ __global__ void __launch_bounds__(SBLOCK) __attribute__((amdgpu_waves_per_eu(MOD
   __syncthreads();
   T.segs = s_segs;   // (the wall table stays global: staged in LDS it measured neutral, and the LDS holds the contacts)
   PROF(1);
-  if (env < 0) return;
-  PROF(2);
-  model_car(P, c, n, T, tb, st, want_term);
-  PROF(5);
-  PROF_RT(15);
+  if (!FUSED && env < 0) return;
+  if (env >= 0) {
+    PROF(2);
+    model_car(P, c, n, T, tb, st, want_term);
+    PROF(5);
+    PROF_RT(15);
+  }
+}
+__global__ void __launch_bounds__(SBLOCK) __attribute__((amdgpu_waves_per_eu(MODEL_WPE))) model_kernel(Params P, const void* actions, int discrete, int want_term,
+                                                                                                    int policy, uint64_t seed, int64_t step, const float* pobs) {
+  const int tid = threadIdx.x, C = P.C;
+  const int el = tid / C, car = tid - el * C;
+  const int slot = (blockIdx.x + P.blk0) * P.epb + el;
+  const int env = blk_env_of(P, el, slot);
+  model_block<false>(P, actions, discrete, want_term, policy, seed, step, pobs, tid, env, env >= 0 ? env * C + car : 0);
 }
 
 // logic_kernel's shared memory: env reductions and the coalesced obs[:, 0:22] row store
@@ -1989,6 +1997,38 @@ __global__ void __launch_bounds__(SBLOCK) LOGIC_ATTR logic_kernel(Params P, floa
   __syncthreads();
   T.segs = TL.segs; T.prefix = TL.prefix;
   logic_run(P, T, TL, L, tid, el, car, env, n, c, sim, pend_in, reason_in, obs, reward, car_flags, env_flags, auto_reset,
+            terminal_obs);
+}
+
+// model_kernel + logic_kernel in one launch (NASCAR_FUSE_ML / nascar_set_fused_logic): each block runs its envs'
+// logic as soon as ITS cars' Box2D steps are done (a block barrier) instead of after the whole grid's slowest
+// wave, and one kernel boundary per step goes.  The logic's LDS (env reductions, obs rows, track segments) reuses
+// the contact-slot region, free once every car of the block has written its contact records back.  Same device
+// code as the two kernels, so the results are identical (tests run both).
+struct FusedLogicLDS { LogicLDS L; TrackLDS TL; };
+#define MODEL_LOGIC_LDS_BYTES (MODEL_CT_LDS_BYTES > sizeof(FusedLogicLDS) ? MODEL_CT_LDS_BYTES : sizeof(FusedLogicLDS))
+__global__ void __launch_bounds__(SBLOCK) __attribute__((amdgpu_waves_per_eu(MODEL_WPE)))
+model_logic_kernel(Params P, const void* actions, int discrete, int want_term, int policy, uint64_t seed, int64_t step,
+                   const float* pobs, float* obs, float* reward, uint8_t* car_flags, uint8_t* env_flags, int auto_reset,
+                   float* terminal_obs) {
+  const int tid = threadIdx.x, C = P.C;
+  const int el = tid / C, car = tid - el * C;
+  const int slot = (blockIdx.x + P.blk0) * P.epb + el;
+  const int env = blk_env_of(P, el, slot);
+  const int n = env >= 0 ? env * C + car : 0;
+  model_block<true>(P, actions, discrete, want_term, policy, seed, step, pobs, tid, env, n);
+  __syncthreads();   // the block's Box2D steps done: body state stored, contact slots written back (LDS free)
+  if (P.car_contact) car_contact_block(P, tid, el, car, env, n);   // block-uniform; holds its own barrier
+  FusedLogicLDS& F = *(FusedLogicLDS*)smem;
+  Car c;
+  double sim;
+  int pend_in, reason_in;
+  logic_load(P, env, car, n, c, sim, pend_in, reason_in);
+  TrackDev T = P.tracks[blk_track_of(P, (blockIdx.x + P.blk0))];
+  stage_track_lds(T, F.TL, tid);
+  __syncthreads();
+  T.segs = F.TL.segs; T.prefix = F.TL.prefix;
+  logic_run(P, T, F.TL, F.L, tid, el, car, env, n, c, sim, pend_in, reason_in, obs, reward, car_flags, env_flags, auto_reset,
             terminal_obs);
 }
 
@@ -2498,6 +2538,7 @@ struct NascarHandle {
   bool pristine = true;             // no reset / step / rollout / set_state yet: track changes apply at once
   int car_contact = 0;              // nascar_set_car_contact (build-only extension)
   int ray_lanes = 0;                // nascar_set_sensor_lanes: 0 automatic, 4 or 16 lanes per car
+  int fuse_ml = 0;                  // nascar_set_fused_logic: model_logic_kernel instead of model_kernel + logic_kernel
   float beam_cell = BEAM_CELL_M;    // nascar_set_beam_cell: cell size (m) of the beam lists of tracks added later
   float* d_vhist = nullptr;  // [VH_RING][N] speed history (nascar_set_perf_history), outside the snapshot arena
   double* d_ctl = nullptr;   // rule-driver state for nascar_policy_actions (inside the arena: snapshots keep it)
@@ -2557,6 +2598,11 @@ extern "C" int nascar_set_envs_per_block(NascarHandle* h, int32_t epb) {
   return 0;
 }
 extern "C" int nascar_get_envs_per_block(NascarHandle* h) { return h ? h->epb : -1; }
+extern "C" int nascar_set_fused_logic(NascarHandle* h, int32_t enable) {
+  if (!h) return fail("null argument");
+  h->fuse_ml = enable != 0;
+  return 0;
+}
 extern "C" int nascar_set_beam_cell(NascarHandle* h, float meters) {
   if (!h) return fail("null argument");
   if (!(meters >= BEAM_CELL_MIN && meters <= BEAM_CELL_MAX))
@@ -2581,6 +2627,7 @@ extern "C" int nascar_create(const NascarConfig* cfg, NascarHandle** out) {
   h->E = cfg->num_envs; h->C = cfg->num_cars; h->N = h->E * h->C;
   h->epb = auto_epb(h->E, h->C, cfg->device);
   if (const char* ev = getenv("NASCAR_RAY_LPC")) h->ray_lanes = atoi(ev);   // A/B
+  if (const char* ev = getenv("NASCAR_FUSE_ML")) h->fuse_ml = atoi(ev) != 0;   // A/B
   if (const char* ev = getenv("NASCAR_BEAM_CELL")) {
     const float v = (float)atof(ev);
     if (v >= BEAM_CELL_MIN && v <= BEAM_CELL_MAX) h->beam_cell = v;
@@ -2996,6 +3043,17 @@ static int launch_step_range(NascarHandle* h, const Params& P, int nb, const voi
                              uint8_t* car_flags, uint8_t* env_flags, int32_t auto_reset, float* terminal_obs,
                              hipStream_t s, int phases = PH_ALL) {
   const bool timed = h->step_ev[0] && nb == h->nblocks;   // nascar_set_step_events: whole-grid steps only
+  if (h->fuse_ml) {   // model + logic in one launch (model_logic_kernel); the logic phase is part of PH_MODEL
+    if (phases & PH_MODEL) {
+      if (timed) HIPCHK(hipEventRecord(h->step_ev[0], s));
+      hipLaunchKernelGGL(model_logic_kernel, dim3(nb), dim3(SBLOCK), MODEL_LOGIC_LDS_BYTES, s, P, actions, discrete,
+                         terminal_obs != nullptr, policy, seed, step, obs_in, obs, reward, car_flags, env_flags, auto_reset,
+                         terminal_obs);
+      HIPCHK(hipGetLastError());
+      if (timed) { HIPCHK(hipEventRecord(h->step_ev[1], s)); HIPCHK(hipEventRecord(h->step_ev[2], s)); }
+    }
+    phases &= ~(PH_MODEL | PH_LOGIC);
+  }
   if (phases & PH_MODEL) {
     if (timed) HIPCHK(hipEventRecord(h->step_ev[0], s));
     hipLaunchKernelGGL(model_kernel, dim3(nb), dim3(SBLOCK), MODEL_CT_LDS_BYTES, s, P, actions, discrete,

@@ -9,14 +9,17 @@ reference's per-env / per-car loops (src/car_env.py:567-570, 1115-1158), so the 
 import numpy as np
 
 
-def make_envs(E, C, tracks, layouts, **kw):
-    """one BatchedCarEnv per layout (None: the engine's automatic choice), asserting that the layout took"""
+def make_envs(E, C, tracks, layouts, fused=(), **kw):
+    """one BatchedCarEnv per layout (None: the engine's automatic choice), asserting that the layout took; the
+    engines whose positions are listed in `fused` step through the fused model + logic kernel"""
     from nascargymnasium_amd.batched import BatchedCarEnv
     envs = []
-    for epb in layouts:
+    for i, epb in enumerate(layouts):
         env = BatchedCarEnv(E, C, tracks, device="cuda:0", envs_per_block=epb, **kw)
         if epb is not None:
             assert env.envs_per_block == epb
+        if i in fused:
+            env.set_fused_logic(True)
         envs.append(env)
     return envs
 
@@ -59,7 +62,7 @@ def closed_loop_vs_oracle(envs, orc, steps, seed, stagger, check_actions=False):
             orc.reset(np.nonzero(done)[0])
             oo = orc.outputs()[0]
         for env in envs:
-            lay = f"envs per block {env.envs_per_block}"
+            lay = f"envs per block {env.envs_per_block}" + (", fused model + logic" if getattr(env, "fused_logic", False) else "")
             gr, gcf, gef = env.reward.cpu().numpy(), env.car_flags.cpu().numpy(), env.env_flags.cpu().numpy()
             assert np.array_equal(gr, orw), f"step {k} ({lay}): reward mismatch at {np.argwhere(gr != orw)[:5].tolist()}"
             assert np.array_equal(gcf & 1, ocf & 1), f"step {k} ({lay}): disabled flags"

@@ -39,7 +39,7 @@ def test_cfg5_mixed_tracks_10_cars_vs_oracle():
     tracks = sorted(f for f in os.listdir(TRACKS) if f.endswith(".track"))
     E, C, S = 128, 10, 900
     files = [os.path.join(TRACKS, tracks[e % 8]) for e in range(E)]
-    envs = make_envs(E, C, files, [1, 12])
+    envs = make_envs(E, C, files, [1, 12, 12], fused=(2,))
     orc = OracleGroups(files, C)
     stagger = {7 * e: e for e in range(8, E)}        # envs 8.. reset at staggered steps (ages spread)
     t = closed_loop_vs_oracle(envs, orc, S, seed=23, stagger=stagger)
@@ -60,7 +60,7 @@ def test_bench_workload_full_episode_vs_oracle():
     from oracle_lib import OracleGroups
     E, C, S = 48, 10, 10830
     path = os.path.join(TRACKS, "daytona.track")
-    envs = make_envs(E, C, path, [12, 1])
+    envs = make_envs(E, C, path, [12, 1, 12], fused=(2,))
     orc = OracleGroups([path] * E, C, shards=8)
     stagger = {225 * e: e for e in range(1, E)}
     t = closed_loop_vs_oracle(envs, orc, S, seed=31, stagger=stagger)
@@ -80,7 +80,7 @@ def test_cfg2_one_car_layouts_vs_oracle():
     from oracle_lib import OracleGroups
     E, C, S = 256, 1, 2500
     path = os.path.join(TRACKS, "daytona.track")
-    envs = make_envs(E, C, path, [8, 128, 1])
+    envs = make_envs(E, C, path, [8, 128, 1, 8], fused=(3,))
     envs[2].set_sensor_lanes(4)          # the small batch's default is 16 sensor lanes per car; pin 4 too
     orc = OracleGroups([path] * E, C, shards=4)
     stagger = {9 * e: e for e in range(1, E)}

@@ -251,3 +251,30 @@ def test_envs_per_block_switch_mid_run():
     a.rollout(3, 100, seed=9, step0=400); b.rollout(3, 100, seed=9, step0=400)
     assert torch.equal(a.obs, b.obs) and torch.equal(a.get_state(), b.get_state())
     a.close(); b.close()
+
+
+def test_fused_model_logic_kernel_identical():
+    """nascar_set_fused_logic: the model + logic step as one launch (each workgroup runs its envs' logic when its own
+    cars' physics is done) gives the two-launch path's results bit for bit -- per step with terminal observations,
+    through the sharded rollout, and with the car-contact extension on (its pass sits between the two phases)."""
+    from nascargymnasium_amd.batched import BatchedCarEnv
+    E, C = 48, 10
+    path = os.path.join(TRACKS, "daytona.track")
+    a = BatchedCarEnv(E, C, path, device="cuda:0", envs_per_block=12)
+    b = BatchedCarEnv(E, C, path, device="cuda:0", envs_per_block=12)
+    b.set_fused_logic(True)
+    a.reset(); b.reset()
+    for k in range(600):
+        if k == 400:
+            a.set_car_contact(True); b.set_car_contact(True)
+        a.step_driven(3, seed=3, step=k, auto_reset=True, terminal_obs=True)
+        b.step_driven(3, seed=3, step=k, auto_reset=True, terminal_obs=True)
+        assert torch.equal(a.obs, b.obs) and torch.equal(a.reward, b.reward), k
+        assert torch.equal(a.car_flags, b.car_flags) and torch.equal(a.env_flags, b.env_flags), k
+        assert torch.equal(a.terminal_obs, b.terminal_obs), k
+    ra = a.rollout(3, 100, seed=3, step0=600, trajectory=True)
+    rb = b.rollout(3, 100, seed=3, step0=600, trajectory=True)
+    for x, y in zip(ra, rb):
+        assert torch.equal(x, y)
+    assert torch.equal(a.get_state(), b.get_state())
+    a.close(); b.close()

@@ -19,6 +19,13 @@ for L in ab_base ab_small; do
 done
 cd "$GRAFT_REPO_ROOT"
 ROUNDS=2 bash tools/ab3.sh tools/ab_ilds0.so tools/ab_base.so tools/ab_rolled.so tools/ab_small.so || exit $?
+for r in 1 2; do   # the fused model + logic kernel on the product library
+  NASCAR_FUSE_ML=1 timeout -k 10 200 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-secondary \
+    > "$OUT/ab3_fused_$r.log" 2>&1 || exit $?
+  python -c "import json;d=json.loads(open('$OUT/ab3_fused_$r.log').read().strip().splitlines()[-1]);print('fused', $r, round(d['value']/1e6,1), 'M car-steps/s', round(d['ms_per_step']*1000,1), 'us/step', {k: round(v*1000,1) for k, v in d['roofline']['kernel_times_ms'].items()})"
+  timeout -k 10 200 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-secondary > "$OUT/ab3_prod_$r.log" 2>&1 || exit $?
+  python -c "import json;d=json.loads(open('$OUT/ab3_prod_$r.log').read().strip().splitlines()[-1]);print('product', $r, round(d['value']/1e6,1), 'M car-steps/s', round(d['ms_per_step']*1000,1), 'us/step', {k: round(v*1000,1) for k, v in d['roofline']['kernel_times_ms'].items()})"
+done
 for r in 1 2; do
   for L in 16 4; do
     NASCAR_RAY_LPC=$L timeout -k 10 200 python bench.py --envs 4096 --cars 1 --steps 200 --warmup 20 --no-cpu-baseline \
