@@ -763,6 +763,12 @@ struct BodyState { V2 c; float a; V2 v; float w; };
 #ifndef ISLAND_MID
 #define ISLAND_MID 3     // islands of 3 .. ISLAND_MID contacts also solved register-resident (0: off; 4 measured slower)
 #endif
+// ISLAND_TWO = 2: islands of 1-2 contacts have their own register-resident solver; 0: they share the
+// ISLAND_MID one (one solver instance less per island kind: a wave whose lanes hold islands of 1 and of 3 contacts
+// then runs one solver, not two in turn)
+#ifndef ISLAND_TWO
+#define ISLAND_TWO 2
+#endif
 template <int NMAX> struct NUNR { static constexpr int v = NMAX <= 2 || NMAX == ISLAND_MID ? NMAX : 1; };
 // The solvers' iteration loops (6 velocity, 4 / 20 position iterations) index nothing per iteration, so rolled
 // loops keep the constraints in the same registers; unrolled, each island size's solver was copied six times over
@@ -1193,7 +1199,7 @@ __device__ inline void solve(Car& c, const WallSet& S, float dt, float dtRatio, 
   CCOUNT(c, 26, n);   // profile builds: the island's touching contacts and its solve cycles (slot 25)
   CTIME_BEGIN();
 #if ISLAND_MID
-  const int positionSolved = n <= 2 ? solve_island<2>(c, W, cidx, n, dt, dtRatio, friction)
+  const int positionSolved = n <= ISLAND_TWO ? solve_island<2>(c, W, cidx, n, dt, dtRatio, friction)
                            : n <= ISLAND_MID ? solve_island<ISLAND_MID>(c, W, cidx, n, dt, dtRatio, friction)
                                              : solve_island_general(c, W, cidx, n, dt, dtRatio, friction);
 #else
@@ -1538,7 +1544,7 @@ __device__ __forceinline__ void island_solve_toi_n(Car& c, const LWall* W, const
   island_solve_toi_buf<NMAX>(c, W, cidx, n, subdt, friction, vc);
 }
 __device__ inline void island_solve_toi(Car& c, const LWall* W, const int* cidx, int n, float subdt, float friction) {
-  if (n <= 2) island_solve_toi_n<2>(c, W, cidx, n, subdt, friction);
+  if (n <= ISLAND_TWO) island_solve_toi_n<2>(c, W, cidx, n, subdt, friction);
 #if ISLAND_MID
   else if (n <= ISLAND_MID) island_solve_toi_n<ISLAND_MID>(c, W, cidx, n, subdt, friction);
 #endif

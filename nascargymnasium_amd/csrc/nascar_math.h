@@ -107,6 +107,12 @@ __host__ __device__ inline double reduce_large(uint32_t xi, int* np) {
 // glibc sinf and cosf (sysdeps/ieee754/flt-32/s_sinf.c, s_cosf.c; FMA variant) of the same argument in one
 // pass: both share the range reduction, and each result is bit-identical to the separate call (the same
 // operations on the same values).  b2Rot::Set calls sinf then cosf.
+#ifndef SINCOS_NOINLINE
+#define SINCOS_NOINLINE 0   // A/B: one out-of-line copy of b2Rot::Set's sincosf instead of one per call site
+#endif
+#if defined(__HIP_DEVICE_COMPILE__) && SINCOS_NOINLINE
+__attribute__((noinline))
+#endif
 __host__ __device__ inline void glibc_sincosf(float y, float* sp, float* cp) {
   double x = y;
   int n = 0, row = 0;

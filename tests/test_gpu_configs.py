@@ -3,7 +3,7 @@
 * cfg5 -- mixed batch of all 8 .track files at 10 cars per env: every env equals the oracle on its own track,
   every step, under the bench's closed-loop noisy driver with staggered masked resets and in-launch auto-reset
   (reference: the per-env track of src/car_env.py:243-303 / 375-394).
-* the bench workload over a whole episode: 48 x 10 daytona at the bench's 12 envs per workgroup (and at 1), noisy
+* the bench workload over a whole episode: 24 x 10 daytona at the bench's 12 envs per workgroup (and at 1), noisy
   driver, >= 10 810 steps, so every env age the bench's steady-state window holds (0 .. 10 800 steps,
   src/car_env.py:1154) is pinned against the oracle at the layout the bench runs.
 * cfg2's shape (1 car per env) at cfg2's layout (8 envs per workgroup) and at 128 and 1.
@@ -51,18 +51,19 @@ def test_cfg5_mixed_tracks_10_cars_vs_oracle():
 
 @pytest.mark.timeout(1200)
 def test_bench_workload_full_episode_vs_oracle():
-    """The bench's steady-state workload over a whole episode at the bench's layout: 48 x 10 daytona at 12 envs per
-    workgroup (4 full workgroups, 120 live lanes in two waves each, as the bench's 8192 x 10 runs) and at one env per
-    workgroup, noisy driver closed loop inside model_kernel, staggered resets (env e reset at step 225 e, so the env
-    ages of every step spread over the episode as in the bench's settled window), in-launch auto-reset, 10 830 steps.
+    """The bench's steady-state workload over a whole episode at the bench's layout: 24 x 10 daytona at 12 envs per
+    workgroup (2 full workgroups, 120 live lanes in two waves each, as the bench's 8192 x 10 runs; also through the
+    fused model + logic kernel) and at one env per workgroup, noisy driver closed loop inside model_kernel, staggered
+    resets (env e reset at step 450 e, so the env ages of every step spread over the episode as in the bench's
+    settled window), in-launch auto-reset, 10 830 steps.
     Env 0 is never reset by the schedule, so unless an earlier termination ends it, it runs to the 10 800-step time
     limit (src/car_env.py:1154): every env age the bench's window holds is compared with the oracle every step."""
     from oracle_lib import OracleGroups
-    E, C, S = 48, 10, 10830
+    E, C, S = 24, 10, 10830
     path = os.path.join(TRACKS, "daytona.track")
     envs = make_envs(E, C, path, [12, 1, 12], fused=(2,))
     orc = OracleGroups([path] * E, C, shards=8)
-    stagger = {225 * e: e for e in range(1, E)}
+    stagger = {450 * e: e for e in range(1, E)}
     t = closed_loop_vs_oracle(envs, orc, S, seed=31, stagger=stagger)
     for env in envs:
         env.close()
