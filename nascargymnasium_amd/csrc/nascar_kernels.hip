@@ -2006,6 +2006,29 @@ __global__ void __launch_bounds__(SBLOCK) LOGIC_ATTR logic_kernel(Params P, floa
 // the contact-slot region, free once every car of the block has written its contact records back.  Same device
 // code as the two kernels, so the results are identical (tests run both).
 struct FusedLogicLDS { LogicLDS L; TrackLDS TL; };
+// the logic half of model_logic_kernel (inlined: out of line it spilled more, 39 vs 30 VGPRs)
+#ifndef FUSED_LOGIC_NOINLINE
+#define FUSED_LOGIC_NOINLINE 0
+#endif
+#if FUSED_LOGIC_NOINLINE
+__attribute__((noinline))
+#else
+__forceinline__
+#endif
+static __device__ void fused_logic_phase(const Params& P, int tid, int el, int car, int env, int n, float* obs, float* reward,
+                                         uint8_t* car_flags, uint8_t* env_flags, int auto_reset, float* terminal_obs) {
+  FusedLogicLDS& F = *(FusedLogicLDS*)smem;
+  Car c;
+  double sim;
+  int pend_in, reason_in;
+  logic_load(P, env, car, n, c, sim, pend_in, reason_in);
+  TrackDev T = P.tracks[blk_track_of(P, (blockIdx.x + P.blk0))];
+  stage_track_lds(T, F.TL, tid);
+  __syncthreads();
+  T.segs = F.TL.segs; T.prefix = F.TL.prefix;
+  logic_run(P, T, F.TL, F.L, tid, el, car, env, n, c, sim, pend_in, reason_in, obs, reward, car_flags, env_flags, auto_reset,
+            terminal_obs);
+}
 #define MODEL_LOGIC_LDS_BYTES (MODEL_CT_LDS_BYTES > sizeof(FusedLogicLDS) ? MODEL_CT_LDS_BYTES : sizeof(FusedLogicLDS))
 __global__ void __launch_bounds__(SBLOCK) __attribute__((amdgpu_waves_per_eu(MODEL_WPE)))
 model_logic_kernel(Params P, const void* actions, int discrete, int want_term, int policy, uint64_t seed, int64_t step,
@@ -2019,17 +2042,7 @@ model_logic_kernel(Params P, const void* actions, int discrete, int want_term, i
   model_block<true>(P, actions, discrete, want_term, policy, seed, step, pobs, tid, env, n);
   __syncthreads();   // the block's Box2D steps done: body state stored, contact slots written back (LDS free)
   if (P.car_contact) car_contact_block(P, tid, el, car, env, n);   // block-uniform; holds its own barrier
-  FusedLogicLDS& F = *(FusedLogicLDS*)smem;
-  Car c;
-  double sim;
-  int pend_in, reason_in;
-  logic_load(P, env, car, n, c, sim, pend_in, reason_in);
-  TrackDev T = P.tracks[blk_track_of(P, (blockIdx.x + P.blk0))];
-  stage_track_lds(T, F.TL, tid);
-  __syncthreads();
-  T.segs = F.TL.segs; T.prefix = F.TL.prefix;
-  logic_run(P, T, F.TL, F.L, tid, el, car, env, n, c, sim, pend_in, reason_in, obs, reward, car_flags, env_flags, auto_reset,
-            terminal_obs);
+  fused_logic_phase(P, tid, el, car, env, n, obs, reward, car_flags, env_flags, auto_reset, terminal_obs);
 }
 
 // Fused multi-step rollout (nascar_rollout): K env steps of each block's envs in one launch, the actions
