@@ -86,7 +86,7 @@ __device__ __forceinline__ BeamHead beam_head(const BeamGrid& G, int li) {
   for (int k = 0; k < BEAM_HW; ++k) h.w[k] = ldg(G.head + (size_t)li * BEAM_HW + k);
   return h;
 }
-#define WALL_LDS_MAX ((size_t)1024 * sizeof(LWall))   // walls per track the sensor kernels' LDS wall image holds (32 B each)
+#define LDS_PER_CU ((size_t)160 * 1024)   // gfx950: 160 KiB of LDS per CU, all of which one workgroup may declare
 struct TrackDev {
   LWall* walls; int nwall;
   const float4* wfat;  // [nwall] broadphase fat AABBs
@@ -2698,6 +2698,7 @@ extern "C" void nascar_destroy(NascarHandle* h) {
   delete h;
 }
 
+static int sensor_lds_reserve(size_t need);
 static int build_track(HostTrack& t, size_t& lds_out, const double* segments, int32_t nseg, double total_length,
                        const double* walls, int32_t nwall, float beam_cell);
 // wall table exactly as Box2D sees it (float32 transform via glibc sinf/cosf, fat AABB, key)
@@ -2733,7 +2734,12 @@ extern "C" int nascar_add_track(NascarHandle* h, const double* segments, int32_t
     g_track_cache[key] = tb;
   }
   const HostTrack& t = tb->t;
-  h->max_sensor_lds = std::max(h->max_sensor_lds, 2 * sizeof(float4) * t.walls.size() + sizeof(float4) * t.groups.size());
+  const size_t need = 2 * sizeof(float4) * t.walls.size() + sizeof(float4) * t.groups.size();
+  if (need > h->max_sensor_lds) {
+    const int rc = sensor_lds_reserve(need);
+    if (rc < 0) return rc;
+  }
+  h->max_sensor_lds = std::max(h->max_sensor_lds, need);
   h->max_sensor_groups_lds = std::max(h->max_sensor_groups_lds, sizeof(float4) * t.groups.size());
   h->max_lds = std::max(h->max_lds, tb->lds);
   h->tracks.push_back(tb);
@@ -2741,6 +2747,22 @@ extern "C" int nascar_add_track(NascarHandle* h, const double* segments, int32_t
   return (int)h->tracks.size() - 1;
 }
 
+// The sensor wall image (2 float4 per wall + 1 per wall group) lives in the dynamic LDS of the kernels that stage it
+// (ray_sensor_kernel, the fused rollout_kernel); with their static LDS it must fit the CU's 160 KiB, so that bounds
+// the walls a track may have (~4 000 with the fused rollout's static LDS, ~4 900 for the sensor kernel alone; the
+// bundled tracks have 730-732).  Images beyond 64 KiB are declared to the runtime first.
+static int sensor_lds_reserve(size_t need) {
+  const void* kern[] = {(const void*)ray_sensor_kernel<4>, (const void*)ray_sensor_kernel<16>, (const void*)rollout_kernel};
+  for (const void* k : kern) {
+    hipFuncAttributes a;
+    if (hipFuncGetAttributes(&a, k) != hipSuccess) return fail("hipFuncGetAttributes failed");
+    if (a.sharedSizeBytes + need > LDS_PER_CU)
+      return fail("track needs %zu B of LDS for its sensor wall image; with %zu B of static LDS a workgroup has %zu",
+                  need, (size_t)a.sharedSizeBytes, LDS_PER_CU - (size_t)a.sharedSizeBytes);
+    if (need > 64 * 1024) HIPCHK(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)need));
+  }
+  return 0;
+}
 // the device tables of one track (nascar_add_track, on the current device); lds: model_kernel's wall table bytes
 static int build_track(HostTrack& t, size_t& lds_out, const double* segments, int32_t nseg, double total_length,
                        const double* walls, int32_t nwall, float beam_cell) {
@@ -2787,8 +2809,7 @@ static int build_track(HostTrack& t, size_t& lds_out, const double* segments, in
     t.walls.push_back(L);
   }
   size_t lds = sizeof(LWall) * t.walls.size();
-  if (lds > WALL_LDS_MAX) return fail("track has %d walls; the sensor kernels' LDS wall image holds %zu", nwall,
-                                      (size_t)(WALL_LDS_MAX / sizeof(LWall)));
+  if (t.walls.size() > 65535) return fail("track has %d walls; the beam lists index at most 65535", nwall);
   {
     std::vector<LWall> dw(t.walls.begin(), t.walls.end());
     std::vector<float4> fat(t.walls.size());

@@ -90,11 +90,14 @@ def _oracle_sensors(orc, pose):
 def test_sensors_on_random_poses(track, E, C):
     """every pose: beam-list kernel (4 and 16 lanes per car) == wall-group kernel == the oracle's brute-force
     cast, bit for bit"""
+    _check_sensors(os.path.join(TRACKS, track), E, C, zlib.crc32(track.encode()))
+
+
+def _check_sensors(path, E, C, seed):
     from nascargymnasium_amd.batched import BatchedCarEnv
     from nascargymnasium_amd.track import build_walls, load_track
     from oracle_lib import OracleEnv
-    path = os.path.join(TRACKS, track)
-    rng = np.random.default_rng(zlib.crc32(track.encode()))
+    rng = np.random.default_rng(seed)
     walls = build_walls(load_track(path))
     env = BatchedCarEnv(E, C, path, device="cuda:0")
     poses = _poses(rng, walls, E * C)
@@ -138,3 +141,57 @@ def test_beam_cell_size_changes_nothing():
         assert len(bad) == 0, f"{cell} m cells differ from 1 m at {bad[:5].tolist()}"
     with pytest.raises(RuntimeError):
         BatchedCarEnv(4, 1, path, device="cuda:0", beam_cell=0.1)
+
+
+# six 180-degree curves of 180 chords per side: 2 160 + walls, a sensor wall image of ~70 KB (beyond 64 KiB of LDS)
+MANY_WALLS_TRACK = """WIDTH 16
+GRID
+STARTLINE
+STRAIGHT 15
+LEFT 180 400
+LEFT 180 400
+RIGHT 180 250
+RIGHT 180 250
+LEFT 180 300
+LEFT 180 300
+STRAIGHT 40
+"""
+
+
+def test_track_with_many_walls(tmp_path):
+    """A custom track with more walls than the bundled ones (2 000+, whose sensor wall image exceeds 64 KiB of LDS)
+    loads; its sensors equal the oracle's brute-force cast on random poses, and 300 closed-loop steps equal the
+    oracle every step (per-step path), with the sharded and the fused rollout equal to the per-step path."""
+    from nascargymnasium_amd.batched import BatchedCarEnv
+    from nascargymnasium_amd.track import build_walls, load_track
+    from closed_loop import closed_loop_vs_oracle
+    from oracle_lib import OracleGroups
+    path = str(tmp_path / "many_walls.track")
+    with open(path, "w") as f:
+        f.write(MANY_WALLS_TRACK)
+    nwall = len(build_walls(load_track(path)))
+    assert nwall > 2048, nwall
+    _check_sensors(path, 256, 4, 1234)
+    E, C, S = 8, 3, 300
+    env = BatchedCarEnv(E, C, path, device="cuda:0")
+    orc = OracleGroups([path] * E, C, shards=4)
+    t = closed_loop_vs_oracle([env], orc, S, seed=5, stagger={})
+    orc.close()
+    assert t["contact"] >= 0
+    outs = []
+    for streams in (4, 0):   # sharded rollout / fused rollout kernel (its LDS holds the wall image too)
+        b = BatchedCarEnv(E, C, path, device="cuda:0")
+        b.set_rollout_streams(streams)
+        b.reset()
+        b.rollout(3, seed=5, step0=0, steps=S)
+        outs.append(b.obs.cpu().numpy().copy())
+        b.close()
+    ref = BatchedCarEnv(E, C, path, device="cuda:0")
+    ref.reset()
+    for k in range(S):
+        ref.step_driven(3, seed=5, step=k, auto_reset=True)
+    ro = ref.obs.cpu().numpy()
+    ref.close()
+    env.close()
+    for o in outs:
+        assert np.array_equal(o.view(np.uint32), ro.view(np.uint32))
