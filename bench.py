@@ -30,6 +30,9 @@ ALGO_BYTES_PER_CAR_STEP = 1221      # 2 x 528 B state + 8 B acti
 # model_kernel's own share (the dominant kernel's roofline): the SURVEY Appendix B state it reads and writes -- Box2D
 # body 7 + contacts 56 + listener 4 + car 27 + tyres 12 = 106 words, read + written -- plus the 8 B action
 MODEL_ALGO_BYTES_PER_CAR = 2 * 106 * 4 + 8
+# model_logic_kernel (the default: vehicle model + Box2D step + env logic in one launch): the whole step's bytes but
+# the sensor kernel's 64 B of obs[22:38] -- every state word read and written, the action, obs[0:22], reward, flags
+FUSED_ALGO_BYTES_PER_CAR = ALGO_BYTES_PER_CAR_STEP - 16 * 4
 HBM_PEAK_GBS = 8000.0               # MI355X HBM3E spec (MI355X_MICROARCH.md)
 EPISODE_STEPS = 10800               # 180 s time limit at dt = 1/60 (src/car_env.py:1154)
 POLICY_ID = {"uniform": 0, "driver": 1, "sac": 2, "noisy": 3}
@@ -529,8 +532,13 @@ def main():
         per_step = timed(ps, first + W, K, world)
     rank_elapsed = gather_all(elapsed, dev)
     elapsed, kern_ms = reduce_max([elapsed, kern_ms], dev)
-    kt_names = ("model_kernel", "logic_kernel", "ray_sensor_kernel")
+    fused = env.fused_logic
+    if fused:   # model_logic_kernel between events 0 and 1 (events 1 and 2 are recorded back to back)
+        ktimes = {"model_logic_kernel": ktimes["model_kernel"], "ray_sensor_kernel": ktimes["ray_sensor_kernel"]}
+    kt_names = tuple(ktimes)
     ktimes = dict(zip(kt_names, reduce_max([ktimes[k] for k in kt_names], dev)))
+    dom = "model_logic_kernel" if fused else "model_kernel"
+    dom_bytes = FUSED_ALGO_BYTES_PER_CAR if fused else MODEL_ALGO_BYTES_PER_CAR
     if per_step is not None:
         per_step = reduce_max([per_step], dev)[0]
     tally = reduce_sum(tally, dev)
@@ -538,7 +546,7 @@ def main():
     # dominant kernel (model_kernel, whole grid): ITS algorithmic bytes per car (the state it reads and writes + the
     # action) x the cars one launch processes, over its mean launch duration (HIP events around it on its stream,
     # per-step path).  The whole step's bytes over the timed window's step time are `roofline.step`.
-    achieved = E * C * MODEL_ALGO_BYTES_PER_CAR / (ktimes["model_kernel"] * 1e-3) / 1e9
+    achieved = E * C * dom_bytes / (ktimes[dom] * 1e-3) / 1e9
     step_achieved = E * C * ALGO_BYTES_PER_CAR_STEP / (elapsed / K) / 1e9      # the timed window itself
     traffic, tnote = None, "no PMC file for this workload"
     tfile = os.path.join(ROOT, "profiles", "pmc_traffic.json")
@@ -550,9 +558,11 @@ def main():
             tnote = f"profiles/pmc_traffic.json is for another workload ({tj.get('tag')})"
         elif tj.get("source_sha") != source_sha():
             tnote = f"stale: profiles/pmc_traffic.json ({tj.get('tag')}) was measured on other kernel sources"
+        elif tj.get(f"{dom}_bytes") is None:
+            tnote = f"profiles/pmc_traffic.json ({tj.get('tag')}) has no {dom} dispatches"
         else:
-            traffic = tj.get("model_kernel_bytes")
-            tnote = f"model_kernel HBM bytes per whole-grid launch from the rocprofv3 FETCH_SIZE/WRITE_SIZE passes of this " \
+            traffic = tj.get(f"{dom}_bytes")
+            tnote = f"{dom} HBM bytes per whole-grid launch from the rocprofv3 FETCH_SIZE/WRITE_SIZE passes of this " \
                     f"build and workload ({tj.get('tag')}, profiles/pmc_traffic.json; not re-measured in this run); whole " \
                     f"step {tj.get('bytes_per_step', 0) / 1e6:.1f} MB"
     ncs = world * E * C * KT
@@ -566,16 +576,18 @@ def main():
                   if closed and not args.no_stagger else "")) if S else (", from a saved steady state" if args.load_state
                                                                         else ", from reset")
     nshard = env.rollout_streams if step.R else 0
+    step_kernels = ("model_logic_kernel + ray_sensor_kernel" if fused
+                    else "model_kernel + logic_kernel + ray_sensor_kernel")
     if not step.R:
         launch_txt = "per-step kernels (nascar_step_driven)"
-        kernel_txt = "model_kernel + logic_kernel + ray_sensor_kernel (one env step)"
+        kernel_txt = f"{step_kernels} (one env step)"
     elif nshard == 0:
         launch_txt = f"fused rollout kernel, {step.R} steps per launch"
         kernel_txt = f"rollout_kernel ({step.R} fused env steps per launch; per-step time)"
     else:
         launch_txt = (f"sharded rollout: {step.R} steps per nascar_rollout call, envs in {nshard} shards on {nshard} "
                       f"streams (bit-identical to the per-step path)")
-        kernel_txt = (f"model_kernel + logic_kernel + ray_sensor_kernel over {nshard} env shards on {nshard} streams "
+        kernel_txt = (f"{step_kernels} over {nshard} env shards on {nshard} streams "
                       f"(per-step time of a {step.R}-step rollout, HIP events on the caller's stream)")
     out = {
         "metric": "env-steps/sec (cars x envs), daytona 10-car",
@@ -592,13 +604,16 @@ def main():
                                    else ", RCCL gather of obs/reward/flags to rank 0 per step)") if gather else ", no collective)")},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": tnote,
-                     "kernel": "model_kernel (dominant kernel; whole-grid launch on the per-step path, HIP events around "
+                     "kernel": f"{dom} (dominant kernel; whole-grid launch on the per-step path, HIP events around "
                                "each launch on its stream)",
-                     "kernel_ms": ktimes["model_kernel"], "units_per_launch": E * C,
-                     "algo_bytes_per_unit": MODEL_ALGO_BYTES_PER_CAR,
-                     "algo_bytes_note": "model_kernel's share of SURVEY Appendix B: body + contacts + listener + car + "
-                                        "tyre state read and written (848 B) + 8 B action; the whole step's 1221 B per "
-                                        "car-step are used in roofline.step",
+                     "kernel_ms": ktimes[dom], "units_per_launch": E * C,
+                     "algo_bytes_per_unit": dom_bytes,
+                     "algo_bytes_note": ("model_logic_kernel's share of SURVEY 8(d)'s 1221 B per car-step: every state "
+                                         "word read and written (2 x 528 B), the 8 B action, obs[0:22] (88 B), reward and "
+                                         "flags (5 B) -- all but the sensor kernel's 64 B of obs[22:38]" if fused else
+                                         "model_kernel's share of SURVEY Appendix B: body + contacts + listener + car + "
+                                         "tyre state read and written (848 B) + 8 B action")
+                                        + "; the whole step's 1221 B per car-step are used in roofline.step",
                      "kernel_times_ms": ktimes,
                      "step": {"achieved": step_achieved, "frac": step_achieved / HBM_PEAK_GBS, "ms": elapsed / K * 1e3,
                               "algo_bytes_per_car_step": ALGO_BYTES_PER_CAR_STEP,

@@ -118,8 +118,7 @@ int nascar_get_envs_per_block(NascarHandle* h);
 
 /* Lanes per car of the distance-sensor kernel (no reference counterpart: DistanceSensor casts its 16 rays one after
  * another, src/distance_sensor.py:93-115): 4 (each lane walks rays r, r + 4, r + 8, r + 12) or 16 (one ray per
- * lane, for small batches that leave most of the chip idle); 0 = automatic (16 up to 16 384 cars, else 4).
- * Identical results either way. */
+ * lane); 0 = automatic (16).  Identical results either way. */
 int nascar_set_sensor_lanes(NascarHandle* h, int32_t lanes);
 
 /* Cell size (m) of the distance sensors' beam lists for the tracks added to this handle AFTER the call (host-built
@@ -128,11 +127,13 @@ int nascar_set_sensor_lanes(NascarHandle* h, int32_t lanes);
  * per track; 2 m quarters both for slightly longer list walks.  Range [0.5, 8].  Identical results at any size. */
 int nascar_set_beam_cell(NascarHandle* h, float meters);
 
-/* Step kernels (no reference counterpart; identical results): enable != 0 runs the vehicle model + Box2D step and
- * the env logic (disable rules, lap timer, obs[0:22], rewards, termination, auto-reset; src/car_env.py:537-803,
- * 805-1158) as one launch per step, each workgroup starting its envs' logic when its own cars' Box2D steps are done;
- * 0 (default) runs them as two launches. */
+/* Step kernels (no reference counterpart; identical results): enable != 0 (default) runs the vehicle model + Box2D
+ * step and the env logic (disable rules, lap timer, obs[0:22], rewards, termination, auto-reset;
+ * src/car_env.py:537-803, 805-1158) as one launch per step, each workgroup starting its envs' logic when its own cars'
+ * Box2D steps are done; 0 runs them as two launches (model_kernel, logic_kernel).  nascar_get_fused_logic returns the
+ * current setting (-1 for a NULL handle). */
 int nascar_set_fused_logic(NascarHandle* h, int32_t enable);
+int nascar_get_fused_logic(NascarHandle* h);
 
 /* Profiling hook (no reference counterpart; bench.py's per-kernel roofline): events = 4 caller-created timing
  * events (hipEvent_t), recorded by every following whole-grid step (nascar_step / nascar_step_driven) on its

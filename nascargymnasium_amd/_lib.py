@@ -95,6 +95,8 @@ def lib():
     L.nascar_set_beam_cell.restype = ctypes.c_int
     L.nascar_set_fused_logic.argtypes = [vp, i32]
     L.nascar_set_fused_logic.restype = ctypes.c_int
+    L.nascar_get_fused_logic.argtypes = [vp]
+    L.nascar_get_fused_logic.restype = ctypes.c_int
     L.nascar_set_perf_history.argtypes = [vp, i32, vp]
     L.nascar_set_perf_history.restype = ctypes.c_int
     L.nascar_get_info.argtypes = [vp, vp, vp]
@@ -125,7 +127,7 @@ def lib():
 
 
 EXPORTED = ["nascar_create", "nascar_destroy", "nascar_last_error", "nascar_add_track", "nascar_set_env_tracks",
-            "nascar_reset", "nascar_step", "nascar_step_driven", "nascar_rollout", "nascar_get_info", "nascar_set_perf_history", "nascar_set_car_contact", "nascar_set_rollout_streams", "nascar_get_rollout_streams", "nascar_set_envs_per_block", "nascar_get_envs_per_block", "nascar_set_sensor_lanes", "nascar_set_beam_cell", "nascar_set_fused_logic", "nascar_state_bytes", "nascar_get_state",
+            "nascar_reset", "nascar_step", "nascar_step_driven", "nascar_rollout", "nascar_get_info", "nascar_set_perf_history", "nascar_set_car_contact", "nascar_set_rollout_streams", "nascar_get_rollout_streams", "nascar_set_envs_per_block", "nascar_get_envs_per_block", "nascar_set_sensor_lanes", "nascar_set_beam_cell", "nascar_set_fused_logic", "nascar_get_fused_logic", "nascar_state_bytes", "nascar_get_state",
             "nascar_set_state", "nascar_policy_actions", "nascar_set_step_events", "nascar_set_actor", "nascar_set_actor_precision", "nascar_actor_forward",
             "nascar_debug_sincosf", "nascar_debug_sensors"]
 

@@ -106,13 +106,16 @@ class BatchedCarEnv:
 
     def set_fused_logic(self, enable: bool = True):
         """One launch per step for the vehicle model + Box2D step and the env logic (each workgroup runs its envs'
-        logic once its own cars' physics is done) instead of two; identical results."""
+        logic once its own cars' physics is done; the default) or two (False); identical results."""
         _lib.check(self.L.nascar_set_fused_logic(self.h, int(bool(enable))))
-        self.fused_logic = bool(enable)
+
+    @property
+    def fused_logic(self) -> bool:
+        return bool(self.L.nascar_get_fused_logic(self.h))
 
     def set_sensor_lanes(self, lanes: int = 0):
-        """Lanes per car of the distance-sensor kernel: 4 or 16 (one ray per lane), 0 automatic (16 for batches of
-        up to 16 384 cars).  Identical results; a scheduling choice."""
+        """Lanes per car of the distance-sensor kernel: 4 or 16 (one ray per lane), 0 automatic (16).  Identical
+        results; a scheduling choice."""
         _lib.check(self.L.nascar_set_sensor_lanes(self.h, int(lanes)))
 
     def set_perf_history(self, enable: bool = True):

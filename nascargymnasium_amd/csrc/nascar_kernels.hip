@@ -2551,7 +2551,7 @@ struct NascarHandle {
   bool pristine = true;             // no reset / step / rollout / set_state yet: track changes apply at once
   int car_contact = 0;              // nascar_set_car_contact (build-only extension)
   int ray_lanes = 0;                // nascar_set_sensor_lanes: 0 automatic, 4 or 16 lanes per car
-  int fuse_ml = 0;                  // nascar_set_fused_logic: model_logic_kernel instead of model_kernel + logic_kernel
+  int fuse_ml = 1;                  // nascar_set_fused_logic: model_logic_kernel (default) or model_kernel + logic_kernel
   float beam_cell = BEAM_CELL_M;    // nascar_set_beam_cell: cell size (m) of the beam lists of tracks added later
   float* d_vhist = nullptr;  // [VH_RING][N] speed history (nascar_set_perf_history), outside the snapshot arena
   double* d_ctl = nullptr;   // rule-driver state for nascar_policy_actions (inside the arena: snapshots keep it)
@@ -2616,6 +2616,7 @@ extern "C" int nascar_set_fused_logic(NascarHandle* h, int32_t enable) {
   h->fuse_ml = enable != 0;
   return 0;
 }
+extern "C" int nascar_get_fused_logic(NascarHandle* h) { return h ? h->fuse_ml : -1; }
 extern "C" int nascar_set_beam_cell(NascarHandle* h, float meters) {
   if (!h) return fail("null argument");
   if (!(meters >= BEAM_CELL_MIN && meters <= BEAM_CELL_MAX))
@@ -3002,11 +3003,14 @@ static int sensor_impl() {
   if (m < 0) { const char* e = getenv("NASCAR_SENSOR"); m = (e && !strcmp(e, "groups")) ? 0 : 1; }
   return m;
 }
-// Lanes per car of the beam-list sensor kernel.  4 (rays r, r + 4, r + 8, r + 12 per lane) fills the chip at the
-// headline's 81 920 cars (16 measured 62 vs 41.5 us there); a small batch leaves most of the chip idle, and then one
-// ray per lane (16 lanes per car) cuts each car's four sequential walks to one.  NASCAR_RAY_LPC = 4 / 16 overrides.
+// Lanes per car of the beam-list sensor kernel: one ray per lane (16 lanes per car) by default, so each car's four
+// sequential walks (4 lanes per car: rays r, r + 4, r + 8, r + 12 per lane) become one and the kernel's slowest lane
+// is one long walk instead of four.  Round 1 (4 m cells, whole-grid launches) measured 4 lanes faster at the
+// headline's 81 920 cars (41.5 vs 62 us); with 1 m cells and the sharded rollout 16 lanes measure faster there too
+// (driver's command 148.9 / 151.7 vs 158.0 / 155.2 us per step, round 4), as they did for small batches (cfg2).
+// NASCAR_RAY_LPC = 4 / 16 or nascar_set_sensor_lanes overrides.
 #ifndef RAY_LPC16_MAX_CARS
-#define RAY_LPC16_MAX_CARS 16384
+#define RAY_LPC16_MAX_CARS (1 << 30)
 #endif
 static int ray_lpc(const NascarHandle* h) {
   if (h->ray_lanes == 4 || h->ray_lanes == 16) return h->ray_lanes;   // nascar_set_sensor_lanes / NASCAR_RAY_LPC

@@ -18,8 +18,7 @@ def make_envs(E, C, tracks, layouts, fused=(), **kw):
         env = BatchedCarEnv(E, C, tracks, device="cuda:0", envs_per_block=epb, **kw)
         if epb is not None:
             assert env.envs_per_block == epb
-        if i in fused:
-            env.set_fused_logic(True)
+        env.set_fused_logic(i in fused)   # explicit either way (the engine's default is the fused kernel)
         envs.append(env)
     return envs
 
@@ -62,7 +61,7 @@ def closed_loop_vs_oracle(envs, orc, steps, seed, stagger, check_actions=False):
             orc.reset(np.nonzero(done)[0])
             oo = orc.outputs()[0]
         for env in envs:
-            lay = f"envs per block {env.envs_per_block}" + (", fused model + logic" if getattr(env, "fused_logic", False) else "")
+            lay = f"envs per block {env.envs_per_block}" + (", fused model + logic" if env.fused_logic else ", model_kernel + logic_kernel")
             gr, gcf, gef = env.reward.cpu().numpy(), env.car_flags.cpu().numpy(), env.env_flags.cpu().numpy()
             assert np.array_equal(gr, orw), f"step {k} ({lay}): reward mismatch at {np.argwhere(gr != orw)[:5].tolist()}"
             assert np.array_equal(gcf & 1, ocf & 1), f"step {k} ({lay}): disabled flags"

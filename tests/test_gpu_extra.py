@@ -262,6 +262,8 @@ def test_fused_model_logic_kernel_identical():
     path = os.path.join(TRACKS, "daytona.track")
     a = BatchedCarEnv(E, C, path, device="cuda:0", envs_per_block=12)
     b = BatchedCarEnv(E, C, path, device="cuda:0", envs_per_block=12)
+    assert b.fused_logic       # the default
+    a.set_fused_logic(False)   # model_kernel + logic_kernel
     b.set_fused_logic(True)
     a.reset(); b.reset()
     for k in range(600):

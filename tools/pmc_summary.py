@@ -6,8 +6,8 @@ Reads the rocprofv3 CSVs under <out_dir>/{kt,fetch,write}, and writes
   profiles/<tag>_kernel_stats.csv  (rocprofv3 --stats summary, copied verbatim)
   profiles/<tag>_pmc_step.json     (per-dispatch FETCH_SIZE / WRITE_SIZE of the two kernels of a step)
   profiles/pmc_traffic.json        (read by bench.py for roofline.traffic)
-One env step = model_kernel + logic_kernel + ray_sensor_kernel over every workgroup: one launch each (per-step
-path) or one launch each per env shard (sharded rollout, a grid of 1/S of the workgroups).  A run holds both, so
+One env step = model_logic_kernel (the default; model_kernel + logic_kernel with the fused kernel off) +
+ray_sensor_kernel over every workgroup: one launch each (per-step path) or one launch each per env shard (sharded rollout, a grid of 1/S of the workgroups).  A run holds both, so
 every dispatch's counter is scaled to the full grid (value / its grid size x the full grid size) before averaging.
 HBM bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024: FETCH_SIZE/WRITE_SIZE are in KiB and gfx950 FETCH_SIZE tallies
 half the bytes of a wide coalesced read (MI355X_MICROARCH.md "HBM").
@@ -23,7 +23,7 @@ import sys
 from collections import defaultdict
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNELS = ("model_kernel", "logic_kernel", "ray_sensor_kernel")
+KERNELS = ("model_logic_kernel", "model_kernel", "logic_kernel", "ray_sensor_kernel")
 
 
 def _find(d, suffix):
@@ -78,13 +78,15 @@ def _trace_steps(path):
             res[f"{kn}_full_grid_calls"] = len(d)
     spans, steps, run = 0.0, 0.0, []
 
+    mk = "model_logic_kernel" if "model_logic_kernel" in full else "model_kernel"   # one per env step
+
     def close(run):
         nonlocal spans, steps
         if run:
-            mg = sum(g for _, _, k, g in run if k == "model_kernel")
+            mg = sum(g for _, _, k, g in run if k == mk)
             if mg:
                 spans += max(e for _, e, _, _ in run) - min(s for s, _, _, _ in run)
-                steps += mg / full["model_kernel"]
+                steps += mg / full[mk]
     for r in rows:
         if r[3] < full[r[2]]:
             run.append(r)
@@ -129,18 +131,20 @@ def main():
     w = _find(os.path.join(out, "write"), "counter_collection.csv")
     if f and w:
         tot_f = tot_w = 0.0
-        ok = True
+        seen = []
         for kn in KERNELS:
             fv, wv = _per_dispatch(f, "FETCH_SIZE", kn), _per_dispatch(w, "WRITE_SIZE", kn)
             if not (fv and wv):
-                ok = False
                 continue
+            seen.append(kn)
             fk, wk = sum(fv) / len(fv), sum(wv) / len(wv)
             res[f"{kn}_fetch_size_kb"], res[f"{kn}_write_size_kb"] = fk, wk
             res[f"{kn}_bytes"] = (2 * fk + wk) * 1024.0
             tot_f += fk
             tot_w += wk
+        ok = "ray_sensor_kernel" in seen and ("model_logic_kernel" in seen or {"model_kernel", "logic_kernel"} <= set(seen))
         if ok:
+            res["step_kernels"] = seen
             res.update(fetch_size_kb=tot_f, write_size_kb=tot_w, bytes_per_step=(2 * tot_f + tot_w) * 1024.0,
                        bytes_per_step_uncorrected=(tot_f + tot_w) * 1024.0)
             if "envs" in res:
@@ -149,7 +153,8 @@ def main():
     if "bytes_per_step" in res and "envs" in res and "source_sha" in res:
         json.dump({k: res[k] for k in ("envs", "cars", "track", "policy", "workload", "source_sha", "bytes_per_step", "bytes_per_step_uncorrected",
                                        "bytes_per_car_step", "fetch_size_kb", "write_size_kb", "tag",
-                                       "model_kernel_bytes", "logic_kernel_bytes", "ray_sensor_kernel_bytes") if k in res},
+                                       "step_kernels", "model_logic_kernel_bytes", "model_kernel_bytes", "logic_kernel_bytes",
+                                       "ray_sensor_kernel_bytes") if k in res},
                   open(os.path.join(prof, "pmc_traffic.json"), "w"), indent=1)
     print(json.dumps(res, indent=1))
 
