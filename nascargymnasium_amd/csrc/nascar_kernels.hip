@@ -1507,10 +1507,10 @@ __device__ __forceinline__ void ray_block_batched(const Params& P, const TrackDe
 }
 // LPC lanes per car, BLOCK / LPC cars per workgroup; `sub` sensor workgroups per step-kernel workgroup (enough for
 // its epb * C cars)
-template <int LPC>
-__global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(RSENSOR_WPE)))
+template <int LPC, int RB = BLOCK>
+__global__ void __launch_bounds__(RB) __attribute__((amdgpu_waves_per_eu(RSENSOR_WPE)))
 ray_sensor_kernel(Params P, float* obs, float* terminal_obs, int passes, int SUB) {
-  constexpr int CPW = BLOCK / LPC;
+  constexpr int CPW = RB / LPC;
   const int bx = blockIdx.x, b = bx / SUB + P.blk0, sub = bx % SUB;
   const int t = threadIdx.x, lc = t / LPC, r = t - lc * LPC;
   const int C = P.C;
@@ -1521,7 +1521,7 @@ ray_sensor_kernel(Params P, float* obs, float* terminal_obs, int passes, int SUB
   {
     float4* s_w = (float4*)smem;
     const int nw2 = 2 * T.nwall;
-    for (int k = t; k < nw2; k += BLOCK) s_w[k] = ldg(T.swall + k);
+    for (int k = t; k < nw2; k += RB) s_w[k] = ldg(T.swall + k);
     __syncthreads();
   }
   if (env < 0) return;
@@ -2551,6 +2551,7 @@ struct NascarHandle {
   bool pristine = true;             // no reset / step / rollout / set_state yet: track changes apply at once
   int car_contact = 0;              // nascar_set_car_contact (build-only extension)
   int ray_lanes = 0;                // nascar_set_sensor_lanes: 0 automatic, 4 or 16 lanes per car
+  int sensor_block = BLOCK;         // threads per ray_sensor_kernel workgroup at 16 lanes per car (256 / 512 / 1024)
   int fuse_ml = 1;                  // nascar_set_fused_logic: model_logic_kernel (default) or model_kernel + logic_kernel
   float beam_cell = BEAM_CELL_M;    // nascar_set_beam_cell: cell size (m) of the beam lists of tracks added later
   float* d_vhist = nullptr;  // [VH_RING][N] speed history (nascar_set_perf_history), outside the snapshot arena
@@ -2642,6 +2643,10 @@ extern "C" int nascar_create(const NascarConfig* cfg, NascarHandle** out) {
   h->epb = auto_epb(h->E, h->C, cfg->device);
   if (const char* ev = getenv("NASCAR_RAY_LPC")) h->ray_lanes = atoi(ev);   // A/B
   if (const char* ev = getenv("NASCAR_FUSE_ML")) h->fuse_ml = atoi(ev) != 0;   // A/B
+  if (const char* ev = getenv("NASCAR_RBLOCK")) {   // A/B
+    const int rb = atoi(ev);
+    if (rb == 256 || rb == 512 || rb == 1024) h->sensor_block = rb;
+  }
   if (const char* ev = getenv("NASCAR_BEAM_CELL")) {
     const float v = (float)atof(ev);
     if (v >= BEAM_CELL_MIN && v <= BEAM_CELL_MAX) h->beam_cell = v;
@@ -2753,7 +2758,9 @@ extern "C" int nascar_add_track(NascarHandle* h, const double* segments, int32_t
 // the walls a track may have (~4 000 with the fused rollout's static LDS, ~4 900 for the sensor kernel alone; the
 // bundled tracks have 730-732).  Images beyond 64 KiB are declared to the runtime first.
 static int sensor_lds_reserve(size_t need) {
-  const void* kern[] = {(const void*)ray_sensor_kernel<4>, (const void*)ray_sensor_kernel<16>, (const void*)rollout_kernel};
+  const void* kern[] = {(const void*)ray_sensor_kernel<4>, (const void*)ray_sensor_kernel<16>,
+                        (const void*)ray_sensor_kernel<16, 512>, (const void*)ray_sensor_kernel<16, 1024>,
+                        (const void*)rollout_kernel};
   for (const void* k : kern) {
     hipFuncAttributes a;
     if (hipFuncGetAttributes(&a, k) != hipSuccess) return fail("hipFuncGetAttributes failed");
@@ -3023,9 +3030,18 @@ static void launch_sensors_impl(NascarHandle* h, const Params& P, int nb, float*
     const size_t rlds = h->max_sensor_lds;   // >= 2 float4 per wall
     const int cars = h->epb * h->C;          // cars per step-kernel workgroup
     if (ray_lpc(h) == 16) {
-      const int sub = (cars + BLOCK / 16 - 1) / (BLOCK / 16);
-      hipLaunchKernelGGL(ray_sensor_kernel<16>, dim3(nb * sub), dim3(BLOCK), rlds, (hipStream_t)stream, P, obs,
-                         terminal_obs, passes, sub);
+      // every sensor workgroup stages the whole wall image: larger workgroups stage it for more cars
+      const int rb = h->sensor_block;
+      const int sub = (cars + rb / 16 - 1) / (rb / 16);
+      if (rb == 1024)
+        hipLaunchKernelGGL((ray_sensor_kernel<16, 1024>), dim3(nb * sub), dim3(rb), rlds, (hipStream_t)stream, P, obs,
+                           terminal_obs, passes, sub);
+      else if (rb == 512)
+        hipLaunchKernelGGL((ray_sensor_kernel<16, 512>), dim3(nb * sub), dim3(rb), rlds, (hipStream_t)stream, P, obs,
+                           terminal_obs, passes, sub);
+      else
+        hipLaunchKernelGGL((ray_sensor_kernel<16, BLOCK>), dim3(nb * sub), dim3(BLOCK), rlds, (hipStream_t)stream, P, obs,
+                           terminal_obs, passes, sub);
     } else {
       const int sub = (cars + BLOCK / RAY_LPC - 1) / (BLOCK / RAY_LPC);
       hipLaunchKernelGGL(ray_sensor_kernel<RAY_LPC>, dim3(nb * sub), dim3(BLOCK), rlds, (hipStream_t)stream, P, obs,
