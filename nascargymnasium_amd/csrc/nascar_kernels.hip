@@ -1432,7 +1432,8 @@ __device__ __forceinline__ void ray_lane(const Params& P, const TrackDev& T, con
 // through ray_lane per car.  Same walks and results as ray_lane.
 __device__ __forceinline__ void ray_block_batched(const Params& P, const TrackDev& T, const float4* __restrict__ sw,
                                                   float* obs, int passes) {
-  static_assert(RAY_LPC == 4 && SBLOCK / RAY_LPC == 32, "batched sensor mapping");
+  static_assert(RAY_LPC == 4, "batched sensor mapping");
+  constexpr int CPR = SBLOCK / RAY_LPC;   // cars per round: NJ rounds cover the block's SBLOCK slots
   constexpr int NJ = 4, RPL = 4;
   const int t = threadIdx.x, r = t & 3, C = P.C;
   const BeamGrid G = T.beam;
@@ -1442,7 +1443,7 @@ __device__ __forceinline__ void ray_block_batched(const Params& P, const TrackDe
   double2 cs[NJ];
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
-    const int lc = (t >> 2) + 32 * j, el = lc / C, car = lc - el * C;
+    const int lc = (t >> 2) + CPR * j, el = lc / C, car = lc - el * C;
     const int env = blk_env_of(P, el, blockIdx.x * P.epb + el);
     ok[j] = env >= 0;
     n[j] = ok[j] ? env * C + car : 0;
@@ -1476,20 +1477,24 @@ __device__ __forceinline__ void ray_block_batched(const Params& P, const TrackDe
     if (!ok[j]) continue;                    // uniform over the car's quad
     const V2 p1 = V(pa[j].x, pa[j].y);
     float v[RPL] = {0.0f, 0.0f, 0.0f, 0.0f};
+    // the car's four heads / end points as named values rotated one place per ray (a select on the ray index
+    // became a dynamically indexed array in scratch memory)
+    BeamHead h0 = hd[j][0], h1 = hd[j][1], h2 = hd[j][2], h3 = hd[j][3];
+    V2 e0 = p2[j][0], e1 = p2[j][1], e2 = p2[j][2], e3 = p2[j][3];
 #pragma unroll 1
     for (int q = 0; q < RPL; ++q) {
       const int i = r + RAY_LPC * q;
-      const V2 e = q == 0 ? p2[j][0] : q == 1 ? p2[j][1] : q == 2 ? p2[j][2] : p2[j][3];
+      const V2 e = e0;
       const float dx = (e.x - p1.x) * 0.004f, dy = (e.y - p1.y) * 0.004f;   // cull only
       float bi;
       if (base[j] >= 0) {
-        const BeamHead h = q == 0 ? hd[j][0] : q == 1 ? hd[j][1] : q == 2 ? hd[j][2] : hd[j][3];
         const int sl = (slot0[j] & ~15) | ((slot0[j] - i) & 15);
-        bi = ray_walk(G, sw, base[j] + sl, h, p1, e, dx, dy);
+        bi = ray_walk(G, sw, base[j] + sl, h0, p1, e, dx, dy);
       } else {
         bi = ray_fallback(T, p1, e.x, e.y, dx, dy, pa[j].z, i);
       }
       put4(v, q, sensor_value(bi));
+      h0 = h1; h1 = h2; h2 = h3; e0 = e1; e1 = e2; e2 = e3;
     }
     float o[4];
     quad_transpose(v, o, r);
@@ -1499,7 +1504,7 @@ __device__ __forceinline__ void ray_block_batched(const Params& P, const TrackDe
   if (passes & 2) {
 #pragma unroll 1
     for (int j = 0; j < NJ; ++j) {
-      const int lc = (t >> 2) + 32 * j, el = lc / C, car = lc - el * C;
+      const int lc = (t >> 2) + CPR * j, el = lc / C, car = lc - el * C;
       const int env = blk_env_of(P, el, blockIdx.x * P.epb + el);
       if (env >= 0) ray_lane(P, T, sw, env * C + car, r, obs, nullptr, 2);
     }

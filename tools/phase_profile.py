@@ -239,6 +239,7 @@ def main():
     if a.rollout:
         import time
         buf.zero_()
+        env.set_rollout_streams(0)   # the fused rollout kernel (its per-wave phase counters)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         env.rollout(3 if a.load_state else 0, a.rollout, seed=0, step0=k0 + a.warmup + a.steps)
@@ -253,6 +254,9 @@ def main():
         for k, name in enumerate(["policy + model (+ barrier)", "logic (+ barrier)", "sensors (+ barrier)"]):
             print(f"  {name:28s} mean {per[:, k].mean():9.0f}  p90 {np.percentile(per[:, k], 90):9.0f}  "
                   f"max {per[:, k].max():9.0f}")
+        print(f"  per-wave totals over the launch (cycles per step): p50 {np.percentile(tot, 50):.0f}, p90 "
+              f"{np.percentile(tot, 90):.0f}, p99 {np.percentile(tot, 99):.0f}, max {tot.max():.0f} -- the launch lasts as "
+              f"long as its slowest workgroup's sum over the steps")
     L.nascar_debug_profile(ctypes.c_void_p(0))
     env.close()
 
