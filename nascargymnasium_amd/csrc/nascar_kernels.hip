@@ -2556,7 +2556,10 @@ struct NascarHandle {
   bool pristine = true;             // no reset / step / rollout / set_state yet: track changes apply at once
   int car_contact = 0;              // nascar_set_car_contact (build-only extension)
   int ray_lanes = 0;                // nascar_set_sensor_lanes: 0 automatic, 4 or 16 lanes per car
-  int sensor_block = BLOCK;         // threads per ray_sensor_kernel workgroup at 16 lanes per car (256 / 512 / 1024)
+  // threads per ray_sensor_kernel workgroup at 16 lanes per car (256 / 512 / 1024; NASCAR_RBLOCK): every workgroup
+  // stages the whole sensor wall image in LDS, so larger workgroups stage it once for more cars.  Driver's command
+  // (2 A/B rounds, round 4): 256 151.9 / 150.3, 512 147.3 / 147.9, 1024 151.4 / 154.4 us per step
+  int sensor_block = 512;
   int fuse_ml = 1;                  // nascar_set_fused_logic: model_logic_kernel (default) or model_kernel + logic_kernel
   float beam_cell = BEAM_CELL_M;    // nascar_set_beam_cell: cell size (m) of the beam lists of tracks added later
   float* d_vhist = nullptr;  // [VH_RING][N] speed history (nascar_set_perf_history), outside the snapshot arena
