@@ -3039,7 +3039,8 @@ static void launch_sensors_impl(NascarHandle* h, const Params& P, int nb, float*
     const int cars = h->epb * h->C;          // cars per step-kernel workgroup
     if (ray_lpc(h) == 16) {
       // every sensor workgroup stages the whole wall image: larger workgroups stage it for more cars
-      const int rb = h->sensor_block;
+      int rb = h->sensor_block;
+      while (rb > BLOCK && rb / 2 >= cars * 16) rb /= 2;   // no wider than a step workgroup's cars need (small batches)
       const int sub = (cars + rb / 16 - 1) / (rb / 16);
       if (rb == 1024)
         hipLaunchKernelGGL((ray_sensor_kernel<16, 1024>), dim3(nb * sub), dim3(rb), rlds, (hipStream_t)stream, P, obs,
