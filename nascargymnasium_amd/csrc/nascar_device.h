@@ -761,7 +761,12 @@ struct BodyState { V2 c; float a; V2 v; float w; };
 #define VC_END(i) (void)0
 #endif
 #ifndef ISLAND_MID
-#define ISLAND_MID 3     // islands of 3 .. ISLAND_MID contacts also solved register-resident (0: off; 4 measured slower)
+// islands of 3 .. ISLAND_MID contacts also solved register-resident (0: off).  2 (round 4): 3-contact islands go to the
+// LDS general solver -- the fully unrolled 3-contact register solver took ~50 k cycles against ~19 k for 1-2 contacts,
+// and dropping it leaves model_kernel / model_logic_kernel spill-free (233 / 244 VGPRs instead of 256 with 15 / 22
+// spilled): driver's command 148.1 / 149.7 -> 143.3 / 144.8 us per step.  (3 measured faster in round 2, before the
+// general island moved out of scratch memory; 4 slower.)
+#define ISLAND_MID 2
 #endif
 // ISLAND_TWO = 2: islands of 1-2 contacts have their own register-resident solver; 0: they share the
 // ISLAND_MID one (one solver instance less per island kind: a wave whose lanes hold islands of 1 and of 3 contacts
