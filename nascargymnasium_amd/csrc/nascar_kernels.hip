@@ -1622,7 +1622,7 @@ __device__ __forceinline__ void model_car(const Params& P, Car& c, int n, const 
 #define CT_LDS_STRIDE ((CT_LDS_CAP * sizeof(DContact) / 16) % 2 ? CT_LDS_CAP * sizeof(DContact) : CT_LDS_CAP * sizeof(DContact) + 16)
 #define MODEL_CT_LDS_BYTES (MODEL_CT_LDS ? (size_t)SBLOCK * CT_LDS_STRIDE : (size_t)0)
 #ifndef MODEL_WPE
-#define MODEL_WPE 2   // 2 waves/SIMD (248 VGPRs, no spills, no scratch since the LDS general island; round 1: 1 wave/SIMD
+#define MODEL_WPE 2   // 2 waves/SIMD (233 VGPRs, 244 fused with the logic, no spills since the LDS islands; round 1: 1 wave/SIMD
                       // with 256 + 44 AGPRs measured 103.6 vs 100.6 us/step)
 #endif
 // policy >= 0: the actions come from device action source `policy` (policy_car, nascar_step_driven) on the
