@@ -61,14 +61,15 @@ def _oracle_shard(track, cars, E, seed, budget_s, out, slot):
     env = OracleEnv(track, E, cars)
     obs = env.reset()[0]
     drv = NoisyRuleDriver(E * cars, seed)
-    steps, t0 = 0, time.perf_counter()
+    steps, contact, t0 = 0, 0, time.perf_counter()
     while time.perf_counter() - t0 < budget_s:
-        obs, _, _, ef = env.step(drv.actions(obs, steps))
+        obs, _, cf, ef = env.step(drv.actions(obs, steps))
+        contact += int(((cf & 4) != 0).sum())   # car flag bit 2: collision impulse this step (as the GPU tally)
         for e in np.nonzero((ef[:, 0] != 0) | (ef[:, 1] != 0))[0]:
             env.reset(int(e))
             obs = env.outputs()[0]
         steps += 1
-    out[slot] = (E * cars * steps, time.perf_counter() - t0, steps)
+    out[slot] = (E * cars * steps, time.perf_counter() - t0, steps, contact)
     env.close()
 
 
@@ -123,12 +124,15 @@ def cpu_baseline(track, cars, budget_s=12.0, threads=None):
     for t in th:
         t.join()
     rate = sum(r[0] for r in res) / max(r[1] for r in res)
+    contact = sum(r[3] for r in res) / max(1, sum(r[0] for r in res))
     return {"value": rate, "unit": "car-steps/s", "cores": threads, "kind": "port",
             "host": host_txt,
             "sample": f"oracle (C restatement of the reference path incl. Box2D subset) on {os.path.basename(track)}, "
                       f"noisy rule driver from reset (first ~{min(r[2] for r in res)} steps; the CPU cannot afford "
                       f"the GPU run's 10 800-step settle): {threads} host threads x one shard of {E} envs x {cars} cars, "
-                      f"~{budget_s / 2:.0f} s each; 1 thread alone: {rate1:.0f} car-steps/s; host: {host_txt}"}
+                      f"~{budget_s / 2:.0f} s each; 1 thread alone: {rate1:.0f} car-steps/s; wall contact in "
+                      f"{100 * contact:.2f} % of the sample's car-steps (the GPU window's workload_stats.contact_frac "
+                      f"is the steady state's); host: {host_txt}"}
 
 
 def reduce_max(values, device):
