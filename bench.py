@@ -51,19 +51,28 @@ def source_sha():
     return h.hexdigest()[:16]
 
 
-def _oracle_shard(track, cars, E, seed, budget_s, out, slot):
+def _oracle_shard(track, cars, E, seed, budget_s, out, slot, init=None, init_seed=0):
     """One host thread: its own OracleEnv shard of E envs x C cars driven by the host restatement of the
     noisy rule driver (tests/drivers.py, same counter hash as the device), auto-reset, ~budget_s of stepping
     (the oracle's C step releases the GIL inside ctypes, so shards on threads run in parallel)."""
     import numpy as np
     from drivers import NoisyRuleDriver
-    from oracle_lib import OracleEnv
+    from oracle_lib import OracleEnv, inject_gpu_state
     env = OracleEnv(track, E, cars)
-    obs = env.reset()[0]
     drv = NoisyRuleDriver(E * cars, seed)
+    step0 = 0
+    if init is None:
+        obs = env.reset()[0]
+    else:   # continue from the GPU's steady state: envs `genvs` of the GPU's E_gpu x cars engine, driver state included
+        blob, E_gpu, genvs, gobs, step0 = init
+        rows = inject_gpu_state(env, blob, E_gpu, cars, genvs)
+        drv.tb = rows[:, 0].copy()
+        drv.steer, drv.last, drv.lim = (rows[:, j].astype(np.float32) for j in (1, 2, 3))
+        drv.seed = init_seed
+        obs = np.ascontiguousarray(gobs[genvs])
     steps, contact, t0 = 0, 0, time.perf_counter()
     while time.perf_counter() - t0 < budget_s:
-        obs, _, cf, ef = env.step(drv.actions(obs, steps))
+        obs, _, cf, ef = env.step(drv.actions(obs, step0 + steps))
         contact += int(((cf & 4) != 0).sum())   # car flag bit 2: collision impulse this step (as the GPU tally)
         for e in np.nonzero((ef[:, 0] != 0) | (ef[:, 1] != 0))[0]:
             env.reset(int(e))
@@ -103,22 +112,35 @@ def host_cores():
                + (f", declared CPU share OMP_NUM_THREADS={share}" if share else "") + f"; {n} threads used")
 
 
-def cpu_baseline(track, cars, budget_s=12.0, threads=None):
+def cpu_baseline(track, cars, budget_s=12.0, threads=None, steady=None):
     """The CPU oracle (C restatement of the reference path) on a bounded sample of the same workload:
-    16 envs x C cars per shard, noisy rule driver from reset.  First 1 thread for budget_s / 2, then one shard
-    per host thread (threads = every core the process may use, host_cores()) for budget_s / 2 of wall time;
-    `value` is the multi-thread rate (car-steps over the slowest shard's time), the 1-thread rate is in `sample`."""
+    16 envs x C cars per shard, noisy rule driver -- from the GPU run's steady state when `steady` = (state blob,
+    E, obs [E][C][38], step, driver seed) is given (each shard continues 16 of the GPU's envs, every field, contact
+    and driver state injected: tests/oracle_lib.inject_gpu_state, tested bit-exact against the GPU), else from
+    reset.  First 1 thread for budget_s / 2, then one shard per host thread (threads = every core the process may
+    use, host_cores()) for budget_s / 2 of wall time; `value` is the multi-thread rate (car-steps over the slowest
+    shard's time), the 1-thread rate is in `sample`."""
     import threading
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     E = 16
     n_host, host_txt = host_cores()
     if threads is None:
         threads = n_host
+
+    def init(k):
+        if steady is None:
+            return None
+        blob, E_gpu, gobs, step0, _ = steady
+        stride = max(1, E_gpu // (E * (threads + 1)))   # shards spread over the GPU's envs (ages uncorrelated)
+        genvs = [((k * E + i) * stride) % E_gpu for i in range(E)]
+        return blob, E_gpu, genvs, gobs, step0
+    seed = steady[4] if steady is not None else 0
     one = [None]
-    _oracle_shard(track, cars, E, 0, budget_s / 2, one, 0)
+    _oracle_shard(track, cars, E, 0, budget_s / 2, one, 0, init(threads), seed)
     rate1 = one[0][0] / one[0][1]
     res = [None] * threads
-    th = [threading.Thread(target=_oracle_shard, args=(track, cars, E, k, budget_s / 2, res, k)) for k in range(threads)]
+    th = [threading.Thread(target=_oracle_shard, args=(track, cars, E, k, budget_s / 2, res, k, init(k), seed))
+          for k in range(threads)]
     for t in th:
         t.start()
     for t in th:
@@ -128,8 +150,11 @@ def cpu_baseline(track, cars, budget_s=12.0, threads=None):
     return {"value": rate, "unit": "car-steps/s", "cores": threads, "kind": "port",
             "host": host_txt,
             "sample": f"oracle (C restatement of the reference path incl. Box2D subset) on {os.path.basename(track)}, "
-                      f"noisy rule driver from reset (first ~{min(r[2] for r in res)} steps; the CPU cannot afford "
-                      f"the GPU run's 10 800-step settle): {threads} host threads x one shard of {E} envs x {cars} cars, "
+                      + (f"noisy rule driver continuing the GPU run's steady state ({min(r[2] for r in res)}+ steps; "
+                         f"each shard's 16 envs injected from the GPU's state, driver state included)"
+                         if steady is not None else
+                         f"noisy rule driver from reset (first ~{min(r[2] for r in res)} steps)")
+                      + f": {threads} host threads x one shard of {E} envs x {cars} cars, "
                       f"~{budget_s / 2:.0f} s each; 1 thread alone: {rate1:.0f} car-steps/s; wall contact in "
                       f"{100 * contact:.2f} % of the sample's car-steps (the GPU window's workload_stats.contact_frac "
                       f"is the steady state's); host: {host_txt}"}
@@ -636,6 +661,10 @@ def main():
         out["per_step"] = {"value": throughput(world, E, C, K, per_step), "ms_per_step": per_step / K * 1e3,
                            "note": "secondary: the same envs and driver stepped by one whole-batch launch per step "
                                    "(nascar_step_driven), every step waiting for the batch's slowest car"}
+    steady = None   # the steady state the CPU baseline continues from (rank 0 of a 1-GPU run, noisy driver, one track)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.policy == "noisy" and not args.mixed:
+        torch.cuda.synchronize()
+        steady = (env.get_state().cpu().numpy(), E, env.obs.cpu().numpy().reshape(E, C, 38).copy(), base + W + 2 * K, rank)
     if not args.no_secondary and args.policy != "uniform" and not args.gather:
         # secondary, labelled: round 1's workload (uniform U[-1,1]^2 from reset) on a fresh engine
         del step
@@ -653,7 +682,7 @@ def main():
                                              "straight; no contacts, laps or resets) -- an upper bound, not the headline"}
         env = env2
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(tpath, C, args.cpu_budget, args.cpu_threads)
+        out["cpu_baseline"] = cpu_baseline(tpath, C, args.cpu_budget, args.cpu_threads, steady)
     if rank == 0:
         print(json.dumps(out), flush=True)
     env.close()

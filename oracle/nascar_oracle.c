@@ -1080,3 +1080,60 @@ EXPORT void or_car_state(void *h, int idx, double *o) {
         c->lt_has_best, c->lt_crossed, c->lt_has_pos, c->lt_laps, c->disabled, c->has_stuck_start, c->first_step, c->prev_laps };
     memcpy(o, v, sizeof v);
 }
+
+/* ================= state injection (test infrastructure) ==========================
+ * The inverse of or_car_state: a car's full state in the GPU arena's layout (nascar_layout.h) -- the f32 / f64 /
+ * i32 per-car fields in their field order, the 10-sample acceleration ring (acc[slot][lon, lat], slot = acc_head +
+ * k oldest first, as here), the b2Contact records (MAXC x 20 words of nascar::DContact) and the listener's
+ * active-contact keys / first normals -- so the oracle can continue from a state the GPU reached (a steady state
+ * the CPU cannot afford to settle to).  Transient b2Body fields (force, torque, sweep c0 / a0 / alpha0, the proxy
+ * move flag) are zero / equal to the body at a step boundary, as on the GPU. */
+#define GPU_MAXC 16
+EXPORT void or_set_car_full(void *h, int idx, const double *f32v, const double *f64v, const int *i32v,
+                            const double *acc20, const int32_t *ct_words, const int32_t *act_key, const float *act_n) {
+    oenv *e = h; ocar *c = &e->car[idx]; oworld *w = &c->w;
+    w->c.x = (float)f32v[0]; w->c.y = (float)f32v[1]; w->a = (float)f32v[2];
+    w->v.x = (float)f32v[3]; w->v.y = (float)f32v[4]; w->w = (float)f32v[5];
+    w->xf.q.s = (float)f32v[6]; w->xf.q.c = (float)f32v[7]; w->xf.p.x = (float)f32v[8]; w->xf.p.y = (float)f32v[9];
+    w->sleepTime = (float)f32v[10]; w->inv_dt0 = (float)f32v[11];
+    w->fat.lo.x = (float)f32v[12]; w->fat.lo.y = (float)f32v[13]; w->fat.hi.x = (float)f32v[14]; w->fat.hi.y = (float)f32v[15];
+    c->cum_reward = (float)f32v[16]; c->cum_reward_info = (float)f32v[17];
+    w->force.x = w->force.y = 0.0f; w->torque = 0.0f;
+    w->c0 = w->c; w->a0 = w->a; w->alpha0 = 0.0f; w->moved = 0;
+    const double *d = f64v;
+    c->rpm = d[0]; c->pvx = d[1]; c->pvy = d[2]; c->lfm = d[3]; c->slip = d[4]; c->bank = d[5];
+    for (int k = 0; k < 4; ++k) { c->load[k] = d[6 + k]; c->temp[k] = d[10 + k]; c->wear[k] = d[14 + k]; }
+    c->imp = d[18];
+    c->lt_start = d[19]; c->lt_cur = d[20]; c->lt_last = d[21]; c->lt_best = d[22]; c->lt_px = d[23]; c->lt_py = d[24];
+    c->lt_dist = d[25]; c->cum_impact = d[26]; c->stuck_dur = d[27]; c->stuck_sx = d[28]; c->stuck_sy = d[29];
+    c->prev_px = d[30]; c->prev_py = d[31]; c->prog_hist = d[32]; c->back = d[33]; c->prev_back = d[34]; c->imp_at_obs = d[35];
+    const int *v = i32v;
+    w->awake = v[0]; w->nct = v[1]; w->overflow = v[2]; c->acc_len = v[3]; c->acc_head = v[4]; c->imp_present = v[5];
+    c->nact = v[6]; c->lt_timing = v[7]; c->lt_has_last = v[8]; c->lt_has_best = v[9]; c->lt_crossed = v[10];
+    c->lt_has_pos = v[11]; c->lt_laps = v[12]; c->disabled = v[13]; c->has_stuck_start = v[14]; c->first_step = v[15];
+    c->prev_laps = v[16];
+    c->just_disabled = 0;
+    for (int s = 0; s < 10; ++s) { c->acc[s][0] = acc20[2 * s]; c->acc[s][1] = acc20[2 * s + 1]; }
+    for (int i = 0; i < OB_MAXC; ++i) memset(&w->ct[i], 0, sizeof w->ct[i]);
+    for (int i = 0; i < GPU_MAXC; ++i) {   /* the GPU keeps MAXC = 16 records per car (nascar_layout.h) */
+        const int32_t *q = ct_words + 20 * i;
+        ocontact *o = &w->ct[i];
+        o->wall = q[0]; o->flags = q[1]; o->m.type = q[2]; o->m.pointCount = q[3];
+        memcpy(&o->m.localNormal.x, &q[4], 4); memcpy(&o->m.localNormal.y, &q[5], 4);
+        memcpy(&o->m.localPoint.x, &q[6], 4); memcpy(&o->m.localPoint.y, &q[7], 4);
+        for (int p = 0; p < 2; ++p) {
+            const int32_t *pp = q + 8 + 5 * p;
+            memcpy(&o->m.pts[p].localPoint.x, &pp[0], 4); memcpy(&o->m.pts[p].localPoint.y, &pp[1], 4);
+            memcpy(&o->m.pts[p].normalImpulse, &pp[2], 4); memcpy(&o->m.pts[p].tangentImpulse, &pp[3], 4);
+            memcpy(&o->m.pts[p].id, &pp[4], 4);
+        }
+        memcpy(&o->toi, &q[18], 4); o->toiCount = q[19];
+    }
+    for (int i = 0; i < GPU_MAXC; ++i) { c->act_key[i] = act_key[i]; c->act_nx[i] = act_n[2 * i]; c->act_ny[i] = act_n[2 * i + 1]; }
+}
+/* per-env words of the GPU arena: simulated time, created / pending / reason / terminated / truncated */
+EXPORT void or_set_env_full(void *h, int env, double sim_time, int created, int pending, int reason, int term, int trunc) {
+    oenv *e = h;
+    e->sim_time[env] = sim_time; e->created[env] = created; e->pending[env] = pending;
+    e->term_reason[env] = reason; e->terminated[env] = term; e->truncated[env] = trunc;
+}

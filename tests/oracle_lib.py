@@ -194,3 +194,68 @@ def car_state(env, idx, n_fields=71):
     o = np.zeros(n_fields, np.float64)
     L.or_car_state(env.h, idx, _p(o, ctypes.c_double))
     return o
+
+
+# ---------------------------------------------------------------- GPU state -> oracle (state injection)
+GPU_MAXC, N_EI32 = 16, 5
+
+
+def _a256(x):
+    return (x + 255) & ~255
+
+
+def gpu_arena(blob, E, C):
+    """Split a nascar_get_state blob (uint8, the arena of nascar_create: nascar_kernels.hip, nascar_layout.h) into its
+    blocks: per-car f32 / f64 / i32 fields, acceleration ring, contact records (raw words), listener keys / normals,
+    per-env time and words, rule-driver state."""
+    from gpu_state import F32, F64, I32
+    b = np.ascontiguousarray(blob).view(np.uint8)
+    N = E * C
+    out, o = {}, 0
+
+    def take(name, nbytes, dtype, shape):
+        nonlocal o
+        out[name] = b[o:o + nbytes].view(dtype).reshape(shape)
+        o = _a256(o + nbytes)
+    take("f32", 4 * len(F32) * N, np.float32, (len(F32), N))
+    take("f64", 8 * len(F64) * N, np.float64, (len(F64), N))
+    take("i32", 4 * len(I32) * N, np.int32, (len(I32), N))
+    take("acc", 8 * 20 * N, np.float64, (20, N))
+    take("ct", 80 * GPU_MAXC * N, np.int32, (N, GPU_MAXC * 20))
+    take("key", 4 * GPU_MAXC * N, np.int32, (N, GPU_MAXC))
+    take("n", 8 * GPU_MAXC * N, np.float32, (N, GPU_MAXC * 2))
+    take("time", 8 * E, np.float64, (E,))
+    take("ei32", 4 * N_EI32 * E, np.int32, (N_EI32, E))
+    take("ctl", 8 * 4 * N, np.float64, (N, 4))
+    assert o == _a256(len(b)) or o == len(b), (o, len(b))
+    return out
+
+
+def inject_gpu_state(orc, blob, E, C, envs):
+    """Continue OracleEnv `orc` (len(envs) envs x C cars) from the GPU state `blob` of an E x C engine: oracle env i
+    takes GPU env envs[i].  Returns the driver state rows (throttle_brake, steering, last_forward, speed_limit) of
+    the selected cars, to seed the host rule driver (tests/drivers.py) as the device one stands."""
+    A = gpu_arena(blob, E, C)
+    L = orc.L
+    orc.reset()   # every car's world wired to the track (the injected state then overwrites its fields)
+    dp, ip, fp = ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_float)
+    L.or_set_car_full.argtypes = [ctypes.c_void_p, ctypes.c_int, dp, dp, ip, dp, ip, ip, fp]
+    L.or_set_env_full.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_double] + [ctypes.c_int] * 5
+    rows = []
+    for i, ge in enumerate(envs):
+        t = A["ei32"][:, ge]
+        L.or_set_env_full(orc.h, i, float(A["time"][ge]), int(t[0]), int(t[1]), int(t[2]), int(t[3]), int(t[4]))
+        for car in range(C):
+            n = ge * C + car
+            f32 = np.ascontiguousarray(A["f32"][:, n].astype(np.float64))
+            f64 = np.ascontiguousarray(A["f64"][:, n])
+            i32 = np.ascontiguousarray(A["i32"][:, n])
+            acc = np.ascontiguousarray(A["acc"][:, n])
+            ct = np.ascontiguousarray(A["ct"][n])
+            key = np.ascontiguousarray(A["key"][n])
+            nn = np.ascontiguousarray(A["n"][n])
+            L.or_set_car_full(orc.h, i * C + car, _p(f32, ctypes.c_double), _p(f64, ctypes.c_double),
+                              _p(i32, ctypes.c_int32), _p(acc, ctypes.c_double), _p(ct, ctypes.c_int32),
+                              _p(key, ctypes.c_int32), _p(nn, ctypes.c_float))
+            rows.append(A["ctl"][n])
+    return np.array(rows)

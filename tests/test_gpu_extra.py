@@ -280,3 +280,52 @@ def test_fused_model_logic_kernel_identical():
         assert torch.equal(x, y)
     assert torch.equal(a.get_state(), b.get_state())
     a.close(); b.close()
+
+
+def test_oracle_continues_from_gpu_mid_episode_state():
+    """State injection: 48 x 10 daytona cars driven by the device noisy rule driver for 2 000 steps on the GPU alone
+    (bench layout, 12 envs per workgroup; env e reset at step 40 e, so the envs are at different points of their
+    episodes), then the GPU state -- every per-car field, contact record, listener entry, acceleration ring, env
+    word and the driver's own state -- is loaded into the CPU oracle (oracle_lib.inject_gpu_state), and the two
+    continue together for 400 steps: obs, rewards, flags and terminations equal every step.  Parity from a state
+    the oracle did not produce itself (the bench's CPU baseline starts from such a state too)."""
+    from nascargymnasium_amd.batched import BatchedCarEnv
+    from drivers import NoisyRuleDriver
+    from oracle_lib import OracleEnv, inject_gpu_state
+    E, C, S, K, seed = 48, 10, 2000, 400, 11
+    path = os.path.join(TRACKS, "daytona.track")
+    env = BatchedCarEnv(E, C, path, device="cuda:0", envs_per_block=12)
+    env.reset()
+    for k in range(S):
+        if k % 40 == 0 and 0 < k // 40 < E:
+            m = torch.zeros(E, dtype=torch.uint8, device=env.device)
+            m[k // 40] = 1
+            env.reset(m)
+        env.step_driven(3, seed=seed, step=k, auto_reset=True)
+    blob = env.get_state().cpu().numpy()
+    oo = env.obs.cpu().numpy().reshape(E, C, 38).copy()
+    orc = OracleEnv(path, E, C)
+    rows = inject_gpu_state(orc, blob, E, C, list(range(E)))
+    drv = NoisyRuleDriver(E * C, seed=seed)
+    drv.tb = rows[:, 0].copy()
+    drv.steer, drv.last, drv.lim = (rows[:, j].astype(np.float32) for j in (1, 2, 3))
+    contact = 0
+    for k in range(S, S + K):
+        ha = drv.actions(oo, k)
+        env.step_driven(3, seed=seed, step=k, auto_reset=True)
+        oo, orw, ocf, oef = orc.step(ha)
+        done = (oef[:, 0] != 0) | (oef[:, 1] != 0)
+        if done.any():
+            for e in np.nonzero(done)[0]:
+                orc.reset(int(e))
+            oo = orc.outputs()[0]
+        gr, gcf, gef = env.reward.cpu().numpy(), env.car_flags.cpu().numpy(), env.env_flags.cpu().numpy()
+        assert np.array_equal(gr, orw), f"step {k}: reward mismatch at {np.argwhere(gr != orw)[:5].tolist()}"
+        assert np.array_equal(gcf & 1, ocf & 1), f"step {k}: disabled flags"
+        assert np.array_equal((gef & 3) != 0, done), f"step {k}: done flags"
+        go = env.obs.cpu().numpy()
+        bad = np.argwhere(go != oo)
+        assert len(bad) == 0, f"step {k}: obs mismatch at {bad[:5].tolist()} gpu {go[tuple(bad[0])]} oracle {oo[tuple(bad[0])]}"
+        contact += int(((gcf & 4) != 0).sum())
+    orc.close(); env.close()
+    assert contact > 0
