@@ -982,7 +982,8 @@ EXPORT void or_outputs(void *h, float *obs, float *rew, uint8_t *cflags, int32_t
         ocar *c = &e->car[i];
         if (obs) memcpy(obs + i * 38, c->obs, sizeof(float) * 38);
         if (rew) rew[i] = c->reward;
-        if (cflags) cflags[i] = (uint8_t)(c->disabled ? 1 : 0);
+        /* bit 0 disabled, bit 2 collision impulse at this step's observation (nascar.h car_flags) */
+        if (cflags) cflags[i] = (uint8_t)((c->disabled ? 1 : 0) | (c->imp_at_obs != 0.0 ? 4 : 0));
     }
     if (eflags) for (int env = 0; env < e->E; ++env) { eflags[env * 3] = e->terminated[env]; eflags[env * 3 + 1] = e->truncated[env]; eflags[env * 3 + 2] = e->term_reason[env]; }
 }

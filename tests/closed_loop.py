@@ -64,7 +64,7 @@ def closed_loop_vs_oracle(envs, orc, steps, seed, stagger, check_actions=False):
             lay = f"envs per block {env.envs_per_block}" + (", fused model + logic" if env.fused_logic else ", model_kernel + logic_kernel")
             gr, gcf, gef = env.reward.cpu().numpy(), env.car_flags.cpu().numpy(), env.env_flags.cpu().numpy()
             assert np.array_equal(gr, orw), f"step {k} ({lay}): reward mismatch at {np.argwhere(gr != orw)[:5].tolist()}"
-            assert np.array_equal(gcf & 1, ocf & 1), f"step {k} ({lay}): disabled flags"
+            assert np.array_equal(gcf & 5, ocf & 5), f"step {k} ({lay}): disabled / collision flags"
             assert np.array_equal((gef & 3) != 0, done), f"step {k} ({lay}): done flags"
             assert np.array_equal(((gef >> 4) & 7)[done], oef[done, 2]), f"step {k} ({lay}): termination reasons"
             go = env.obs.cpu().numpy()

@@ -321,7 +321,7 @@ def test_oracle_continues_from_gpu_mid_episode_state():
             oo = orc.outputs()[0]
         gr, gcf, gef = env.reward.cpu().numpy(), env.car_flags.cpu().numpy(), env.env_flags.cpu().numpy()
         assert np.array_equal(gr, orw), f"step {k}: reward mismatch at {np.argwhere(gr != orw)[:5].tolist()}"
-        assert np.array_equal(gcf & 1, ocf & 1), f"step {k}: disabled flags"
+        assert np.array_equal(gcf & 5, ocf & 5), f"step {k}: disabled / collision flags"
         assert np.array_equal((gef & 3) != 0, done), f"step {k}: done flags"
         go = env.obs.cpu().numpy()
         bad = np.argwhere(go != oo)

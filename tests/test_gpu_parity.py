@@ -143,7 +143,7 @@ def test_random_batch_vs_oracle(track, E, C, steps):
             assert len(bad) == 0, f"step {k} ({lay}): obs mismatch at {bad[:5].tolist()}: gpu {go[tuple(bad[0])]} oracle {oo[tuple(bad[0])]}"
             assert np.array_equal(gr, orw), f"step {k} ({lay}): reward mismatch"
             assert np.array_equal(gt.cpu().numpy(), oef[:, 0] != 0) and np.array_equal(gtr.cpu().numpy(), oef[:, 1] != 0)
-            assert np.array_equal((env.car_flags.cpu().numpy() & 1), ocf & 1)
+            assert np.array_equal((env.car_flags.cpu().numpy() & 5), ocf & 5)   # disabled, collision
         n_collide += int(((envs[0].car_flags & 4) != 0).sum())
     assert n_collide > 0, "scenario exercised no wall contact"
     for env in envs:
