@@ -134,3 +134,56 @@ def test_cfg3_car_contact_at_talladega_10_cars():
     assert torch.equal(env.get_state(), ref.get_state())
     for x in (env, twin, ref):
         x.close()
+
+
+def test_bench_steady_state_full_size_vs_oracle():
+    """The bench's own workload at its full size and layout: daytona 8192 x 10 at 12 envs per workgroup, settled by
+    bench.settle (10 800 noisy-driver steps, env ages staggered over the episode), then 64 of its envs (spread over the
+    batch) are loaded into the CPU oracle (oracle_lib.inject_gpu_state) and the whole batch and the oracle continue
+    150 steps through the sharded rollout's kernels one step at a time (nascar_step_driven): the 64 envs' obs,
+    rewards, disabled / collision flags and terminations equal the oracle's every step."""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    from nascargymnasium_amd.batched import BatchedCarEnv
+    from oracle_lib import OracleEnv, inject_gpu_state
+    E, C, K, seed = 8192, 10, 150, 0
+    path = os.path.join(TRACKS, "daytona.track")
+    env = BatchedCarEnv(E, C, path, device="cuda:0")
+    assert env.envs_per_block == 12 and env.fused_logic
+    env.reset()
+    st = bench.Stepper(env, "noisy", seed, None, None, 0)
+    bench.settle(env, st, bench.EPISODE_STEPS, True, env.device)
+    blob = env.get_state().cpu().numpy()
+    gobs = env.obs.cpu().numpy().reshape(E, C, 38).copy()
+    pick = [int(x) for x in np.linspace(0, E - 1, 64)]
+    orc = OracleEnv(path, len(pick), C)
+    inject_gpu_state(orc, blob, E, C, pick)
+    # the device driver's noise hash uses each car's global index, so the oracle is fed the device's actions for the
+    # picked cars (the device driver equals the host restatement: tests/closed_loop.py)
+    pk = torch.tensor(pick, device=env.device)
+    oo = gobs[pick]
+    k0 = bench.EPISODE_STEPS
+    contact = 0
+    for k in range(k0, k0 + K):
+        a = env.policy_actions(3, seed=seed, step=k).clone()
+        env.launch_step(a, auto_reset=True)
+        ha = a.view(E, C, 2)[pk].cpu().numpy()
+        oo, orw, ocf, oef = orc.step(ha)
+        done = (oef[:, 0] != 0) | (oef[:, 1] != 0)
+        if done.any():
+            for e in np.nonzero(done)[0]:
+                orc.reset(int(e))
+            oo = orc.outputs()[0]
+        gr = env.reward.view(E, C)[pk].cpu().numpy()
+        gcf = env.car_flags.view(E, C)[pk].cpu().numpy()
+        gef = env.env_flags[pk].cpu().numpy()
+        go = env.obs.view(E, C, 38)[pk].cpu().numpy()
+        assert np.array_equal(gr, orw), f"step {k}: reward mismatch at {np.argwhere(gr != orw)[:5].tolist()}"
+        assert np.array_equal(gcf & 5, ocf & 5), f"step {k}: disabled / collision flags"
+        assert np.array_equal((gef & 3) != 0, done), f"step {k}: done flags"
+        bad = np.argwhere(go != oo)
+        assert len(bad) == 0, f"step {k}: obs mismatch at {bad[:5].tolist()}"
+        contact += int(((gcf & 4) != 0).sum())
+    orc.close(); env.close()
+    assert contact > 0
