@@ -10,8 +10,10 @@ replaced by a counter-hash uniform action), SB3-style auto-reset.  Before timing
 steady state: 10 800 steps (one 180 s episode) during which env e is reset at a staggered step, so that the
 env ages at the start of the timed window are spread uniformly over the episode -- cars are spread round the
 track, touch walls, complete laps, get disabled and auto-reset inside the timed window (the rates are reported
-in `workload_stats`).  A "step" = the driver's policy kernel + one env step (model_kernel, logic_kernel,
-ray_sensor_kernel) over all E*C cars of a rank.  The uniform-U[-1,1]^2-from-reset number of round 1 is kept
+in `workload_stats`).  A "step" = one env step over all E*C cars of a rank: model_logic_kernel (the noisy driver,
+the vehicle + tyre model, the Box2D step and the env logic in one launch; nascar_set_fused_logic(h, 0) splits it
+into model_kernel + logic_kernel) then ray_sensor_kernel, issued on the sharded rollout schedule (4 env shards on 4
+streams, 50 steps per nascar_rollout call; bit-identical to one whole-batch launch per step).  The uniform-U[-1,1]^2-from-reset number of round 1 is kept
 only as the labelled secondary field `uniform_from_reset`.
 Prints ONE JSON line on rank 0 (schema: see DESIGN.md "Measurement").
 """
@@ -59,16 +61,18 @@ def _oracle_shard(track, cars, E, seed, budget_s, out, slot, init=None, init_see
     from drivers import NoisyRuleDriver
     from oracle_lib import OracleEnv, inject_gpu_state
     env = OracleEnv(track, E, cars)
-    drv = NoisyRuleDriver(E * cars, seed)
     step0 = 0
     if init is None:
+        drv = NoisyRuleDriver(E * cars, seed)
         obs = env.reset()[0]
     else:   # continue from the GPU's steady state: envs `genvs` of the GPU's E_gpu x cars engine, driver state included
         blob, E_gpu, genvs, gobs, step0 = init
+        # the driver's noise keyed by the cars' global ids on the GPU, from the GPU's next step index: the sample
+        # continues the GPU run's own action stream (tests/test_gpu_configs.py pins this host driver at full size)
+        drv = NoisyRuleDriver(E * cars, init_seed, ids=[g * cars + c for g in genvs for c in range(cars)])
         rows = inject_gpu_state(env, blob, E_gpu, cars, genvs)
         drv.tb = rows[:, 0].copy()
         drv.steer, drv.last, drv.lim = (rows[:, j].astype(np.float32) for j in (1, 2, 3))
-        drv.seed = init_seed
         obs = np.ascontiguousarray(gobs[genvs])
     steps, contact, t0 = 0, 0, time.perf_counter()
     while time.perf_counter() - t0 < budget_s:
@@ -84,8 +88,10 @@ def _oracle_shard(track, cars, E, seed, budget_s, out, slot, init=None, init_see
 
 def host_cores():
     """(threads to use, description): every core this process may run on -- its affinity mask, capped by a cgroup
-    CPU quota and by the host's declared CPU share (OMP_NUM_THREADS) when set: on the GPU box the affinity mask lists
-    the whole machine while the job's share is 16 cores, and more threads than the share only time-slice."""
+    CPU quota and by the host's declared CPU share when set: NASCAR_CPU_SHARE, else OMP_NUM_THREADS (on the GPU box the
+    affinity mask lists the whole machine while the job's share, OMP_NUM_THREADS, is 16 cores, and more threads than the
+    share only time-slice).  When the share is what binds, the description says so: an OMP_NUM_THREADS set for another
+    reason (e.g. 1) would shrink the baseline -- override with NASCAR_CPU_SHARE or --cpu-threads."""
     aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
     quota = None
     try:
@@ -102,14 +108,20 @@ def host_cores():
                 break
     except OSError:
         pass
-    share = None
-    try:
-        share = int(os.environ["OMP_NUM_THREADS"]) if os.environ.get("OMP_NUM_THREADS") else None
-    except ValueError:
-        pass
+    share, share_var = None, None
+    for var in ("NASCAR_CPU_SHARE", "OMP_NUM_THREADS"):
+        try:
+            if os.environ.get(var):
+                share, share_var = int(os.environ[var]), var
+                break
+        except ValueError:
+            pass
     n = min([aff] + [x for x in (quota, share) if x])
+    binding = share is not None and share == n and share < min([aff] + ([quota] if quota else []))
     return n, (f"{model}; affinity {aff} cores" + (f", cgroup quota {quota} cores" if quota else ", no cgroup quota")
-               + (f", declared CPU share OMP_NUM_THREADS={share}" if share else "") + f"; {n} threads used")
+               + (f", declared CPU share {share_var}={share}" if share else "")
+               + (f" (the binding limit; NASCAR_CPU_SHARE or --cpu-threads override it)" if binding else "")
+               + f"; {n} threads used")
 
 
 def cpu_baseline(track, cars, budget_s=12.0, threads=None, steady=None):
@@ -160,13 +172,54 @@ def cpu_baseline(track, cars, budget_s=12.0, threads=None, steady=None):
                       f"is the steady state's); host: {host_txt}"}
 
 
+COLLECTIVES = []    # this rank's collective calls in issue order (reported by --plumbing runs; every rank must match)
+
+
+def _dist_on():
+    import torch.distributed as dist
+    return dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+
+
+def barrier():
+    import torch.distributed as dist
+    if _dist_on():
+        COLLECTIVES.append("barrier")
+        dist.barrier()
+
+
+def sync(dev):
+    """wait for the device's queued work (no-op for the --plumbing engine on the CPU)"""
+    import torch
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+
+
+class HostEvent:
+    """torch.cuda.Event's record / elapsed_time on the host clock (the --plumbing engine has no device)"""
+
+    def __init__(self):
+        self.t = None
+
+    def record(self, stream=None):
+        self.t = time.perf_counter()
+
+    def elapsed_time(self, end):
+        return (end.t - self.t) * 1e3
+
+
+def new_event(dev):
+    import torch
+    return torch.cuda.Event(enable_timing=True) if dev.type == "cuda" else HostEvent()
+
+
 def reduce_max(values, device):
     """MAX over ranks of per-rank timings (no-op at world size 1).  Ranks own disjoint env shards and
     never exchange simulation data: this is the only collective in the benchmark."""
     import torch
     import torch.distributed as dist
-    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+    if not _dist_on():
         return [float(v) for v in values]
+    COLLECTIVES.append(f"all_reduce_max[{len(values)}]")
     t = torch.tensor([float(v) for v in values], device=device, dtype=torch.float64)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return [float(x) for x in t.tolist()]
@@ -175,8 +228,9 @@ def reduce_max(values, device):
 def reduce_sum(values, device):
     import torch
     import torch.distributed as dist
-    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+    if not _dist_on():
         return [float(v) for v in values]
+    COLLECTIVES.append(f"all_reduce_sum[{len(values)}]")
     t = torch.tensor([float(v) for v in values], device=device, dtype=torch.float64)
     dist.all_reduce(t, op=dist.ReduceOp.SUM)
     return [float(x) for x in t.tolist()]
@@ -186,8 +240,9 @@ def gather_all(value, device):
     """every rank's value (rank order; [value] at world size 1) -- the per-rank timings the MAX is taken over"""
     import torch
     import torch.distributed as dist
-    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+    if not _dist_on():
         return [float(value)]
+    COLLECTIVES.append("all_gather[1]")
     t = torch.tensor([float(value)], device=device, dtype=torch.float64)
     out = [torch.zeros_like(t) for _ in range(dist.get_world_size())]
     dist.all_gather(out, t)
@@ -210,37 +265,6 @@ def launch_ranks(n, argv):
     env = dict(os.environ)
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     return subprocess.run(cmd, env=env).returncode
-
-
-def plumbing(args, world, rank):
-    """--plumbing: the multi-rank launch and reduction path without a GPU (CPU tests): gloo process group, rank r
-    'steps' by sleeping (r + 1) ms per step, then the same barrier-bracketed timing, MAX over ranks, whole-job value
-    and per-rank record as the measured line.  Not a measurement: the line's metric says so."""
-    import torch
-    import torch.distributed as dist
-    if world > 1:
-        dist.init_process_group("gloo")
-    dev = torch.device("cpu")
-    E, C, K = args.envs, args.cars, args.steps
-    if world > 1:
-        dist.barrier()
-    t0 = time.perf_counter()
-    for _ in range(K):
-        time.sleep((rank + 1) * 1e-3)
-    if world > 1:
-        dist.barrier()
-    el = time.perf_counter() - t0
-    per_rank = gather_all(el, dev)
-    elapsed = reduce_max([el], dev)[0]
-    out = {"metric": "plumbing (no GPU, not a measurement)", "value": throughput(world, E, C, K, elapsed),
-           "unit": "car-steps/s", "n_gpus": world, "steps": K, "warmup": args.warmup, "ms_per_step": elapsed / K * 1e3,
-           "ranks": {"world_size": dist.get_world_size() if world > 1 else 1,
-                     "backend": dist.get_backend() if world > 1 else None, "elapsed_s": per_rank},
-           "config": {"envs_per_gpu": E, "cars_per_env": C}}
-    if rank == 0:
-        print(json.dumps(out), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
 
 
 def throughput(world, envs, cars, steps, elapsed_max):
@@ -324,6 +348,104 @@ class Stepper:
             k += n
 
 
+class PlumbingEngine:
+    """--plumbing (CPU tests): a stand-in for BatchedCarEnv with exactly the interface main() uses, on the CPU.  A step
+    sleeps (rank + 1) ms and writes deterministic outputs, so a gloo world-2 run goes through main()'s own settle,
+    timing, statistics and kernel passes, per-step pass, secondary pass, every collective and the JSON line without a
+    GPU.  Not a measurement (the line's metric says so)."""
+
+    def __init__(self, E, C, rank, device):
+        import torch
+        self.E, self.C, self.N, self.rank, self.device = E, C, E * C, rank, torch.device(device)
+        self.obs = torch.zeros(E, C, 38, dtype=torch.float32)
+        self.reward = torch.zeros(E, C, dtype=torch.float32)
+        self.car_flags = torch.zeros(E, C, dtype=torch.uint8)
+        self.env_flags = torch.zeros(E, dtype=torch.uint8)
+        self._actions = torch.zeros(E, C, 2, dtype=torch.float32)
+        self.envs_per_block, self.fused_logic, self.rollout_streams = max(1, 128 // C), True, 4
+        self._events, self.steps_done = None, 0
+
+    def set_rollout_streams(self, streams=4):
+        self.rollout_streams = int(streams)
+
+    def set_car_contact(self, enable=True):
+        pass
+
+    def set_actor(self, weights, precision="fp32"):
+        pass
+
+    def reset(self, env_mask=None):
+        if env_mask is None:
+            self.obs.zero_()
+        else:
+            self.obs[env_mask.bool()] = 0.0
+        return self.obs
+
+    def _advance(self, step):
+        import torch
+        ev = self._events
+        if ev:
+            ev[0].record()
+        time.sleep((self.rank + 1) * 1e-3)
+        if ev:
+            ev[1].record()
+            ev[2].record()
+        n = torch.arange(self.N).view(self.E, self.C)
+        self.obs.fill_(float(step))
+        self.obs[..., 4] = 0.25
+        self.reward.fill_(float(self.rank))
+        self.car_flags.copy_((((n + step) % 7 == 0).to(torch.uint8) * 4) | (((n + step) % 11 == 0).to(torch.uint8) * 8))
+        self.env_flags.copy_(((torch.arange(self.E) + step) % 50 == 0).to(torch.uint8) * 8)
+        self.steps_done += 1
+        if ev:
+            ev[3].record()
+
+    def policy_actions(self, policy, seed=0, step=0, obs=None):
+        return self._actions
+
+    def launch_step(self, actions, auto_reset=False, terminal_obs=False):
+        self._advance(self.steps_done)
+
+    def step_driven(self, policy, seed=0, step=0, auto_reset=True, terminal_obs=False):
+        self._advance(step)
+        return self.obs, self.reward
+
+    def rollout(self, policy, steps, seed=0, step0=0, auto_reset=True, trajectory=False, out=None,
+                obs_trajectory=False):
+        import torch
+        E, C = self.E, self.C
+        if trajectory:
+            if out is None:
+                out = ((torch.empty(steps + 1, E, C, 38),) if obs_trajectory else ()) + (
+                    torch.empty(steps, E, C), torch.empty(steps, E, C, dtype=torch.uint8),
+                    torch.empty(steps, E, dtype=torch.uint8))
+            ot = out[0] if obs_trajectory else None
+            rew, cf, ef = out[-3:]
+            if ot is not None:
+                ot[0].copy_(self.obs)
+        for k in range(steps):
+            self._advance(step0 + k)
+            if trajectory:
+                rew[k].copy_(self.reward); cf[k].copy_(self.car_flags); ef[k].copy_(self.env_flags)
+                if ot is not None:
+                    ot[k + 1].copy_(self.obs)
+        if not trajectory:
+            return self.obs, self.reward, self.car_flags, self.env_flags
+        return (ot if ot is not None else self.obs), rew, cf, ef
+
+    def set_step_events(self, events=None):
+        self._events = events
+
+    def get_state(self):
+        return self.obs.clone().view(-1).view(__import__("torch").uint8)
+
+    def set_state(self, buf):
+        self.obs.view(-1).view(__import__("torch").uint8).copy_(buf)
+
+    def close(self):
+        pass
+
+
 def settle(env, step, n, stagger, dev):
     """bring the envs to the steady state of the workload (not timed): n closed-loop steps, env e reset at
     its staggered step."""
@@ -352,17 +474,16 @@ def settle(env, step, n, stagger, dev):
 
 
 def timed(step, first, K, world):
-    import torch
-    import torch.distributed as dist
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
+    """K steps back to back between a barrier + device synchronisation on both sides; this rank's wall time"""
+    dev = step.env.device
+    sync(dev)
+    barrier()
+    sync(dev)
     # K steps back to back (no per-step events: each event record costs ~5 us of device time between kernels
     # on this stack, which would be charged to the throughput)
     diag = os.environ.get("NASCAR_BENCH_DIAG")
     if diag:      # where the window's wall time goes: GPU span (2 events) vs host enqueue vs sync
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0, e1 = new_event(dev), new_event(dev)
         e0.record()
     t0 = time.perf_counter()
     step.run(first, K)
@@ -371,9 +492,8 @@ def timed(step, first, K, world):
         e1.record()
     if step.gather is not None:
         step.gather.wait()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
+    sync(dev)
+    barrier()
     el = time.perf_counter() - t0
     if diag:
         print(f"[diag] K={K} wall {el * 1e3:.3f} ms, gpu span {e0.elapsed_time(e1):.3f} ms, host enqueue "
@@ -383,14 +503,14 @@ def timed(step, first, K, world):
 
 def stats_pass(env, step, first, KR):
     """after the timed region, KR further steps of the same workload: HIP events on the launch stream around
-    each env step (model_kernel + logic_kernel + ray_sensor_kernel; the policy kernel is outside the
-    brackets) -- or around one fused KR-step rollout launch -- for the roofline, and device-side tallies of
-    what happened in those car-steps."""
+    one KR-step rollout call on the timed schedule (or, on the per-step path, around each env step's
+    model_logic_kernel + ray_sensor_kernel launches), and device-side tallies of what happened in those car-steps."""
     import torch
-    tally = torch.zeros(7, dtype=torch.float64, device=env.device)
+    dev = env.device
+    tally = torch.zeros(7, dtype=torch.float64, device=dev)
     KR_timed = KR
     if step.R:
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0, e1 = new_event(dev), new_event(dev)
         step.run(first, KR, trajectory=True)         # allocates the trajectory buffers outside the bracket
         e0.record()
         step.run(first + KR, KR, trajectory=True)
@@ -406,9 +526,9 @@ def stats_pass(env, step, first, KR):
                               ((cf & 2) != 0).sum(), ((ef & 8) != 0).sum(), ((cf & 128) != 0).sum(),
                               torch.zeros((), device=env.device)]).double()
         tally[6] = env.obs[..., 4].double().sum() * KR    # speed sampled at the window's last step
-        torch.cuda.synchronize()
+        sync(dev)
         return e0.elapsed_time(e1) / KR_timed, tally.tolist(), KR
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(KR)]
+    ev = [(new_event(dev), new_event(dev)) for _ in range(KR)]
     for i in range(KR):
         a = step.actions(first + i)
         ev[i][0].record()
@@ -418,7 +538,7 @@ def stats_pass(env, step, first, KR):
         tally += torch.stack([((cf & 4) != 0).sum(), ((cf & 8) != 0).sum(), ((cf & 1) != 0).sum(),
                               ((cf & 2) != 0).sum(), ((ef & 8) != 0).sum(), ((cf & 128) != 0).sum(),
                               env.obs[..., 4].double().sum()]).double()
-    torch.cuda.synchronize()
+    sync(dev)
     kern_ms = sum(s.elapsed_time(e) for s, e in ev) / KR
     return kern_ms, tally.tolist(), KR
 
@@ -427,13 +547,13 @@ def kernel_pass(env, step, first, KR):
     """per-kernel durations of the whole-grid step (the per-step path, nascar_step_driven / nascar_step): HIP events
     recorded by the engine before model_kernel, after it, after logic_kernel and after the sensor launch, on the launch
     stream (nascar_set_step_events), over KR steps of the same workload.  Returns mean ms per launch of each kernel."""
-    import torch
-    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(KR)]
+    dev = env.device
+    evs = [[new_event(dev) for _ in range(4)] for _ in range(KR)]
     for i in range(KR):
         step.env.set_step_events(evs[i])
         step(first + i)
     step.env.set_step_events(None)
-    torch.cuda.synchronize()
+    sync(dev)
     t = [[e[k].elapsed_time(e[k + 1]) for k in range(3)] for e in evs]
     return {name: sum(r[k] for r in t) / KR for k, name in enumerate(("model_kernel", "logic_kernel", "ray_sensor_kernel"))}
 
@@ -473,8 +593,8 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
-    ap.add_argument("--plumbing", action="store_true", help="CPU tests: the multi-rank launch + reduction path only "
-                    "(gloo, no GPU, no engine; not a measurement)")
+    ap.add_argument("--plumbing", action="store_true", help="CPU tests: main() unchanged on a CPU stand-in engine "
+                    "(PlumbingEngine: sleeps per step), gloo between the ranks; not a measurement")
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ:
@@ -487,20 +607,19 @@ def main():
             print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world} ranks were launched", file=sys.stderr)
             sys.exit(2)
     rank = int(os.environ.get("RANK", "0"))
-    if args.plumbing:
-        plumbing(args, world, rank)
-        return
 
     import torch
     import torch.distributed as dist
-    from nascargymnasium_amd.batched import BatchedCarEnv
     from nascargymnasium_amd.track import track_path
 
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)   # before the process group, so RCCL's barrier binds this rank's GPU
+    if args.plumbing:      # CPU tests: the same main() on the CPU stand-in engine, gloo between the ranks
+        dev = torch.device("cpu")
+    else:
+        torch.cuda.set_device(local)   # before the process group, so RCCL's barrier binds this rank's GPU
+        dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl")
-    dev = torch.device("cuda", local)
+        dist.init_process_group("gloo" if args.plumbing else "nccl")
     E, C, K, W = args.envs, args.cars, args.steps, args.warmup
     closed = args.policy != "uniform"
     S = args.settle if args.settle is not None else (EPISODE_STEPS if closed else 0)
@@ -509,6 +628,9 @@ def main():
     tpath = track_path(args.track)
 
     def make_env():
+        if args.plumbing:
+            return PlumbingEngine(E, C, rank, dev)
+        from nascargymnasium_amd.batched import BatchedCarEnv
         if args.mixed:
             from nascargymnasium_amd.track import available_tracks
             names = available_tracks()
@@ -543,7 +665,7 @@ def main():
     else:   # per-step settle whatever the timed path: each staggered reset lands on its exact step
         settle(env, Stepper(env, args.policy, rank, acts, None, 0), S, closed and not args.no_stagger, dev)
         base = S
-    torch.cuda.synchronize()
+    sync(dev)
     t_settle = time.perf_counter() - t_settle
     if args.save_state:
         torch.save({"state": env.get_state().cpu(), "obs": env.obs.cpu(), "step": base}, args.save_state)
@@ -554,11 +676,13 @@ def main():
     kern_ms, tally, KT = stats_pass(env, step, base + W + K, KR)   # KT: the steps the tallies cover
     ktimes = kernel_pass(env, Stepper(env, args.policy, rank, acts, None, 0), base + W + K + 2 * KR, KR)
     per_step = None
+    next_step = base + W + K + 3 * KR        # the driver's next step index (its counter-hash key)
     if step.R:   # the per-step path on the same envs, timed the same way (labelled secondary)
         ps = Stepper(env, args.policy, rank, acts, None, 0)
-        first = base + W + K + 3 * KR
+        first = next_step
         ps.run(first, W)
         per_step = timed(ps, first + W, K, world)
+        next_step = first + W + K
     rank_elapsed = gather_all(elapsed, dev)
     elapsed, kern_ms = reduce_max([elapsed, kern_ms], dev)
     fused = env.fused_logic
@@ -662,9 +786,10 @@ def main():
                            "note": "secondary: the same envs and driver stepped by one whole-batch launch per step "
                                    "(nascar_step_driven), every step waiting for the batch's slowest car"}
     steady = None   # the steady state the CPU baseline continues from (rank 0 of a 1-GPU run, noisy driver, one track)
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.policy == "noisy" and not args.mixed:
-        torch.cuda.synchronize()
-        steady = (env.get_state().cpu().numpy(), E, env.obs.cpu().numpy().reshape(E, C, 38).copy(), base + W + 2 * K, rank)
+    cpu_leg = rank == 0 and world == 1 and not args.no_cpu_baseline and not args.plumbing
+    if cpu_leg and args.policy == "noisy" and not args.mixed:
+        sync(dev)
+        steady = (env.get_state().cpu().numpy(), E, env.obs.cpu().numpy().reshape(E, C, 38).copy(), next_step, rank)
     if not args.no_secondary and args.policy != "uniform" and not args.gather:
         # secondary, labelled: round 1's workload (uniform U[-1,1]^2 from reset) on a fresh engine
         del step
@@ -681,7 +806,13 @@ def main():
                                      "note": "secondary: uniform actions from reset (cars stay on the start "
                                              "straight; no contacts, laps or resets) -- an upper bound, not the headline"}
         env = env2
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if args.plumbing:   # every rank must have issued the same collectives in the same order
+        seq = list(COLLECTIVES)
+        h = int(hashlib.sha256("|".join(seq).encode()).hexdigest()[:12], 16)
+        hs = gather_all(h, dev)
+        out["metric"] = "plumbing (no GPU, not a measurement)"
+        out["collectives"] = {"rank0": seq, "all_ranks_equal": len(set(hs)) == 1, "ranks": len(hs)}
+    if cpu_leg:
         out["cpu_baseline"] = cpu_baseline(tpath, C, args.cpu_budget, args.cpu_threads, steady)
     if rank == 0:
         print(json.dumps(out), flush=True)

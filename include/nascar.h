@@ -121,9 +121,14 @@ int nascar_get_envs_per_block(NascarHandle* h);
  * lane); 0 = automatic (16).  Identical results either way. */
 int nascar_set_sensor_lanes(NascarHandle* h, int32_t lanes);
 
+/* Threads per workgroup of the 16-lane distance-sensor kernel (no reference counterpart; src/distance_sensor.py:93-115
+ * casts one ray at a time): 256, 512 or 1024 (each workgroup stages the track's wall image in LDS once for
+ * threads / 16 cars); 0 = automatic (512).  Identical results at any size. */
+int nascar_set_sensor_block(NascarHandle* h, int32_t threads);
+
 /* Cell size (m) of the distance sensors' beam lists for the tracks added to this handle AFTER the call (host-built
  * per track in nascar_add_track; no reference counterpart -- DistanceSensor ray-casts against every wall,
- * src/distance_sensor.py:93-115).  Default 1 m (or NASCAR_BEAM_CELL): ~0.8 GB of device lists and ~2 s of host build
+ * src/distance_sensor.py:93-115).  Default 1 m: ~0.8 GB of device lists and ~2 s of host build
  * per track; 2 m quarters both for slightly longer list walks.  Range [0.5, 8].  Identical results at any size. */
 int nascar_set_beam_cell(NascarHandle* h, float meters);
 

@@ -91,6 +91,8 @@ def lib():
     L.nascar_get_envs_per_block.restype = ctypes.c_int
     L.nascar_set_sensor_lanes.argtypes = [vp, i32]
     L.nascar_set_sensor_lanes.restype = ctypes.c_int
+    L.nascar_set_sensor_block.argtypes = [vp, i32]
+    L.nascar_set_sensor_block.restype = ctypes.c_int
     L.nascar_set_beam_cell.argtypes = [vp, ctypes.c_float]
     L.nascar_set_beam_cell.restype = ctypes.c_int
     L.nascar_set_fused_logic.argtypes = [vp, i32]
@@ -127,7 +129,7 @@ def lib():
 
 
 EXPORTED = ["nascar_create", "nascar_destroy", "nascar_last_error", "nascar_add_track", "nascar_set_env_tracks",
-            "nascar_reset", "nascar_step", "nascar_step_driven", "nascar_rollout", "nascar_get_info", "nascar_set_perf_history", "nascar_set_car_contact", "nascar_set_rollout_streams", "nascar_get_rollout_streams", "nascar_set_envs_per_block", "nascar_get_envs_per_block", "nascar_set_sensor_lanes", "nascar_set_beam_cell", "nascar_set_fused_logic", "nascar_get_fused_logic", "nascar_state_bytes", "nascar_get_state",
+            "nascar_reset", "nascar_step", "nascar_step_driven", "nascar_rollout", "nascar_get_info", "nascar_set_perf_history", "nascar_set_car_contact", "nascar_set_rollout_streams", "nascar_get_rollout_streams", "nascar_set_envs_per_block", "nascar_get_envs_per_block", "nascar_set_sensor_lanes", "nascar_set_sensor_block", "nascar_set_beam_cell", "nascar_set_fused_logic", "nascar_get_fused_logic", "nascar_state_bytes", "nascar_get_state",
             "nascar_set_state", "nascar_policy_actions", "nascar_set_step_events", "nascar_set_actor", "nascar_set_actor_precision", "nascar_actor_forward",
             "nascar_debug_sincosf", "nascar_debug_sensors"]
 

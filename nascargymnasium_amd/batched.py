@@ -118,6 +118,10 @@ class BatchedCarEnv:
         results; a scheduling choice."""
         _lib.check(self.L.nascar_set_sensor_lanes(self.h, int(lanes)))
 
+    def set_sensor_block(self, threads: int = 0):
+        """threads per workgroup of the 16-lane sensor kernel: 256, 512 or 1024 (0: automatic, 512); identical results"""
+        _lib.check(self.L.nascar_set_sensor_block(self.h, int(threads)))
+
     def set_perf_history(self, enable: bool = True):
         """Keep Car.velocity_history on the device so the info's `performance` dict is Car.validate_performance
         (src/car.py:1060-1098); a 640-sample float32 ring per car, one 4-byte store per car-step.  Enabled before the
@@ -136,8 +140,9 @@ class BatchedCarEnv:
         seg = np.ascontiguousarray(t.segment_table())
         walls = np.ascontiguousarray(build_walls(t)[:, :4])
         dp = ctypes.POINTER(ctypes.c_double)
-        tid = _lib.check(self.L.nascar_add_track(self.h, seg.ctypes.data_as(dp), seg.shape[0], float(t.total_length),
-                                                 walls.ctypes.data_as(dp), walls.shape[0]))
+        with torch.cuda.device(self.device):   # (the library also brackets its device work with the handle's device)
+            tid = _lib.check(self.L.nascar_add_track(self.h, seg.ctypes.data_as(dp), seg.shape[0], float(t.total_length),
+                                                     walls.ctypes.data_as(dp), walls.shape[0]))
         self.tracks.append(t)
         self._track_id[path] = tid
         return tid

@@ -1690,6 +1690,7 @@ __device__ inline void solve_toi(Car& c, const WallSet& S, float dt, float frict
   c.alpha0 = 0.0f;
   for (int i = 0; i < c.nct; ++i) { c.ct[i].flags &= ~(CT_TOI | CT_ISLAND); c.ct[i].toiCount = 0; c.ct[i].toi = 1.0f; }
   bool active = true;
+  bool had_event = false;   // profile builds' rescan counters only (dead code otherwise)
   for (;;) {
     // (1) this lane's fresh TOIs of this scan: enabled, under the substep cap, no cached alpha, body awake,
     // not provably far (toi_far: alpha = 1 without computing)
@@ -1700,6 +1701,7 @@ __device__ inline void solve_toi(Car& c, const WallSet& S, float dt, float frict
         if (!(ct.flags & CT_ENABLED) || ct.toiCount > MAX_SUBSTEPS || (ct.flags & CT_TOI)) continue;
         if (toi_far(c, &pa, ldg(W + ct.wall))) {
           PCOUNT(13, 1); CCOUNT(c, 3, 1);
+          if (had_event) CCOUNT(c, 29, 1);   // profile builds: culled in a rescan after this car's event
 #ifdef NASCAR_TOI_CULL_CHECK   // check builds: every culled call run anyway; slot 11 counts culled TOUCHING outcomes
           if (toi_alpha(make_float4(c.c0.x, c.c0.y, c.c.x, c.c.y), make_float4(c.a0, c.a, c.alpha0, 0.0f),
                         ldg(W + ct.wall)) < 1.0f) PCOUNT(11, 1);
@@ -1708,6 +1710,7 @@ __device__ inline void solve_toi(Car& c, const WallSet& S, float dt, float frict
           continue;
         }
         need |= 1u << i;
+        if (had_event) CCOUNT(c, 27, 1);   // profile builds: computed in a rescan after this car's event
       }
     }
     // (2) the wave's pairs, numbered lane by lane (prefix over the lanes' counts by bit ballots)
@@ -1752,7 +1755,10 @@ __device__ inline void solve_toi(Car& c, const WallSet& S, float dt, float frict
         uint32_t nb = need; int k = off;
         while (nb) {
           const int i = __ffs(nb) - 1; nb &= nb - 1;
-          if (k >= r0 && k < r0 + TOI_JOBCAP) { c.ct[i].toi = L.res[k - r0]; c.ct[i].flags |= CT_TOI; }
+          if (k >= r0 && k < r0 + TOI_JOBCAP) {
+            c.ct[i].toi = L.res[k - r0]; c.ct[i].flags |= CT_TOI;
+            if (had_event && c.ct[i].toi < 1.0f) CCOUNT(c, 28, 1);   // profile builds: a rescan's TOUCHING result
+          }
           ++k;
         }
       }
@@ -1780,6 +1786,7 @@ __device__ inline void solve_toi(Car& c, const WallSet& S, float dt, float frict
       } else {
         ev = true;
         PCOUNT(15, 1); CCOUNT(c, 4, 1);
+        had_event = true;
         bc0 = c.c0; bc = c.c; ba0 = c.a0; ba = c.a; balpha0 = c.alpha0;
         {
           float beta = fdiv_cr(minAlpha - c.alpha0, 1.0f - c.alpha0);

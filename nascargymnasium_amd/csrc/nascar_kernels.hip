@@ -2597,14 +2597,17 @@ extern "C" const char* nascar_last_error(void) { return g_err.c_str(); }
 // fewer than 2 workgroups per CU -- a small batch (e.g. 4096 envs x 1 car: 32 workgroups) is then spread over
 // 2 x CUs workgroups with fewer envs each.  Every step kernel lasts as long as its slowest wave, and a wave's
 // time is the sum over its phases of the slowest lane's: fewer cars per wave shorten the slowest car's wait on
-// its wave-mates (the chip has room for the extra, partly empty waves).  NASCAR_EPB overrides (A/B).
+// its wave-mates (the chip has room for the extra, partly empty waves).  nascar_set_envs_per_block overrides it
+// (and, in tools builds with -DNASCAR_AB_KNOBS only, NASCAR_EPB).
 static int auto_epb(int E, int C, int device) {
   int epb = SBLOCK / C;
   int cus = 0;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus <= 0) cus = 256;
   const long target = 2L * cus;
   if ((E + epb - 1) / epb < target) epb = std::max(1, (int)((E + target - 1) / target));
+#ifdef NASCAR_AB_KNOBS   // A/B tools builds only: the product library reads no environment knob that changes a kernel path
   if (const char* ev = getenv("NASCAR_EPB")) { const int v = atoi(ev); if (v >= 1 && v <= SBLOCK / C) epb = v; }
+#endif
   return epb;
 }
 
@@ -2633,6 +2636,13 @@ extern "C" int nascar_set_beam_cell(NascarHandle* h, float meters) {
   h->beam_cell = meters;
   return 0;
 }
+extern "C" int nascar_set_sensor_block(NascarHandle* h, int32_t threads) {
+  if (!h) return fail("null argument");
+  if (threads != 0 && threads != 256 && threads != 512 && threads != 1024)
+    return fail("sensor workgroup size must be 0 (automatic: 512), 256, 512 or 1024 threads, got %d", threads);
+  h->sensor_block = threads ? threads : 512;
+  return 0;
+}
 extern "C" int nascar_set_sensor_lanes(NascarHandle* h, int32_t lanes) {
   if (!h) return fail("null argument");
   if (lanes != 0 && lanes != 4 && lanes != 16) return fail("sensor lanes per car must be 0 (automatic), 4 or 16, got %d", lanes);
@@ -2649,9 +2659,11 @@ extern "C" int nascar_create(const NascarConfig* cfg, NascarHandle** out) {
   h->cfg = *cfg;
   h->E = cfg->num_envs; h->C = cfg->num_cars; h->N = h->E * h->C;
   h->epb = auto_epb(h->E, h->C, cfg->device);
-  if (const char* ev = getenv("NASCAR_RAY_LPC")) h->ray_lanes = atoi(ev);   // A/B
-  if (const char* ev = getenv("NASCAR_FUSE_ML")) h->fuse_ml = atoi(ev) != 0;   // A/B
-  if (const char* ev = getenv("NASCAR_RBLOCK")) {   // A/B
+#ifdef NASCAR_AB_KNOBS   // A/B tools builds only (the product library: nascar_set_sensor_lanes / _fused_logic /
+                         // _sensor_block / _beam_cell)
+  if (const char* ev = getenv("NASCAR_RAY_LPC")) h->ray_lanes = atoi(ev);
+  if (const char* ev = getenv("NASCAR_FUSE_ML")) h->fuse_ml = atoi(ev) != 0;
+  if (const char* ev = getenv("NASCAR_RBLOCK")) {
     const int rb = atoi(ev);
     if (rb == 256 || rb == 512 || rb == 1024) h->sensor_block = rb;
   }
@@ -2659,6 +2671,7 @@ extern "C" int nascar_create(const NascarConfig* cfg, NascarHandle** out) {
     const float v = (float)atof(ev);
     if (v >= BEAM_CELL_MIN && v <= BEAM_CELL_MAX) h->beam_cell = v;
   }
+#endif
   size_t N = h->N, E = h->E, o = 0;
   h->off_f32 = o; o = align256(o + sizeof(float) * N_F32 * N);
   h->off_f64 = o; o = align256(o + sizeof(double) * N_F64 * N);
@@ -2749,8 +2762,12 @@ extern "C" int nascar_add_track(NascarHandle* h, const double* segments, int32_t
   }
   const HostTrack& t = tb->t;
   const size_t need = 2 * sizeof(float4) * t.walls.size() + sizeof(float4) * t.groups.size();
-  if (need > h->max_sensor_lds) {
+  if (need > h->max_sensor_lds) {   // on the handle's device (the attribute is per device), cached track or not
+    int cur = 0;
+    HIPCHK(hipGetDevice(&cur));
+    if (cur != h->cfg.device) HIPCHK(hipSetDevice(h->cfg.device));
     const int rc = sensor_lds_reserve(need);
+    if (cur != h->cfg.device) hipSetDevice(cur);
     if (rc < 0) return rc;
   }
   h->max_sensor_lds = std::max(h->max_sensor_lds, need);
@@ -2986,7 +3003,9 @@ static int prepare(NascarHandle* h, hipStream_t stream) {
     if (blk_env[s] != ((int)s < h->E ? (int)s : -1)) { h->map_identity = 0; break; }
   h->one_track = blk_track.empty() ? -1 : blk_track[0];
   for (int tr : blk_track) if (tr != h->one_track) { h->one_track = -1; break; }
-  if (getenv("NASCAR_NO_MAP_SHORTCUT")) { h->map_identity = 0; h->one_track = -1; }   // A/B and tests
+#ifdef NASCAR_AB_KNOBS
+  if (getenv("NASCAR_NO_MAP_SHORTCUT")) { h->map_identity = 0; h->one_track = -1; }   // A/B tools builds only
+#endif
   h->dirty_tracks = false;
   return 0;
 }
@@ -3012,11 +3031,16 @@ static Params make_params(NascarHandle* h) {
 
 // passes: 1 = pass A only (pose[n] with its A-mode bits: nascar_reset), 3 = pass A then pass B (the reset
 // poses pose[N + n] of auto-reset cars overwrite those cars' pass-A obs values: nascar_step)
-// NASCAR_SENSOR=groups selects the wall-group sensor kernel (A/B and cross-checks); default: beam lists
+// the beam-list sensor kernel; tools builds with -DNASCAR_AB_KNOBS: NASCAR_SENSOR=groups selects the wall-group kernel
+// for the step (the tests cross-check the two through nascar_debug_sensors)
 static int sensor_impl() {
+#ifdef NASCAR_AB_KNOBS
   static int m = -1;
   if (m < 0) { const char* e = getenv("NASCAR_SENSOR"); m = (e && !strcmp(e, "groups")) ? 0 : 1; }
   return m;
+#else
+  return 1;
+#endif
 }
 // Lanes per car of the beam-list sensor kernel: one ray per lane (16 lanes per car) by default, so each car's four
 // sequential walks (4 lanes per car: rays r, r + 4, r + 8, r + 12 per lane) become one and the kernel's slowest lane
@@ -3107,6 +3131,10 @@ static int launch_step_range(NascarHandle* h, const Params& P, int nb, const voi
                              hipStream_t s, int phases = PH_ALL) {
   const bool timed = h->step_ev[0] && nb == h->nblocks;   // nascar_set_step_events: whole-grid steps only
   if (h->fuse_ml) {   // model + logic in one launch (model_logic_kernel); the logic phase is part of PH_MODEL
+    // Contract: under the fused kernel the logic phase IS part of PH_MODEL's launch, so a PH_LOGIC-only request
+    // enqueues nothing -- correct only for callers that request PH_MODEL for the same step and range first, as the
+    // sharded rollout's phase-major loop does (1 << ph for ph = 0, 1, 2); nascar_step / nascar_step_driven pass
+    // PH_ALL.  A logic-only launch (the two-kernel build's logic_kernel alone) needs nascar_set_fused_logic(h, 0).
     if (phases & PH_MODEL) {
       if (timed) HIPCHK(hipEventRecord(h->step_ev[0], s));
       hipLaunchKernelGGL(model_logic_kernel, dim3(nb), dim3(SBLOCK), MODEL_LOGIC_LDS_BYTES, s, P, actions, discrete,
@@ -3449,7 +3477,11 @@ extern "C" int nascar_set_actor_precision(NascarHandle* h, int32_t fp32) {
 }
 
 static void launch_actor(NascarHandle* h, int n, const float* obs, float* actions, void* stream) {
-  static const int fp32_valu = getenv("NASCAR_ACTOR_FP32_VALU") != nullptr;   // A/B: the f32 VALU kernel
+#ifdef NASCAR_AB_KNOBS
+  static const int fp32_valu = getenv("NASCAR_ACTOR_FP32_VALU") != nullptr;   // A/B tools builds: the f32 VALU kernel
+#else
+  const int fp32_valu = 0;
+#endif
   if (h->actor_fp32 && !fp32_valu) {   // reference precision on the f32 MFMA: one wave per 32 observations
     const int tiles = (n + 31) / 32;
     hipLaunchKernelGGL(actor_mfma32_kernel, dim3((tiles + AM_WAVES - 1) / AM_WAVES), dim3(64 * AM_WAVES), 0,

@@ -21,16 +21,18 @@ def mix32(x):
     return (x >> np.uint64(32)).astype(np.uint32)
 
 
-def hash_keys(N, seed, step):
-    n = np.arange(N, dtype=np.uint64)
+def hash_keys(N, seed, step, ids=None):
+    """per-car counter keys; `ids` (optional, length N): the cars' global indices in the device engine (car n of env e
+    is e * C + n there), so a host shard of a few envs draws the same numbers as those cars on the device"""
+    n = np.arange(N, dtype=np.uint64) if ids is None else np.asarray(ids, dtype=np.uint64)
     with np.errstate(over="ignore"):
         s = np.uint64((seed * 0x100000001B3) & M64)
         k = np.uint64((step * 0x9E3779B1) & M64)
         return s ^ (n << np.uint64(24)) ^ k
 
 
-def uniform_actions(N, seed, step):
-    key = hash_keys(N, seed, step)
+def uniform_actions(N, seed, step, ids=None):
+    key = hash_keys(N, seed, step, ids)
     with np.errstate(over="ignore"):
         u0 = (mix32(key) >> np.uint32(8)).astype(np.float32) * np.float32(2.0 / 16777216.0) - np.float32(1.0)
         u1 = (mix32(key ^ np.uint64(0xABCDEF12345)) >> np.uint32(8)).astype(np.float32) * np.float32(2.0 / 16777216.0) \
@@ -68,18 +70,23 @@ class RuleDriver:
         return np.stack([tb.astype(np.float32), steer], 1)
 
 
-def noisy_mask(N, seed, step):
-    key = hash_keys(N, seed, step)
+def noisy_mask(N, seed, step, ids=None):
+    key = hash_keys(N, seed, step, ids)
     return (mix32(key ^ np.uint64(0x5DEECE66D)) >> np.uint32(16)) < NOISE_P16
 
 
 class NoisyRuleDriver(RuleDriver):
-    def __init__(self, N, seed=0):
+    """ids: the cars' global indices on the device (default 0..N-1), which key the noise hash"""
+
+    def __init__(self, N, seed=0, ids=None):
         super().__init__(N)
         self.N, self.seed = N, seed
+        self.ids = None if ids is None else np.asarray(ids, dtype=np.uint64)
+        if self.ids is not None and self.ids.shape != (N,):
+            raise ValueError(f"ids must hold {N} car indices")
 
     def actions(self, obs, step):
         a = self(obs)
-        m = noisy_mask(self.N, self.seed, step)
-        a[m] = uniform_actions(self.N, self.seed, step)[m]
+        m = noisy_mask(self.N, self.seed, step, self.ids)
+        a[m] = uniform_actions(self.N, self.seed, step, self.ids)[m]
         return a

@@ -1,5 +1,6 @@
 """Host logic of bench.py and the host restatement of the device action sources (no GPU)."""
 import numpy as np
+import pytest
 
 import bench
 from drivers import M64, mix32, noisy_mask, uniform_actions, RuleDriver
@@ -64,21 +65,47 @@ def _bench(args, env=None, timeout=240):
                           capture_output=True, text=True, timeout=timeout)
 
 
-def test_gpus_n_launches_n_ranks():
-    """`bench.py --gpus 2` outside torchrun starts 2 ranks itself (torch.distributed.run child, gloo in --plumbing);
-    rank 0's line has n_gpus = world = 2, the MAX over the ranks' timings, and the whole-job value from it."""
+@pytest.mark.parametrize("gather", [False, True])
+def test_gpus_n_runs_main_on_n_ranks(gather):
+    """`bench.py --gpus 2 --plumbing` outside torchrun starts 2 ranks itself (torch.distributed.run child) and runs
+    bench.main() unchanged on the CPU stand-in engine (PlumbingEngine) over gloo: the settle, the warm-up, the
+    barrier-bracketed timed window, the statistics and kernel passes, the per-step pass, the secondary pass and every
+    collective main() issues (gather_all, the reduce_max / reduce_sum calls, the barriers), with and without the
+    --gather path (ObsGather of the rollout's trajectory records to rank 0).  Rank 0's line has n_gpus = world = 2,
+    the MAX over the ranks' timings, the whole-job value from it, and both ranks issued the same collectives in the
+    same order."""
     import json
     K, E, C = 6, 16, 10
-    r = _bench(["--gpus", "2", "--plumbing", "--steps", str(K), "--warmup", "0", "--envs", str(E), "--cars", str(C)])
+    args = ["--gpus", "2", "--plumbing", "--steps", str(K), "--warmup", "2", "--envs", str(E), "--cars", str(C),
+            "--settle", "12"] + (["--gather"] if gather else [])
+    r = _bench(args)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1, r.stdout          # rank 0 only
     d = json.loads(lines[0])
+    assert d["metric"].startswith("plumbing")
     assert d["n_gpus"] == 2 and d["ranks"]["world_size"] == 2 and d["ranks"]["backend"] == "gloo"
     el = d["ranks"]["elapsed_s"]
     assert len(el) == 2 and max(el) >= K * 2e-3          # rank 1 sleeps 2 ms per step
     assert np.isclose(d["ms_per_step"], max(el) / K * 1e3)
     assert np.isclose(d["value"], 2 * E * C * K / max(el))
+    col = d["collectives"]
+    assert col["ranks"] == 2 and col["all_ranks_equal"], col
+    seq = col["rank0"]
+    # timed window (2 barriers) + per-step window (2 barriers), the per-rank gather, the reductions of main()
+    assert seq[:4] == ["barrier"] * 4
+    assert seq[4:9] == ["all_gather[1]", "all_reduce_max[2]", "all_reduce_max[2]", "all_reduce_max[1]",
+                        "all_reduce_sum[7]"], seq
+    if gather:
+        assert len(seq) == 9 and "uniform_from_reset" not in d
+        assert "RCCL gather" in d["config"]["parallelism"]
+    else:   # the secondary pass: its own barrier-bracketed window and MAX
+        assert seq[9:] == ["barrier", "barrier", "all_reduce_max[1]"], seq
+        assert d["uniform_from_reset"]["ms_per_step"] >= 2.0
+    assert set(d["roofline"]["kernel_times_ms"]) == {"model_logic_kernel", "ray_sensor_kernel"}
+    assert d["per_step"]["ms_per_step"] >= 2.0
+    ws = d["workload_stats"]
+    assert ws["window_car_steps"] > 0 and 0 < ws["contact_frac"] < 1
 
 
 def test_world_size_mismatch_is_an_error():
@@ -88,6 +115,34 @@ def test_world_size_mismatch_is_an_error():
     assert r.returncode == 2 and "WORLD_SIZE=2" in r.stderr
 
 
-def test_host_cores_reports_the_cpu():
+def test_host_cores_reports_the_cpu(monkeypatch):
     n, txt = bench.host_cores()
     assert n >= 1 and "affinity" in txt and f"{n} threads used" in txt
+    # an OMP_NUM_THREADS set for another reason binds the thread count: the description says so, and
+    # NASCAR_CPU_SHARE overrides it
+    monkeypatch.setenv("OMP_NUM_THREADS", "1")
+    monkeypatch.delenv("NASCAR_CPU_SHARE", raising=False)
+    n1, txt1 = bench.host_cores()
+    aff = len(__import__("os").sched_getaffinity(0))
+    assert n1 == 1 and ("binding limit" in txt1) == (aff > 1)
+    monkeypatch.setenv("NASCAR_CPU_SHARE", "2")
+    n2, txt2 = bench.host_cores()
+    assert n2 == min(2, aff) and "NASCAR_CPU_SHARE=2" in txt2
+
+
+def test_host_driver_global_ids_match_the_device_keys():
+    """the host driver of a few picked envs, keyed by the cars' global ids, draws the same noise as those cars in
+    the full batch (the device's key uses the global car index n = e * C + c)"""
+    from drivers import NoisyRuleDriver
+    E, C, step = 300, 10, 12345
+    full = uniform_actions(E * C, 5, step)
+    fm = noisy_mask(E * C, 5, step)
+    pick = [3, 77, 299]
+    ids = [e * C + c for e in pick for c in range(C)]
+    assert np.array_equal(uniform_actions(len(ids), 5, step, ids), full[ids])
+    assert np.array_equal(noisy_mask(len(ids), 5, step, ids), fm[ids])
+    d = NoisyRuleDriver(len(ids), 5, ids=ids)
+    obs = np.zeros((len(ids), 38), np.float32)
+    obs[:, 22] = 1.0
+    a = d.actions(obs, step)
+    assert np.array_equal(a[fm[ids]], full[ids][fm[ids]])

@@ -136,15 +136,27 @@ def test_cfg3_car_contact_at_talladega_10_cars():
         x.close()
 
 
+@pytest.mark.timeout(600)
 def test_bench_steady_state_full_size_vs_oracle():
-    """The bench's own workload at its full size and layout: daytona 8192 x 10 at 12 envs per workgroup, settled by
-    bench.settle (10 800 noisy-driver steps, env ages staggered over the episode), then 64 of its envs (spread over the
-    batch) are loaded into the CPU oracle (oracle_lib.inject_gpu_state) and the whole batch and the oracle continue
-    150 steps through the sharded rollout's kernels one step at a time (nascar_step_driven): the 64 envs' obs,
-    rewards, disabled / collision flags and terminations equal the oracle's every step."""
+    """The bench's own workload at its full size, layout and schedule: daytona 8192 x 10 at 12 envs per workgroup,
+    settled once by bench.settle (10 800 noisy-driver steps, env ages staggered over the episode).  Three engines then
+    hold that state and run the same 150 steps:
+      A -- one whole-batch launch per step through nascar_step_driven (the noisy driver inside the step kernel, the
+           bench's per-step path); 64 of its envs (spread over the batch) are loaded into the CPU oracle
+           (oracle_lib.inject_gpu_state, driver state included) and stepped by the host driver keyed by the device's
+           global car ids: the 64 envs' obs, rewards, disabled / collision flags, done flags and termination reasons
+           equal the oracle's every step;
+      B -- the schedule bench.py TIMES (nascar_rollout on the default 4 shards / 4 streams, each shard's
+           launches offset by its workgroups) in one 150-step call recording every step (trajectory + obs trajectory);
+      C -- the same schedule exactly as bench.py's timed loop issues it (bench.Stepper: 3 calls of 50 steps, no
+           records).
+    Every step's observation, reward, car flags and env flags of all 81 920 cars of A equal B's records, and A, B and
+    C end with byte-identical state arenas and observations.  The reference steps these cars one by one in Python
+    (src/car_env.py:567-570, 678-803); the shards, streams and workgroup offsets must not change any result."""
     import sys
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     import bench
+    from drivers import NoisyRuleDriver
     from nascargymnasium_amd.batched import BatchedCarEnv
     from oracle_lib import OracleEnv, inject_gpu_state
     E, C, K, seed = 8192, 10, 150, 0
@@ -152,29 +164,51 @@ def test_bench_steady_state_full_size_vs_oracle():
     env = BatchedCarEnv(E, C, path, device="cuda:0")
     assert env.envs_per_block == 12 and env.fused_logic
     env.reset()
-    st = bench.Stepper(env, "noisy", seed, None, None, 0)
-    bench.settle(env, st, bench.EPISODE_STEPS, True, env.device)
-    blob = env.get_state().cpu().numpy()
-    gobs = env.obs.cpu().numpy().reshape(E, C, 38).copy()
+    bench.settle(env, bench.Stepper(env, "noisy", seed, None, None, 0), bench.EPISODE_STEPS, True, env.device)
+    state0, obs0 = env.get_state(), env.obs.clone()
+    k0 = bench.EPISODE_STEPS
+    twins = []
+    for _ in range(2):
+        t = BatchedCarEnv(E, C, path, device="cuda:0")
+        assert t.envs_per_block == 12 and t.fused_logic and t.rollout_streams == 4, (t.envs_per_block, t.rollout_streams)
+        t.set_state(state0)
+        t.obs.copy_(obs0)
+        twins.append(t)
+    ot, rt, cft, eft = twins[0].rollout(3, K, seed=seed, step0=k0, auto_reset=True, trajectory=True,
+                                         obs_trajectory=True)
+    stc = bench.Stepper(twins[1], "noisy", seed, None, None, 50)
+    assert stc.R == 50
+    stc.run(k0, K)
+    assert torch.equal(ot[0], obs0)
+    # A and the oracle
+    blob = state0.cpu().numpy()
+    gobs = obs0.cpu().numpy().reshape(E, C, 38)
     pick = [int(x) for x in np.linspace(0, E - 1, 64)]
     orc = OracleEnv(path, len(pick), C)
-    inject_gpu_state(orc, blob, E, C, pick)
-    # the device driver's noise hash uses each car's global index, so the oracle is fed the device's actions for the
-    # picked cars (the device driver equals the host restatement: tests/closed_loop.py)
+    rows = inject_gpu_state(orc, blob, E, C, pick)
+    drv = NoisyRuleDriver(len(pick) * C, seed, ids=[e * C + c for e in pick for c in range(C)])
+    drv.tb = rows[:, 0].copy()
+    drv.steer, drv.last, drv.lim = (rows[:, j].astype(np.float32) for j in (1, 2, 3))
     pk = torch.tensor(pick, device=env.device)
-    oo = gobs[pick]
-    k0 = bench.EPISODE_STEPS
-    contact = 0
-    for k in range(k0, k0 + K):
-        a = env.policy_actions(3, seed=seed, step=k).clone()
-        env.launch_step(a, auto_reset=True)
-        ha = a.view(E, C, 2)[pk].cpu().numpy()
-        oo, orw, ocf, oef = orc.step(ha)
+    oo = np.ascontiguousarray(gobs[pick])
+    contact = resets = 0
+    for i, k in enumerate(range(k0, k0 + K)):
+        ha = drv.actions(oo, k)
+        env.step_driven(3, seed=seed, step=k, auto_reset=True)
+        # the whole batch: per-step path == the timed schedule's records of this step
+        assert torch.equal(env.obs, ot[i + 1]), f"step {k}: per-step obs != sharded rollout's record " \
+            f"{torch.nonzero(env.obs != ot[i + 1])[:5].tolist()}"
+        assert torch.equal(env.reward, rt[i]), f"step {k}: reward != sharded rollout's"
+        assert torch.equal(env.car_flags, cft[i]), f"step {k}: car flags != sharded rollout's"
+        assert torch.equal(env.env_flags, eft[i]), f"step {k}: env flags != sharded rollout's"
+        # the 64 envs: per-step path == oracle
+        oo, orw, ocf, oef = orc.step(ha.reshape(len(pick), C, 2))
         done = (oef[:, 0] != 0) | (oef[:, 1] != 0)
         if done.any():
             for e in np.nonzero(done)[0]:
                 orc.reset(int(e))
             oo = orc.outputs()[0]
+            resets += int(done.sum())
         gr = env.reward.view(E, C)[pk].cpu().numpy()
         gcf = env.car_flags.view(E, C)[pk].cpu().numpy()
         gef = env.env_flags[pk].cpu().numpy()
@@ -182,8 +216,16 @@ def test_bench_steady_state_full_size_vs_oracle():
         assert np.array_equal(gr, orw), f"step {k}: reward mismatch at {np.argwhere(gr != orw)[:5].tolist()}"
         assert np.array_equal(gcf & 5, ocf & 5), f"step {k}: disabled / collision flags"
         assert np.array_equal((gef & 3) != 0, done), f"step {k}: done flags"
+        assert np.array_equal(((gef >> 4) & 7)[done], oef[done, 2]), f"step {k}: termination reasons"
         bad = np.argwhere(go != oo)
         assert len(bad) == 0, f"step {k}: obs mismatch at {bad[:5].tolist()}"
         contact += int(((gcf & 4) != 0).sum())
-    orc.close(); env.close()
+    sa = env.get_state()
+    for name, t in (("rollout, one 150-step call with records", twins[0]), ("rollout, bench.Stepper's 3 x 50", twins[1])):
+        assert torch.equal(t.get_state(), sa), f"final state arena differs: {name}"
+        assert torch.equal(t.obs, env.obs), f"final obs differ: {name}"
+    assert int(((eft & 8) != 0).sum()) > 0, "no auto-reset inside the window"
+    orc.close()
+    for x in [env] + twins:
+        x.close()
     assert contact > 0

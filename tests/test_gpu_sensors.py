@@ -197,9 +197,9 @@ def test_track_with_many_walls(tmp_path):
         assert np.array_equal(o.view(np.uint32), ro.view(np.uint32))
 
 
-def test_sensor_workgroup_sizes_identical(monkeypatch):
-    """ray_sensor_kernel at 16 lanes per car in 256-, 512- (the default) and 1024-thread workgroups (NASCAR_RBLOCK,
-    read at nascar_create) and at 4 lanes per car: the same sensor values on every pose, bit for bit."""
+def test_sensor_workgroup_sizes_identical():
+    """ray_sensor_kernel at 16 lanes per car in 256-, 512- (the default) and 1024-thread workgroups
+    (nascar_set_sensor_block) and at 4 lanes per car: the same sensor values on every pose, bit for bit."""
     from nascargymnasium_amd.batched import BatchedCarEnv
     from nascargymnasium_amd.track import build_walls, load_track
     path = os.path.join(TRACKS, "martinsville.track")
@@ -207,8 +207,8 @@ def test_sensor_workgroup_sizes_identical(monkeypatch):
     poses = _poses(rng, build_walls(load_track(path)), 480 * 10)
     out = {}
     for rb in ("256", "512", "1024"):
-        monkeypatch.setenv("NASCAR_RBLOCK", rb)
         env = BatchedCarEnv(480, 10, path, device="cuda:0", envs_per_block=12)   # 120 cars per step workgroup
+        env.set_sensor_block(int(rb))
         out[rb] = _device_sensors(env, poses, 1)
         if rb == "512":
             env.set_sensor_lanes(4)

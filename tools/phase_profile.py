@@ -64,7 +64,7 @@ def main():
     a = ap.parse_args()
     so = os.path.join(ROOT, "tools", a.lib)
     if not a.no_build:
-        subprocess.run(["hipcc"] + _lib.HIPCC_FLAGS + ["-DNASCAR_PROFILE"] + (["-DNASCAR_PROFILE_UP"] if a.up else [])
+        subprocess.run(["hipcc"] + _lib.HIPCC_FLAGS + ["-DNASCAR_PROFILE", "-DNASCAR_AB_KNOBS"] + (["-DNASCAR_PROFILE_UP"] if a.up else [])
                        + (["-DNASCAR_PROFILE_COUNT"] if a.count else []) + ["-D" + d for d in a.define]
                        + ["-o", so, os.path.join(_lib.CSRC, "nascar_kernels.hip")], check=True)
     _lib.LIB_PATH = so
@@ -152,6 +152,9 @@ def main():
                     print(f"    car {i}: events {cp[i, 4]}, island solve {cp[i, 11]}, event contact updates {cp[i, 12]}, "
                           f"TOI calls computed by this lane {cp[i, 2]}: outer iters {cp[i, 6]}, root iters {cp[i, 7]}, "
                           f"GJK cycles {cp[i, 9]}, separation-fn cycles {cp[i, 10]}")
+            print(f"  rescans after a car's TOI event: TOIs computed {cp[:, 27].sum()} (TOUCHING {cp[:, 28].sum()}), "
+                  f"culled {cp[:, 29].sum()}; slowest wave's cars: computed {cp[w0:w1, 27].sum()} "
+                  f"(TOUCHING {cp[w0:w1, 28].sum()}), culled {cp[w0:w1, 29].sum()}")
             tc = cp[:, 2].sum()
             if tc:
                 print(f"  all TOI calls {tc}: outer iters/call {cp[:, 6].sum() / tc:.2f}, root iters/call {cp[:, 7].sum() / tc:.2f}, "
