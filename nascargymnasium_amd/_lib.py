@@ -27,8 +27,11 @@ TRAJ_RECORDS, TRAJ_OBS = 1, 2          # nascar_rollout traj flags (include/nasc
 REASONS = {0: None, 1: "all_cars_disabled", 2: "all_active_cars_low_reward (threshold: -250.0)",
            3: "time_limit", 4: "truncated"}
 
-HIPCC_FLAGS = ["--offload-arch=gfx950", "-O3", "-ffp-contract=off", "-fno-fast-math", "-fPIC", "-shared",
-               "-std=c++17", "-Wno-unused-value", "-Wno-unused-result"]
+# -fno-slp-vectorize: the one-lane-per-car code is long dependent scalar chains (Box2D's solver / GJK / TOI per car), and
+# the SLP vectorizer packs pairs of its f32 operations into v_pk_* instructions plus the v_mov shuffles that feed them,
+# lengthening the chains a lone wave waits on (driver's command, 3 A/B rounds: 144.0 -> 139.2 us per step; round 5)
+HIPCC_FLAGS = ["--offload-arch=gfx950", "-O3", "-ffp-contract=off", "-fno-fast-math", "-fno-slp-vectorize", "-fPIC",
+               "-shared", "-std=c++17", "-Wno-unused-value", "-Wno-unused-result"]
 
 
 class NascarConfig(ctypes.Structure):

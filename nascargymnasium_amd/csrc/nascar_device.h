@@ -30,6 +30,11 @@ __device__ unsigned long long* g_prof = nullptr;
     if (g_prof && (threadIdx.x & 63) == 0) g_prof[((size_t)blockIdx.x * (BLOCK / 64) + threadIdx.x / 64) * 16 + (ph)] = _t; } while (0)
 #define PROFS(ph) do { unsigned long long _t = __builtin_amdgcn_s_memtime(); \
     if (g_prof && (threadIdx.x & 63) == 0) g_prof[(65536 + (size_t)blockIdx.x * (BLOCK / 64) + threadIdx.x / 64) * 16 + (ph)] = _t; } while (0)
+// ray_sensor_kernel stamps (any block size): rows of the sensor region by blockIdx.x * waves per block + wave
+#define PROFR(ph) do { unsigned long long _t = __builtin_amdgcn_s_memtime(); \
+    if (g_prof && (threadIdx.x & 63) == 0) g_prof[(65536 + (size_t)blockIdx.x * (blockDim.x >> 6) + threadIdx.x / 64) * 16 + (ph)] = _t; } while (0)
+#define PROFR_RT(ph) do { unsigned long long _t = __builtin_amdgcn_s_memrealtime(); \
+    if (g_prof && (threadIdx.x & 63) == 0) g_prof[(65536 + (size_t)blockIdx.x * (blockDim.x >> 6) + threadIdx.x / 64) * 16 + (ph)] = _t; } while (0)
 #define PROFS_RT(ph) do { unsigned long long _t = __builtin_amdgcn_s_memrealtime(); \
     if (g_prof && (threadIdx.x & 63) == 0) g_prof[(65536 + (size_t)blockIdx.x * (BLOCK / 64) + threadIdx.x / 64) * 16 + (ph)] = _t; } while (0)
 // event counters: same-address global atomics from every lane serialise (milliseconds per launch), so
@@ -71,6 +76,10 @@ __device__ unsigned long long* g_prof = nullptr;
 #define RPROF_ADD(slot, v) do { if (g_prof && (threadIdx.x & 63) == 0) \
     g_prof[RPROF_BASE + ((size_t)blockIdx.x * (SBLOCK / 64) + threadIdx.x / 64) * 4 + (slot)] += (v); } while (0)
 #define CTIME_END(c, slot) CCOUNT(c, slot, __builtin_amdgcn_s_memtime() - _ct0)
+// -DNASCAR_TOI_CAPTURE (with NASCAR_PROFILE): the inputs of every computed b2TimeOfImpact job (the car's sweep as two
+// float4 and the wall record), for tools/toi_bench.py; a counter word, then TCAP_MAX records of 8 words
+#define TCAP_BASE (RPROF_BASE + (size_t)65536 * 5)
+#define TCAP_MAX 16384
 #else
 #define CCOUNT(c, slot, v) do { } while (0)
 #define CTIME_BEGIN() do { } while (0)
@@ -78,6 +87,8 @@ __device__ unsigned long long* g_prof = nullptr;
 #define CTIME_END(c, slot) do { } while (0)
 #define PROF(ph) do { } while (0)
 #define PROFS(ph) do { } while (0)
+#define PROFR(ph) do { } while (0)
+#define PROFR_RT(ph) do { } while (0)
 #define PROFS_RT(ph) do { } while (0)
 #define PROFB(ph) do { } while (0)
 #define PROFU(ph) do { } while (0)
@@ -1243,12 +1254,32 @@ __device__ inline void solve(Car& c, const WallSet& S, float dt, float dtRatio, 
 // arrays: those lived in scratch memory).  Same operations in the same order as b2Simplex::ReadCache /
 // Solve2 / Solve3 / GetSearchDirection / GetWitnessPoints / WriteCache.
 struct SV { V2 wA, wB, w; float a; int iA, iB; };
-struct SCache { float metric; int count; int iA0, iA1, iA2, iB0, iB1, iB2; };
+struct SCache { float metric; int count; int iA0, iA1, iA2, iB0, iB1, iB2;
+#ifdef NASCAR_PROFILE
+  int iters = 0;   // profile builds: GJK iterations summed over the calls that used this cache
+#endif
+};
 
+#ifndef SUPPORT_BOX
+#define SUPPORT_BOX 1
+#endif
+// b2PolygonShape / b2DistanceProxy::GetSupport: the first vertex of maximal dot product with d.  For a box the four
+// dot products (+-hx) dx + (+-hy) dy share the two products a = hx dx, b = hy dy ((-hx) dx is -(hx dx) exactly in
+// IEEE arithmetic), so they are (-a) + (-b), a + (-b), a + b, (-a) + b -- the same values, 2 products instead of 8.
 __device__ __forceinline__ int support(const Poly* p, V2 d) {
+#if SUPPORT_BOX
+  const float a = p->hx * d.x, b = p->hy * d.y;
+  const float v1 = a + (-b), v2 = a + b, v3 = (-a) + b;
+  int best = 0; float bestValue = (-a) + (-b);
+  if (v1 > bestValue) { best = 1; bestValue = v1; }
+  if (v2 > bestValue) { best = 2; bestValue = v2; }
+  if (v3 > bestValue) { best = 3; }
+  return best;
+#else
   int best = 0; float bestValue = vdot(pv(p, 0), d);
   for (int i = 1; i < 4; ++i) { float value = vdot(pv(p, i), d); if (value > bestValue) { best = i; bestValue = value; } }
   return best;
+#endif
 }
 __device__ __forceinline__ float simplex_metric(int count, const SV& v0, const SV& v1, const SV& v2) {
   if (count == 1) return 0.0f;
@@ -1261,6 +1292,120 @@ __device__ __forceinline__ void sv_set(SV& v, int ia, int ib, const Poly* pA, Xf
   v.wA = xmul(tA, pv(pA, ia)); v.wB = xmul(tB, pv(pB, ib));
   v.w = vsub(v.wB, v.wA); v.a = 0.0f;
 }
+#ifndef GJK_V2
+#define GJK_V2 1
+#endif
+#if GJK_V2
+// b2Distance (b2GJK) for two boxes, restated for a short dependent chain: the simplex is held as its vertices' w
+// (= wB - wA), packed index pairs (iA | iB << 2) and barycentric weights only -- the support points wA / wB are
+// recomputed from their indices where b2Simplex::GetWitnessPoints needs them (b2Transform * vertex again: the same
+// operations on the same values) -- and Solve2 / Solve3's case analysis is evaluated as selects with one division
+// (the chosen case's denominator), so a step moves 5 registers per vertex instead of 9 and takes no branch per case.
+// Same cases in the same priority order, same arithmetic per case: identical results (tools/toi_bench.py compares the
+// alphas of the captured steady-state TOI jobs bit for bit; the GPU parity suite covers the rest).
+__device__ __forceinline__ V2 gjk_w(int ip, const Poly* pA, Xf tA, const Poly* pB, Xf tB) {
+  return vsub(xmul(tB, pv(pB, ip >> 2)), xmul(tA, pv(pA, ip & 3)));
+}
+__device__ inline float gjk_distance(SCache& cache, const Poly* pA, Xf tA, const Poly* pB, Xf tB) {
+  V2 w0 = zero2(), w1 = zero2(), w2 = zero2();
+  int i0 = 0, i1 = 0, i2 = 0;
+  float a0 = 0.0f, a1 = 0.0f, a2 = 0.0f;
+  int count = cache.count;
+  if (count > 0) { i0 = cache.iA0 | (cache.iB0 << 2); w0 = gjk_w(i0, pA, tA, pB, tB); }
+  if (count > 1) { i1 = cache.iA1 | (cache.iB1 << 2); w1 = gjk_w(i1, pA, tA, pB, tB); }
+  if (count > 2) { i2 = cache.iA2 | (cache.iB2 << 2); w2 = gjk_w(i2, pA, tA, pB, tB); }
+  if (count > 1) {   // b2Simplex::ReadCache: flush a cache whose metric changed a lot
+    const float metric1 = cache.metric;
+    const float metric2 = count == 2 ? vlen(vsub(w0, w1)) : (count == 3 ? vcross(vsub(w1, w0), vsub(w2, w0)) : 0.0f);
+    if (metric2 < 0.5f * metric1 || 2.0f * metric1 < metric2 || metric2 < FLT_EPS) count = 0;
+  }
+  if (count == 0) { i0 = 0; w0 = gjk_w(0, pA, tA, pB, tB); a0 = 1.0f; count = 1; }
+  int iter = 0;
+  while (iter < 20) {
+    const int saveCount = count, s0 = i0, s1 = i1, s2 = i2;
+    if (count == 2) {   // b2Simplex::Solve2
+      const V2 e12 = vsub(w1, w0);
+      const float d12_2 = -vdot(w0, e12), d12_1 = vdot(w1, e12);
+      const bool c1 = d12_2 <= 0.0f, c2 = !c1 && d12_1 <= 0.0f, c3 = !c1 && !c2;
+      const float inv = fdiv_cr(1.0f, c3 ? d12_1 + d12_2 : 1.0f);
+      if (c2) { w0 = w1; i0 = i1; }
+      a0 = c3 ? d12_1 * inv : 1.0f;
+      a1 = c3 ? d12_2 * inv : (c2 ? 1.0f : a1);
+      count = c3 ? 2 : 1;
+    } else if (count == 3) {   // b2Simplex::Solve3
+      const V2 e12 = vsub(w1, w0);
+      const float d12_1 = vdot(w1, e12), d12_2 = -vdot(w0, e12);
+      const V2 e13 = vsub(w2, w0);
+      const float d13_1 = vdot(w2, e13), d13_2 = -vdot(w0, e13);
+      const V2 e23 = vsub(w2, w1);
+      const float d23_1 = vdot(w2, e23), d23_2 = -vdot(w1, e23);
+      const float n123 = vcross(e12, e13);
+      const float d123_1 = n123 * vcross(w1, w2), d123_2 = n123 * vcross(w2, w0), d123_3 = n123 * vcross(w0, w1);
+      const bool cA = d12_2 <= 0.0f && d13_2 <= 0.0f;
+      const bool cB = !cA && d12_1 > 0.0f && d12_2 > 0.0f && d123_3 <= 0.0f;
+      const bool cC = !cA && !cB && d13_1 > 0.0f && d13_2 > 0.0f && d123_2 <= 0.0f;
+      const bool cD = !cA && !cB && !cC && d12_1 <= 0.0f && d23_2 <= 0.0f;
+      const bool cE = !cA && !cB && !cC && !cD && d13_1 <= 0.0f && d23_1 <= 0.0f;
+      const bool cF = !cA && !cB && !cC && !cD && !cE && d23_1 > 0.0f && d23_2 > 0.0f && d123_1 <= 0.0f;
+      const bool cG = !cA && !cB && !cC && !cD && !cE && !cF;
+      const float den = cB ? d12_1 + d12_2 : cC ? d13_1 + d13_2 : cF ? d23_1 + d23_2 : cG ? d123_1 + d123_2 + d123_3 : 1.0f;
+      const float inv = fdiv_cr(1.0f, den);
+      // new vertex 0: old 0 (A, B, C, G), old 1 (D), old 2 (E, F); new vertex 1: old 2 (C), else old 1
+      const V2 n0 = cD ? w1 : (cE || cF) ? w2 : w0;
+      const int j0 = cD ? i1 : (cE || cF) ? i2 : i0;
+      const float b0 = cB ? d12_1 * inv : cC ? d13_1 * inv : cF ? d23_2 * inv : cG ? d123_1 * inv : 1.0f;
+      const float b1 = cB ? d12_2 * inv : cC ? d13_2 * inv : cF ? d23_1 * inv : cG ? d123_2 * inv : cD ? 1.0f : a1;
+      if (cC) { w1 = w2; i1 = i2; }
+      w0 = n0; i0 = j0; a0 = b0; a1 = b1;
+      if (cG) a2 = d123_3 * inv;
+      else if (cE) a2 = 1.0f;
+      else if (cC) a2 = d13_2 * inv;
+      else if (cF) a2 = d23_2 * inv;
+      count = cG ? 3 : (cB || cC || cF) ? 2 : 1;
+    }
+    if (count == 3) break;
+    V2 d;
+    if (count == 1) d = vneg(w0);
+    else {
+      const V2 e12 = vsub(w1, w0);
+      const float sgn = vcross(e12, vneg(w0));
+      d = sgn > 0.0f ? vcross_sv(1.0f, e12) : vcross_vs(e12, 1.0f);
+    }
+    if (vdot(d, d) < FLT_EPS * FLT_EPS) break;
+    const int ia = support(pA, rmulT(tA.q, vneg(d)));
+    const int ib = support(pB, rmulT(tB.q, d));
+    const int ix = ia | (ib << 2);
+    const V2 wx = vsub(xmul(tB, pv(pB, ib)), xmul(tA, pv(pA, ia)));
+    ++iter;
+#ifdef NASCAR_PROFILE
+    ++cache.iters;
+#endif
+    const bool dup = ix == s0 || (saveCount > 1 && ix == s1) || (saveCount > 2 && ix == s2);
+    if (dup) break;
+    if (count == 1) { w1 = wx; i1 = ix; a1 = 0.0f; } else { w2 = wx; i2 = ix; a2 = 0.0f; }
+    ++count;
+  }
+  // b2Simplex::GetWitnessPoints, the support points recomputed from their indices
+  V2 wa = zero2(), wb = zero2();
+  const V2 wA0 = xmul(tA, pv(pA, i0 & 3)), wB0 = xmul(tB, pv(pB, i0 >> 2));
+  if (count == 1) { wa = wA0; wb = wB0; }
+  else {
+    const V2 wA1 = xmul(tA, pv(pA, i1 & 3)), wB1 = xmul(tB, pv(pB, i1 >> 2));
+    if (count == 2) {
+      wa = vadd(vmul(a0, wA0), vmul(a1, wA1));
+      wb = vadd(vmul(a0, wB0), vmul(a1, wB1));
+    } else if (count == 3) {
+      const V2 wA2 = xmul(tA, pv(pA, i2 & 3));
+      wa = vadd(vadd(vmul(a0, wA0), vmul(a1, wA1)), vmul(a2, wA2));
+      wb = wa;
+    }
+  }
+  cache.metric = count == 2 ? vlen(vsub(w0, w1)) : (count == 3 ? vcross(vsub(w1, w0), vsub(w2, w0)) : 0.0f);
+  cache.count = count;
+  cache.iA0 = i0 & 3; cache.iB0 = i0 >> 2; cache.iA1 = i1 & 3; cache.iB1 = i1 >> 2; cache.iA2 = i2 & 3; cache.iB2 = i2 >> 2;
+  return vlen(vsub(wa, wb));
+}
+#else
 __device__ inline float gjk_distance(SCache& cache, const Poly* pA, Xf tA, const Poly* pB, Xf tB) {
   SV v0, v1, v2;
   v0.wA = v0.wB = v0.w = zero2(); v0.a = 0.0f; v0.iA = v0.iB = 0;
@@ -1332,6 +1477,9 @@ __device__ inline float gjk_distance(SCache& cache, const Poly* pA, Xf tA, const
     vx.w = vsub(vx.wB, vx.wA);
     vx.a = 0.0f;
     ++iter;
+#ifdef NASCAR_PROFILE
+    ++cache.iters;
+#endif
     bool dup = (vx.iA == sA0 && vx.iB == sB0) || (saveCount > 1 && vx.iA == sA1 && vx.iB == sB1) ||
                (saveCount > 2 && vx.iA == sA2 && vx.iB == sB2);
     if (dup) break;
@@ -1352,6 +1500,8 @@ __device__ inline float gjk_distance(SCache& cache, const Poly* pA, Xf tA, const
   cache.iA0 = v0.iA; cache.iB0 = v0.iB; cache.iA1 = v1.iA; cache.iB1 = v1.iB; cache.iA2 = v2.iA; cache.iB2 = v2.iB;
   return vlen(vsub(wa, wb));
 }
+
+#endif
 
 struct Sweep { V2 c0, c; float a0, a, alpha0; };
 __device__ __forceinline__ Xf sweep_xf(const Sweep& s, float beta) {
@@ -1518,6 +1668,9 @@ __device__ inline float time_of_impact(int* state, const Poly* pA, const Sweep& 
     if (done) break;
     if (iter == 20) { *state = TOI_FAILED; out_t = t1; break; }
   }
+#ifdef NASCAR_PROFILE
+  if (prof_iters) prof_iters[2] += cache.iters;
+#endif
   return out_t;
 }
 
@@ -1743,11 +1896,22 @@ __device__ inline void solve_toi(Car& c, const WallSet& S, float dt, float frict
         const int owner = jb.x & 0xFF;
         PCOUNT(12, 1); CCOUNT(c, 2, 1);
 #ifdef NASCAR_PROFILE   // per computing lane: TOI outer / root-finder iterations, GJK and separation-function cycles
-        int it2[2] = {0, 0}; unsigned long long cy2[2] = {0ull, 0ull};
+        int it2[3] = {0, 0, 0}; unsigned long long cy2[2] = {0ull, 0ull};
         L.res[j] = toi_alpha(L.sw0[owner], L.sw1[owner], ldg(W + jb.y), it2, cy2);
         CCOUNT(c, 6, it2[0]); CCOUNT(c, 7, it2[1]); CCOUNT(c, 9, cy2[0]); CCOUNT(c, 10, cy2[1]);
 #else
         L.res[j] = toi_alpha(L.sw0[owner], L.sw1[owner], ldg(W + jb.y));
+#endif
+#if defined(NASCAR_PROFILE) && defined(NASCAR_TOI_CAPTURE)
+        if (g_prof) {
+          const unsigned long long k = atomicAdd(&g_prof[TCAP_BASE], 1ull);
+          if (k < TCAP_MAX) {
+            float4* r = (float4*)&g_prof[TCAP_BASE + 8 + k * 8];
+            const LWall w = ldg(W + jb.y);
+            r[0] = L.sw0[owner]; r[1] = L.sw1[owner];
+            r[2] = make_float4(w.px, w.py, w.qs, w.qc); r[3] = make_float4(w.hx, w.hy, w.ang, __int_as_float(w.key));
+          }
+        }
 #endif
       }
       wave_lds_sync();

@@ -1353,7 +1353,9 @@ __device__ __forceinline__ void ray_lane(const Params& P, const TrackDev& T, con
     const V2 p1 = V(ps.x, ps.y);
     const double px = ps.x, py = ps.y, ang = ps.z;
     const double2 cs = P.pose_cs[pass == 0 ? (size_t)n : (size_t)P.N + n];
+    if (LPC == 16 && pass == 0) PROFR(2);   // profile builds (16 lanes per car): pose loaded
     const int base = beam_cell_base(G, p1.x, p1.y);
+    if (LPC == 16 && pass == 0) { asm volatile("" :: "v"(base)); PROFR(3); }   // beam cell looked up
     // direction bin of sa = -radians(22.5 i) + ang (f64; the lists carry a 2e-3 rad guard) -> list slot
     // ray i is exactly BEAM_STRIDE bins clockwise of ray 0 in real arithmetic, and the f64 rounding of
     // sa_i (~1e-15 rad) is far inside the lists' 2e-3 rad guard, so bin_i = bin_0 - BEAM_STRIDE i:
@@ -1396,7 +1398,13 @@ __device__ __forceinline__ void ray_lane(const Params& P, const TrackDev& T, con
         const BeamHead h = beam_head(G, base + sl);
         bi = __uint_as_float((h.w[0].x & 1u) | 0x3f800000u);
 #else
+#ifdef NASCAR_PROFILE
+        const BeamHead hh = beam_head(G, base + sl);
+        if (LPC == 16 && pass == 0) { PROFR(4); asm volatile("" :: "v"(hh.w[0].x)); PROFR(5); }   // end points; head loaded
+        bi = ray_walk(G, sw, base + sl, hh, p1, p2, dx, dy);
+#else
         bi = ray_walk(G, sw, base + sl, beam_head(G, base + sl), p1, p2, dx, dy);
+#endif
 #endif
       } else {
         PCOUNT(9, 1);
@@ -1418,6 +1426,7 @@ __device__ __forceinline__ void ray_lane(const Params& P, const TrackDev& T, con
       if (pass == 1 || (mode & PM_A_OBS)) { *(float2*)(obs + at) = lo; *(float2*)(obs + at + 2) = hi; }
       if (pass == 0 && (mode & PM_A_TERM)) { *(float2*)(terminal_obs + at) = lo; *(float2*)(terminal_obs + at + 2) = hi; }
     } else {
+      if (pass == 0) { asm volatile("" :: "v"(v[0])); PROFR(6); }   // profile builds: walk done
       const size_t at = (size_t)nq * 38 + 22 + rq;
       if (pass == 1 || (mode & PM_A_OBS)) obs[at] = v[0];
       if (pass == 0 && (mode & PM_A_TERM)) terminal_obs[at] = v[0];
@@ -1523,14 +1532,17 @@ ray_sensor_kernel(Params P, float* obs, float* terminal_obs, int passes, int SUB
   const int el = slot / C, car = slot - el * C;
   const int env = blk_env_of(P, el, b * P.epb + el);
   const TrackDev& T = P.tracks[blk_track_of(P, b)];
+  PROFR_RT(14); PROFR(0);   // profile builds: stamp slots 0-7 (16 lanes per car: ray_lane's 2-6), realtime 14 / 15
   {
     float4* s_w = (float4*)smem;
     const int nw2 = 2 * T.nwall;
     for (int k = t; k < nw2; k += RB) s_w[k] = ldg(T.swall + k);
     __syncthreads();
   }
+  PROFR(1);
   if (env < 0) return;
   ray_lane<LPC>(P, T, (const float4*)smem, env * C + car, r, obs, terminal_obs, passes);
+  PROFR(7); PROFR_RT(15);
 }
 
 __device__ __forceinline__ uint32_t mix32(uint64_t x) {   // splitmix64 finaliser
@@ -2030,6 +2042,7 @@ static __device__ void fused_logic_phase(const Params& P, int tid, int el, int c
   TrackDev T = P.tracks[blk_track_of(P, (blockIdx.x + P.blk0))];
   stage_track_lds(T, F.TL, tid);
   __syncthreads();
+  PROF(7);
   T.segs = F.TL.segs; T.prefix = F.TL.prefix;
   logic_run(P, T, F.TL, F.L, tid, el, car, env, n, c, sim, pend_in, reason_in, obs, reward, car_flags, env_flags, auto_reset,
             terminal_obs);
@@ -2046,8 +2059,11 @@ model_logic_kernel(Params P, const void* actions, int discrete, int want_term, i
   const int n = env >= 0 ? env * C + car : 0;
   model_block<true>(P, actions, discrete, want_term, policy, seed, step, pobs, tid, env, n);
   __syncthreads();   // the block's Box2D steps done: body state stored, contact slots written back (LDS free)
+  PROF(6);           // profile builds: the fused kernel's logic half (stamp slots 6-9)
   if (P.car_contact) car_contact_block(P, tid, el, car, env, n);   // block-uniform; holds its own barrier
   fused_logic_phase(P, tid, el, car, env, n, obs, reward, car_flags, env_flags, auto_reset, terminal_obs);
+  PROF(8);
+  PROF_RT(9);
 }
 
 // Fused multi-step rollout (nascar_rollout): K env steps of each block's envs in one launch, the actions

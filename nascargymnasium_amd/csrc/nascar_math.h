@@ -110,10 +110,40 @@ __host__ __device__ inline double reduce_large(uint32_t xi, int* np) {
 #ifndef SINCOS_NOINLINE
 #define SINCOS_NOINLINE 0   // A/B: one out-of-line copy of b2Rot::Set's sincosf instead of one per call site
 #endif
+#ifndef SINCOS_V2
+#define SINCOS_V2 1
+#endif
 #if defined(__HIP_DEVICE_COMPILE__) && SINCOS_NOINLINE
 __attribute__((noinline))
 #endif
 __host__ __device__ inline void glibc_sincosf(float y, float* sp, float* cp) {
+#if SINCOS_V2
+  // One straight-line path for |y| < 120 (the only rare branch is glibc's reduce_large): glibc's |y| < pi/4 path is
+  // reduce_fast's n = 0 case (x - 0 * pi/2 == x exactly, sign +1, first table row), and both polynomials are
+  // evaluated side by side and assigned by the quadrant's parity (glibc evaluates the same two polynomials on the
+  // same values), so the dependent chain is one polynomial deep instead of two plus branches.  |y| < 2^-12 returns
+  // (y, 1) as glibc does (also keeping sin(-0) = -0).  Bit-identical to the branchy form over all 2^32 floats
+  // (tests/test_sincos_cpu.py).
+  const uint32_t t = top12(y);
+  if (t >= top12(120.0f)) {
+    uint32_t xi = f_as_u(y);
+    int sign = xi >> 31, n = 0;
+    const double x = reduce_large(xi, &n);
+    const double sgn = ((n + sign + 1) & 2) ? -1.0 : 1.0;
+    const int row = (n + sign) & 2;
+    const double xs = x * sgn, x2 = x * x;
+    *sp = sc_poly(xs, x2, n, row);
+    *cp = sc_poly(xs, x2, n ^ 1, row);
+    return;
+  }
+  int n = 0;
+  const double x = reduce_fast((double)y, &n);
+  const double xs = ((n + 1) & 2) ? -x : x, x2 = x * x;   // x * sgn, sgn = {1, -1, -1, 1}[n & 3]
+  const float ps = sc_poly(xs, x2, 0, 0), pc = sc_poly(xs, x2, 1, n & 2);
+  const bool odd = n & 1, tiny = t < top12(0x1p-12f);
+  *sp = tiny ? y : (odd ? pc : ps);
+  *cp = tiny ? 1.0f : (odd ? ps : pc);
+#else
   double x = y;
   int n = 0, row = 0;
   double sgn = 1.0;
@@ -138,6 +168,7 @@ __host__ __device__ inline void glibc_sincosf(float y, float* sp, float* cp) {
   const double xs = x * sgn, x2 = x * x;
   *sp = sc_poly(xs, x2, n, row);
   *cp = sc_poly(xs, x2, n ^ 1, row);
+#endif
 }
 
 // Python float64 helpers

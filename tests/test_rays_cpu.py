@@ -19,8 +19,9 @@ def test_ray_end_points_match_direct_evaluation(tmp_path):
 
 
 def test_glibc_sincosf_restatement_matches_host_libm(tmp_path):
-    """nascar_math.h glibc_sincosf (b2Rot::Set's sinf/cosf on the device, load-free fused form) equals the host
-    glibc on every 61st float bit pattern (the whole float range was checked the same way with stride 1)."""
+    """nascar_math.h glibc_sincosf (b2Rot::Set's sinf/cosf on the device: load-free, and since round 5 one
+    straight-line path with both polynomials side by side) equals the host glibc on every 61st float bit pattern (the
+    whole float range -- 4 278 190 080 finite floats -- was checked the same way with stride 1: 0 mismatches)."""
     exe = tmp_path / "sincosf_harness"
     subprocess.run(["hipcc", "-O2", "-ffp-contract=off", "-o", str(exe),
                     os.path.join(ROOT, "tests", "native", "sincosf_harness.cpp")], check=True)

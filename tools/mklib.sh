@@ -4,5 +4,5 @@
 # read only by such builds): tools/mklib.sh OUT.so [SRC_DIR(csrc)] [extra hipcc flags...]
 out=$1; shift
 src=${1:-nascargymnasium_amd/csrc}; shift
-hipcc --offload-arch=gfx950 -O3 -ffp-contract=off -fno-fast-math -fPIC -shared -std=c++17 -Wno-unused-value \
+hipcc --offload-arch=gfx950 -O3 -ffp-contract=off -fno-fast-math -fno-slp-vectorize -fPIC -shared -std=c++17 -Wno-unused-value \
   -Wno-unused-result -DNASCAR_AB_KNOBS "$@" -o "$out" "$src/nascar_kernels.hip"

@@ -59,6 +59,8 @@ def main():
     ap.add_argument("--define", action="append", default=[], help="extra -D for the profile build")
     ap.add_argument("--rollout", type=int, default=0, help="also profile one fused rollout launch of this many steps "
                     "(per-wave phase cycles per step: model, logic, sensors, each up to its block barrier)")
+    ap.add_argument("--capture", default=None, help="library built with -DNASCAR_TOI_CAPTURE: save every computed TOI job's "
+                    "inputs (float32 [n, 16]: car sweep c0.xy c.xy, a0 a alpha0 -, wall px py qs qc hx hy ang key) to this .npy")
     ap.add_argument("--count", action="store_true", help="library built with -DNASCAR_PROFILE_COUNT (sensor event "
                     "counters; the atomics distort that build's sensor timings)")
     a = ap.parse_args()
@@ -93,7 +95,9 @@ def main():
     CPROF_BASE = LPROF_BASE + NW * 16
     N = a.envs * a.cars
     RPROF_BASE = CPROF_BASE + (1 << 20) * 16
-    buf = torch.zeros(RPROF_BASE + 65536 * 5, dtype=torch.int64, device="cuda:0")
+    TCAP_BASE, TCAP_MAX = RPROF_BASE + 65536 * 5, 16384
+    buf = torch.zeros(TCAP_BASE + 8 + TCAP_MAX * 8, dtype=torch.int64, device="cuda:0")
+    caps = []
     L.nascar_debug_profile(ctypes.c_void_p(buf.data_ptr()))
     for s in range(a.steps):
         acts = actions(k0 + a.warmup + s)
@@ -102,6 +106,10 @@ def main():
         env.launch_step(acts, auto_reset=True)
         torch.cuda.synchronize()
         b = buf.cpu().numpy()
+        if a.capture:   # -DNASCAR_TOI_CAPTURE builds: this step's b2TimeOfImpact jobs (sweep s0, s1, wall record)
+            nc = min(int(b[TCAP_BASE]), TCAP_MAX)
+            caps.append(b[TCAP_BASE + 8:TCAP_BASE + 8 + nc * 8].copy().view(np.float32).reshape(nc, 16))
+            print(f"captured {nc} TOI jobs")
         model = b[:NW * 16].reshape(NW, 16)
         sens = b[NW * 16:2 * NW * 16].reshape(NW, 16)
         cnt = b[2 * NW * 16:2 * NW * 16 + 8]
@@ -213,6 +221,18 @@ def main():
                 m = (cp[:, 1] >= lo) & (cp[:, 1] < hi)
                 if m.any():
                     print(f"  cars with {lo}-{hi - 1} contacts: {m.mean() * 100:5.1f}%  mean b2 cycles {cyc[m].mean():.0f}")
+        fz = model[(model[:, 6] != 0) & (model[:, 8] != 0) & (model[:, 15] != 0)].astype(np.float64)
+        if len(fz):   # the fused model_logic_kernel's logic half: barrier wait, loads + staging, logic_run
+            i_last = np.argmax(fz[:, 9])
+            rt0 = fz[:, 14].min()
+            print(f"model_logic_kernel logic half: waves {len(fz)}; barrier wait (model end -> block barrier) mean "
+                  f"{(fz[:, 6] - fz[:, 5]).mean():.0f}, loads + staging mean {(fz[:, 7] - fz[:, 6]).mean():.0f}, logic_run mean "
+                  f"{(fz[:, 8] - fz[:, 7]).mean():.0f} cycles; realtime us: median model end {(np.median(fz[:, 15]) - rt0) / 100:.1f}, "
+                  f"median logic end {(np.median(fz[:, 9]) - rt0) / 100:.1f}, last logic end {(fz[:, 9].max() - rt0) / 100:.1f}")
+            w = fz[i_last]
+            print(f"  last-ending wave: model half {w[5] - w[0]:.0f} cycles (b2_step {w[4] - w[3]:.0f}), barrier wait "
+                  f"{w[6] - w[5]:.0f}, loads + staging {w[7] - w[6]:.0f}, logic_run {w[8] - w[7]:.0f}; model end "
+                  f"{(w[15] - rt0) / 100:.1f} us, logic end {(w[9] - rt0) / 100:.1f} us")
         phases(logic, LOGIC, 0, "logic_kernel")
         if a.raw:
             live = sens[sens[:, 0] != 0]
@@ -227,6 +247,19 @@ def main():
         if n:
             extra = (f"\n  per active lane: groups visited {cnt[0] / n:.1f}, in range {cnt[1] / n:.1f}, open {cnt[2] / n:.1f}, "
                      f"walls {cnt[3] / n:.1f}, wall-ray pairs {cnt[4] / n:.1f}, exact casts {cnt[5] / n:.1f}")
+        rs = sens[(sens[:, 0] != 0) & (sens[:, 7] != 0) & (sens[:, 2] != 0)].astype(np.float64)
+        if len(rs):   # ray_sensor_kernel at 16 lanes per car (PROFR stamps)
+            d = np.diff(rs[:, 0:8], axis=1)
+            names = ["wall image staging + barrier", "pose load", "beam cell lookup", "ray end point (f64)", "list head load",
+                     "walk", "store"]
+            tot = d.sum(1)
+            print(f"ray_sensor_kernel: waves {len(rs)}, mean wave cycles {tot.mean():.0f} (p50 {np.median(tot):.0f}, max "
+                  f"{tot.max():.0f}); realtime us: last start {(rs[:, 14].max() - rs[:, 14].min()) / 100:.1f}, median end "
+                  f"{(np.median(rs[:, 15]) - rs[:, 14].min()) / 100:.1f}, last end {(rs[:, 15].max() - rs[:, 14].min()) / 100:.1f}")
+            for k, nm in enumerate(names):
+                print(f"  {nm:34s} mean {d[:, k].mean():9.0f}  p50 {np.median(d[:, k]):9.0f}  max {d[:, k].max():9.0f}")
+            w = rs[np.argmax(rs[:, 15])]
+            print("  last-ending wave: " + ", ".join(f"{nm} {w[k + 1] - w[k]:.0f}" for k, nm in enumerate(names)))
         phases(sens, SENSOR, 0, "sensor_kernel", extra)
         cb = b[2 * NW * 16 + 8:2 * NW * 16 + 16]
         if cb[4] or cb[5] or cb[6]:
@@ -239,6 +272,8 @@ def main():
         if cb[0]:
             print(f"ray_sensor_kernel: rays {cb[0]}, fallback rays {cb[1]} ({100 * cb[1] / cb[0]:.2f}%), "
                   f"list entries per ray {cb[3] / max(1, cb[0] - cb[1]):.2f}, walked {cb[2] / max(1, cb[0] - cb[1]):.2f}")
+    if a.capture and caps:
+        np.save(a.capture, np.concatenate(caps))
     if a.rollout:
         import time
         buf.zero_()

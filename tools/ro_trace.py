@@ -19,8 +19,8 @@ a = ap.parse_args()
 f = glob.glob(a.dir + "/**/*kernel_trace.csv", recursive=True)[0]
 rows = []
 for r in csv.DictReader(open(f)):
-    name = r["Kernel_Name"].split("(")[0].replace("void ", "")
-    if name in ("model_kernel", "logic_kernel", "ray_sensor_kernel"):
+    name = r["Kernel_Name"].split("(")[0].split("<")[0].replace("void ", "")
+    if name in ("model_kernel", "logic_kernel", "model_logic_kernel", "ray_sensor_kernel"):
         rows.append((int(r["Dispatch_Id"]), name, int(r["Stream_Id"]), int(r["Start_Timestamp"]), int(r["End_Timestamp"]),
                      int(r["Grid_Size_X"])))
 rows.sort()
@@ -52,6 +52,16 @@ for t, d, s in ev:
     last = t
     active[s] += d
 print("  streams busy: " + ", ".join(f"{k}: {v / 1000:.1f} us" for k, v in sorted(prof.items())))
+# per stream: kernel durations and the idle gap before each kernel (previous end on the same stream -> start)
+for s, rs in sorted(by.items()):
+    rs = sorted(rs, key=lambda r: r[3])
+    gaps = [(b[3] - a[4]) / 1000 for a, b in zip(rs, rs[1:])]
+    dur = collections.defaultdict(list)
+    for r in rs:
+        dur[r[1]].append((r[4] - r[3]) / 1000)
+    g = sorted(gaps)
+    print(f"  stream {s}: " + ", ".join(f"{k} mean {sum(v) / len(v):.1f} max {max(v):.1f} us" for k, v in sorted(dur.items()))
+          + (f"; gaps mean {sum(g) / len(g):.1f} p50 {g[len(g) // 2]:.1f} max {g[-1]:.1f} us" if g else ""))
 # per-step end times per stream (sensor kernel ends)
 for s, rs in sorted(by.items()):
     ends = [(r[4] - t0) / 1000 for r in rs if r[1] == "ray_sensor_kernel"]
