@@ -61,6 +61,8 @@ def main():
                     "(per-wave phase cycles per step: model, logic, sensors, each up to its block barrier)")
     ap.add_argument("--capture", default=None, help="library built with -DNASCAR_TOI_CAPTURE: save every computed TOI job's "
                     "inputs (float32 [n, 16]: car sweep c0.xy c.xy, a0 a alpha0 -, wall px py qs qc hx hy ang key) to this .npy")
+    ap.add_argument("--two-kernel", action="store_true", help="step through model_kernel + logic_kernel (the logic "
+                    "kernel's own stamps) instead of the fused model_logic_kernel")
     ap.add_argument("--count", action="store_true", help="library built with -DNASCAR_PROFILE_COUNT (sensor event "
                     "counters; the atomics distort that build's sensor timings)")
     a = ap.parse_args()
@@ -76,6 +78,8 @@ def main():
     L = _lib.lib()
     L.nascar_debug_profile.argtypes = [ctypes.c_void_p]
     env = BatchedCarEnv(a.envs, a.cars, track_path(a.track), device="cuda:0")
+    if a.two_kernel:
+        env.set_fused_logic(False)
     env.reset()
     g = torch.Generator(device="cuda:0")
     g.manual_seed(7)
@@ -94,7 +98,7 @@ def main():
         env.step(actions(k0 + k), auto_reset=True)
     CPROF_BASE = LPROF_BASE + NW * 16
     N = a.envs * a.cars
-    RPROF_BASE = CPROF_BASE + (1 << 20) * 16
+    RPROF_BASE = CPROF_BASE + (1 << 19) * 48   # device: CPROF_STRIDE 48 per car
     TCAP_BASE, TCAP_MAX = RPROF_BASE + 65536 * 5, 16384
     buf = torch.zeros(TCAP_BASE + 8 + TCAP_MAX * 8, dtype=torch.int64, device="cuda:0")
     caps = []
@@ -132,7 +136,7 @@ def main():
             st, en = m[:, 14], m[:, 15]
             print(f"    realtime us: last start {(st.max() - st.min()) / 100:.1f}, median end {(np.median(en) - st.min()) / 100:.1f}, "
                   f"last end {(en.max() - st.min()) / 100:.1f}")
-        cp = b[CPROF_BASE:CPROF_BASE + N * 32].reshape(N, 32)   # CPROF_STRIDE
+        cp = b[CPROF_BASE:CPROF_BASE + N * 48].reshape(N, 48)   # CPROF_STRIDE
         if cp[:, 0].any():
             cyc = cp[:, 0]
             print(f"  per-car b2_step cycles: mean {cyc.mean():.0f}, p50 {np.percentile(cyc, 50):.0f}, "
@@ -179,6 +183,11 @@ def main():
                       f"{cp[:, 19].sum() / ne:.2f}, {cp[:, 20].sum() / ne:.0f} cycles; island contacts {cp[:, 18].sum() / ne:.2f}), "
                       f"contact updates {cp[:, 12].sum() / ne:.0f}, sync_fixtures+flags {cp[:, 17].sum() / ne:.0f}, "
                       f"find_new_contacts {cp[:, 16].sum() / ne:.0f}")
+                print(f"    event sub-phases (cycles per event): scan + advance {cp[:, 38].sum() / ne:.0f}, manifold round "
+                      f"{cp[:, 32].sum() / ne:.0f}, event contact's update {cp[:, 33].sum() / ne:.0f}; TOI island: init "
+                      f"{cp[:, 34].sum() / ne:.0f}, position iterations {cp[:, 20].sum() / ne:.0f}, velocity init "
+                      f"{cp[:, 35].sum() / ne:.0f}, 6 velocity iterations {cp[:, 36].sum() / ne:.0f}, integrate + transform + "
+                      f"report {cp[:, 37].sum() / ne:.0f}")
                 per = (128 // a.cars) * a.cars             # cars per workgroup (SBLOCK 128, whole envs)
                 l0 = np.sort(np.concatenate([np.arange(0, N, per), np.arange(64, N, per)]))
                 l0 = l0[l0 < N]                            # lane 0 of each wave
