@@ -67,7 +67,7 @@ __device__ unsigned long long* g_prof = nullptr;
 #define CPROF_BASE (LPROF_BASE + 65536 * 16)
 // per-car slots (CPROF_STRIDE per car): non-returning atomics, so a count does not wait on memory (a read-modify-
 // write here put a dependent global round trip into every counted phase)
-#define CPROF_STRIDE 32
+#define CPROF_STRIDE 48
 #define CCOUNT(c, slot, v) do { if (g_prof) (void)atomicAdd(&g_prof[CPROF_BASE + (size_t)(c).pid * CPROF_STRIDE + (slot)], \
                                                           (unsigned long long)(v)); } while (0)
 #define CTIME_BEGIN() const unsigned long long _ct0 = __builtin_amdgcn_s_memtime()
@@ -1678,7 +1678,11 @@ template <int NMAX>
 __device__ __forceinline__ void island_solve_toi_buf(Car& c, const LWall* W, const int* cidx, int n, float subdt, float friction,
                                                      VC* vc) {
   BodyState A; A.c = c.c; A.a = c.a; A.v = c.v; A.w = c.w;
+  {
+  CTIME_BEGIN();
   cs_init<NMAX>(vc, n, c, cidx, W, false, 1.0f);
+  CTIME_END(c, 34);   // profile builds: TOI island sub-phases in slots 34-37
+  }
   RotCache rcA; rcA.bits = __float_as_uint(c.a) ^ 1u; rcA.q.s = 0.0f; rcA.q.c = 1.0f;   // (empty: no angle matches)
   {
   CTIME_BEGIN();
@@ -1688,13 +1692,23 @@ __device__ __forceinline__ void island_solve_toi_buf(Car& c, const LWall* W, con
   CTIME_END(c, 20);
   }
   c.c0 = A.c; c.a0 = A.a;
+  {
+  CTIME_BEGIN();
   cs_init_velocity<NMAX>(vc, n, c, A);
+  CTIME_END(c, 35);
+  }
+  {
+  CTIME_BEGIN();
   SOLVER_ITER_LOOP
   for (int it = 0; it < 6; ++it) cs_solve_velocity<NMAX>(vc, n, A, friction);
+  CTIME_END(c, 36);
+  }
+  CTIME_BEGIN();
   integrate_positions(A, subdt);
   c.c = A.c; c.a = A.a; c.v = A.v; c.w = A.w;
   c.xf.q = rot_cached(rcA, c.a); c.xf.p = vsub(c.c, rmul(c.xf.q, zero2()));   // sync_transform
   report<NMAX>(c, vc, n);
+  CTIME_END(c, 37);
 }
 template <int NMAX>
 __device__ __forceinline__ void island_solve_toi_n(Car& c, const LWall* W, const int* cidx, int n, float subdt, float friction) {
@@ -1933,6 +1947,9 @@ __device__ inline void solve_toi(Car& c, const WallSet& S, float dt, float frict
     const unsigned long long te0 = __builtin_amdgcn_s_memtime();
 #endif
     // (3) this lane's scan on cached alphas and its event, as Box2D
+#ifdef NASCAR_PROFILE
+    const unsigned long long ts3 = __builtin_amdgcn_s_memtime();
+#endif
     int minC = -1; float minAlpha = 1.0f;
     bool ev = false;
     V2 bc0 = c.c0, bc = c.c; float ba0 = c.a0, ba = c.a, balpha0 = c.alpha0;
@@ -1967,6 +1984,10 @@ __device__ inline void solve_toi(Car& c, const WallSet& S, float dt, float frict
     // computed up front by any present lane; the owners then apply them in Box2D's order (contact_apply), and
     // only results they reach are used.  Contacts past the LDS job capacity are updated by their owner.
     int moff = MANI_JOBCAP;   // this lane's first result slot (contact i -> slot moff + i)
+#ifdef NASCAR_PROFILE
+    const unsigned long long tm0 = __builtin_amdgcn_s_memtime();
+    if (ev) CCOUNT(c, 38, tm0 - ts3);   // scan on cached alphas + advance to the TOI pose
+#endif
 #if TOI_COOP_MANI
     if (__ballot(ev)) {   // wave-uniform
       ManiWaveLDS& M = g_wave_lds[threadIdx.x >> 6].mani;
@@ -1994,12 +2015,16 @@ __device__ inline void solve_toi(Car& c, const WallSet& S, float dt, float frict
       wave_lds_sync();
     }
 #endif
+#ifdef NASCAR_PROFILE
+    if (ev) CCOUNT(c, 32, __builtin_amdgcn_s_memtime() - tm0);   // the wave's manifold round for this event
+#endif
     if (ev) {
       {
         {
         CTIME_BEGIN();
         toi_contact_update(c, minC, W, moff);
         CTIME_END(c, 12);
+        CTIME_END(c, 33);   // (the event contact's own update)
         }
         c.ct[minC].flags &= ~CT_TOI;
         ++c.ct[minC].toiCount;

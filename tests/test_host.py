@@ -60,3 +60,17 @@ def test_capi_library_exports_every_declared_symbol():
     L = ctypes.CDLL(_lib.LIB_PATH)
     for sym in declared:
         assert hasattr(L, sym), sym
+
+
+def test_product_library_reads_no_ab_knobs():
+    """The product build reads no environment variable that changes a kernel path (round-4 verdict item 7): the A/B
+    knobs (NASCAR_EPB, NASCAR_RAY_LPC, NASCAR_FUSE_ML, NASCAR_RBLOCK, NASCAR_BEAM_CELL, NASCAR_SENSOR,
+    NASCAR_NO_MAP_SHORTCUT, NASCAR_ACTOR_FP32_VALU) exist only in tools builds (-DNASCAR_AB_KNOBS, tools/mklib.sh);
+    the library's only environment reads are GPU_MAX_HW_QUEUES (the process's hardware queues, which bound the
+    rollout's shard streams) and NASCAR_VERBOSE (diagnostic prints)."""
+    from nascargymnasium_amd import _lib
+    if not os.path.exists(_lib.LIB_PATH):
+        _lib.build()
+    blob = open(_lib.LIB_PATH, "rb").read()
+    names = set(m.decode() for m in re.findall(rb"NASCAR_[A-Z0-9_]+", blob))
+    assert names <= {"NASCAR_VERBOSE"}, names

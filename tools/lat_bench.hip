@@ -3,7 +3,7 @@
 #include "../nascargymnasium_amd/csrc/nascar_device.h"
 using namespace nascar;
 #define N 256
-__global__ void __launch_bounds__(64) lat_kernel(float x0, double y0, unsigned long long* out, float* sink) {
+__global__ void __launch_bounds__(64) lat_kernel(float x0, double y0, unsigned long long* out, float* sink, int flat_lds) {
   __shared__ float lds[64];
   const int lane = threadIdx.x;
   float x = x0 + lane * 1e-7f; double y = y0 + lane * 1e-9;
@@ -23,10 +23,23 @@ __global__ void __launch_bounds__(64) lat_kernel(float x0, double y0, unsigned l
   MEASURE(for (int i = 0; i < N / 4; ++i) { lds[lane] = x; __builtin_amdgcn_s_waitcnt(0xc07f); x = lds[lane ^ 1] + 1.0f; })  // 6 lds
   MEASURE(for (int i = 0; i < N; ++i) { asm volatile("v_mul_f32 %0, %0, %1" : "+v"(x) : "v"(x0)); })            // 7 dep mul
   MEASURE(for (int i = 0; i < N / 4; ++i) { x = (x > 0.5f) ? x * 0.5f : x + 0.7f; })                                 // 8 select chain
+  // 9: the same LDS round trip through a generic (flat) pointer, as the Box2D step's contact records are reached
+  float* gp = flat_lds ? (float*)lds : sink + 64;
+  asm volatile("" : "+v"(gp));
+  MEASURE(for (int i = 0; i < N / 4; ++i) { gp[lane] = x; x = gp[lane ^ 1] + 1.0f; })
+  // 10: flat LDS round trips while a global store is outstanding (one store to sink per iteration)
+  MEASURE(for (int i = 0; i < N / 4; ++i) { sink[128 + lane] = x; gp[lane] = x; x = gp[lane ^ 1] + 1.0f; })
+  // 11: LDS round trips with a global store outstanding (ds ops do not wait for it)
+  MEASURE(for (int i = 0; i < N / 4; ++i) { sink[128 + lane] = x; lds[lane] = x; __builtin_amdgcn_s_waitcnt(0xc07f); x = lds[lane ^ 1] + 1.0f; })
+  // 12: f64 divide, 13: f64 sqrt (dependent)
+  MEASURE(for (int i = 0; i < N / 4; ++i) { y = 1.0 / (y + 1.5); } x += (float)y;)
+  MEASURE(for (int i = 0; i < N / 4; ++i) { y = sqrt(y + 1.5); } x += (float)y;)
+  // 14: global load round trip (L2-warm, dependent)
+  MEASURE(for (int i = 0; i < N / 4; ++i) { x = sink[64 + (((int)x) & 3)] + x; })
   if (lane == 0) sink[0] = x;
 }
 extern "C" int lat_bench(unsigned long long* out, float* sink) {
-  hipLaunchKernelGGL(lat_kernel, dim3(1), dim3(64), 0, 0, 1.25f, 1.0000001, out, sink);
-  hipLaunchKernelGGL(lat_kernel, dim3(1), dim3(64), 0, 0, 1.25f, 1.0000001, out, sink);
+  hipLaunchKernelGGL(lat_kernel, dim3(1), dim3(64), 0, 0, 1.25f, 1.0000001, out, sink, 1);
+  hipLaunchKernelGGL(lat_kernel, dim3(1), dim3(64), 0, 0, 1.25f, 1.0000001, out, sink, 1);
   return hipDeviceSynchronize() == hipSuccess ? 0 : -1;
 }
