@@ -122,8 +122,9 @@ int nascar_get_envs_per_block(NascarHandle* h);
 int nascar_set_sensor_lanes(NascarHandle* h, int32_t lanes);
 
 /* Threads per workgroup of the 16-lane distance-sensor kernel (no reference counterpart; src/distance_sensor.py:93-115
- * casts one ray at a time): 256, 512 or 1024 (each workgroup stages the track's wall image in LDS once for
- * threads / 16 cars); 0 = automatic (512).  Identical results at any size. */
+ * casts one ray at a time): 64 or 128 (the walks read the track's wall image from global memory; no LDS), 256, 512
+ * or 1024 (each workgroup stages the wall image in LDS once for threads / 16 cars); 0 = automatic (128).  Identical
+ * results at any size. */
 int nascar_set_sensor_block(NascarHandle* h, int32_t threads);
 
 /* Cell size (m) of the distance sensors' beam lists for the tracks added to this handle AFTER the call (host-built

@@ -119,7 +119,8 @@ class BatchedCarEnv:
         _lib.check(self.L.nascar_set_sensor_lanes(self.h, int(lanes)))
 
     def set_sensor_block(self, threads: int = 0):
-        """threads per workgroup of the 16-lane sensor kernel: 256, 512 or 1024 (0: automatic, 512); identical results"""
+        """threads per workgroup of the 16-lane sensor kernel: 64 / 128 (walls read from global memory) or 256 / 512 /
+        1024 (walls staged in LDS per workgroup); 0: automatic (128); identical results"""
         _lib.check(self.L.nascar_set_sensor_block(self.h, int(threads)))
 
     def set_perf_history(self, enable: bool = True):

@@ -1285,6 +1285,8 @@ __device__ __forceinline__ void quad_transpose(const float v[4], float o[4], int
 // One ray's walk of its beam list (list index li, head record h = G.head[li]): the first BEAM_HEAD entries from
 // the head, the rest of the list only when all of them were walked; stops at the first entry whose distance
 // bound lies beyond the best hit.  Returns the best b2PolygonShape::RayCast fraction (2 = no hit).
+// GW: the wall image sw is the track's global one (read through the L2), else the workgroup's LDS copy.
+template <bool GW>
 __device__ __forceinline__ float ray_walk(const BeamGrid& G, const float4* __restrict__ sw, int li, const BeamHead& h, V2 p1,
                                           V2 p2, float dx, float dy) {
   float bi = 2.0f;
@@ -1298,7 +1300,8 @@ __device__ __forceinline__ float ray_walk(const BeamGrid& G, const float4* __res
     if ((float)(v >> 16) * 0.01f > bi * 250.0f * 1.00001f + 0.01f) { more = false; break; }
     const int j = (int)(v & 0xFFFFu);
     PCOUNT(10, 1);
-    bi = wall_cast(sw[2 * j], sw[2 * j + 1], p1, p2.x, p2.y, dx, dy, bi);
+    bi = GW ? wall_cast(ldg(sw + 2 * j), ldg(sw + 2 * j + 1), p1, p2.x, p2.y, dx, dy, bi)
+               : wall_cast(sw[2 * j], sw[2 * j + 1], p1, p2.x, p2.y, dx, dy, bi);
   }
   const uint32_t tail = hv[BEAM_HEAD];
   if (more && tail != 0u) {
@@ -1313,7 +1316,8 @@ __device__ __forceinline__ float ray_walk(const BeamGrid& G, const float4* __res
         if ((float)(v >> 16) * 0.01f > bi * 250.0f * 1.00001f + 0.01f) { stop = true; break; }
         const int j = (int)(v & 0xFFFFu);
         PCOUNT(10, 1);
-        bi = wall_cast(sw[2 * j], sw[2 * j + 1], p1, p2.x, p2.y, dx, dy, bi);
+        bi = GW ? wall_cast(ldg(sw + 2 * j), ldg(sw + 2 * j + 1), p1, p2.x, p2.y, dx, dy, bi)
+               : wall_cast(sw[2 * j], sw[2 * j + 1], p1, p2.x, p2.y, dx, dy, bi);
       }
       if (stop) break;
     }
@@ -1331,7 +1335,7 @@ __device__ __forceinline__ int beam_slot0(double ang) {   // list slot of ray 0'
 // All 4 lanes of a car are consecutive lanes of one quad and call this together.
 // LPC = 16 (small batches, see launch_sensors_impl): one ray per lane, the 16 lanes of a car store its 16 values
 // directly (64 contiguous bytes per car).
-template <int LPC = RAY_LPC>
+template <int LPC = RAY_LPC, bool GW = false>
 __device__ __forceinline__ void ray_lane(const Params& P, const TrackDev& T, const float4* __restrict__ sw, int n, int r,
                                          float* obs, float* terminal_obs, int passes) {
   static_assert(LPC == 4 || LPC == 16, "lanes per car");
@@ -1393,7 +1397,7 @@ __device__ __forceinline__ void ray_lane(const Params& P, const TrackDev& T, con
       if (base >= 0) {
         const int sl = slot_of(i);
 #if RAY_HEADS_AHEAD
-        bi = ray_walk(G, sw, base + sl, hd[q], p1, p2, dx, dy);
+        bi = ray_walk<GW>(G, sw, base + sl, hd[q], p1, p2, dx, dy);
 #elif RAY_NO_WALK   // timing probe only (wrong results): the head load without the walk
         const BeamHead h = beam_head(G, base + sl);
         bi = __uint_as_float((h.w[0].x & 1u) | 0x3f800000u);
@@ -1401,9 +1405,9 @@ __device__ __forceinline__ void ray_lane(const Params& P, const TrackDev& T, con
 #ifdef NASCAR_PROFILE
         const BeamHead hh = beam_head(G, base + sl);
         if (LPC == 16 && pass == 0) { PROFR(4); asm volatile("" :: "v"(hh.w[0].x)); PROFR(5); }   // end points; head loaded
-        bi = ray_walk(G, sw, base + sl, hh, p1, p2, dx, dy);
+        bi = ray_walk<GW>(G, sw, base + sl, hh, p1, p2, dx, dy);
 #else
-        bi = ray_walk(G, sw, base + sl, beam_head(G, base + sl), p1, p2, dx, dy);
+        bi = ray_walk<GW>(G, sw, base + sl, beam_head(G, base + sl), p1, p2, dx, dy);
 #endif
 #endif
       } else {
@@ -1498,7 +1502,7 @@ __device__ __forceinline__ void ray_block_batched(const Params& P, const TrackDe
       float bi;
       if (base[j] >= 0) {
         const int sl = (slot0[j] & ~15) | ((slot0[j] - i) & 15);
-        bi = ray_walk(G, sw, base[j] + sl, h0, p1, e, dx, dy);
+        bi = ray_walk<false>(G, sw, base[j] + sl, h0, p1, e, dx, dy);
       } else {
         bi = ray_fallback(T, p1, e.x, e.y, dx, dy, pa[j].z, i);
       }
@@ -1521,7 +1525,7 @@ __device__ __forceinline__ void ray_block_batched(const Params& P, const TrackDe
 }
 // LPC lanes per car, BLOCK / LPC cars per workgroup; `sub` sensor workgroups per step-kernel workgroup (enough for
 // its epb * C cars)
-template <int LPC, int RB = BLOCK>
+template <int LPC, int RB = BLOCK, bool GW = false>
 __global__ void __launch_bounds__(RB) __attribute__((amdgpu_waves_per_eu(RSENSOR_WPE)))
 ray_sensor_kernel(Params P, float* obs, float* terminal_obs, int passes, int SUB) {
   constexpr int CPW = RB / LPC;
@@ -1533,6 +1537,13 @@ ray_sensor_kernel(Params P, float* obs, float* terminal_obs, int passes, int SUB
   const int env = blk_env_of(P, el, b * P.epb + el);
   const TrackDev& T = P.tracks[blk_track_of(P, b)];
   PROFR_RT(14); PROFR(0);   // profile builds: stamp slots 0-7 (16 lanes per car: ray_lane's 2-6), realtime 14 / 15
+  if constexpr (GW) {   // walls read from the track's global image: no staging, no LDS, no barrier
+    PROFR(1);
+    if (env < 0) return;
+    ray_lane<LPC, true>(P, T, T.swall, env * C + car, r, obs, terminal_obs, passes);
+    PROFR(7); PROFR_RT(15);
+    return;
+  }
   {
     float4* s_w = (float4*)smem;
     const int nw2 = 2 * T.nwall;
@@ -2572,10 +2583,14 @@ struct NascarHandle {
   bool pristine = true;             // no reset / step / rollout / set_state yet: track changes apply at once
   int car_contact = 0;              // nascar_set_car_contact (build-only extension)
   int ray_lanes = 0;                // nascar_set_sensor_lanes: 0 automatic, 4 or 16 lanes per car
-  // threads per ray_sensor_kernel workgroup at 16 lanes per car (256 / 512 / 1024; NASCAR_RBLOCK): every workgroup
-  // stages the whole sensor wall image in LDS, so larger workgroups stage it once for more cars.  Driver's command
-  // (2 A/B rounds, round 4): 256 151.9 / 150.3, 512 147.3 / 147.9, 1024 151.4 / 154.4 us per step
-  int sensor_block = 512;
+  // threads per ray_sensor_kernel workgroup at 16 lanes per car (nascar_set_sensor_block).  64 / 128: the walks read
+  // the track's wall image from global memory (L2-resident); the workgroups need no LDS, so they start on any CU with
+  // free wave slots, beside the other shards' step workgroups (which hold ~52 KiB of LDS each).  256 / 512 / 1024:
+  // every workgroup stages the whole image in LDS (larger ones stage it once for more cars).  Round 5 (per-shard
+  // sensor dispatch at the steady state, 2 rounds): 64 21.0 / 20.9, 128 21.1 / 20.9, 256 (global walls) 23.5 / 23.5,
+  // 512 (global) 25.9 / 26.1, 512 (LDS) 25.9 / 25.9 us; driver's command 128 131.6 / 132.2 vs 512 (LDS) 136.7 / 134.9
+  // us per step.  Round 4 (LDS, driver's command): 256 151.9 / 150.3, 512 147.3 / 147.9, 1024 151.4 / 154.4
+  int sensor_block = 128;
   int fuse_ml = 1;                  // nascar_set_fused_logic: model_logic_kernel (default) or model_kernel + logic_kernel
   float beam_cell = BEAM_CELL_M;    // nascar_set_beam_cell: cell size (m) of the beam lists of tracks added later
   float* d_vhist = nullptr;  // [VH_RING][N] speed history (nascar_set_perf_history), outside the snapshot arena
@@ -2654,9 +2669,9 @@ extern "C" int nascar_set_beam_cell(NascarHandle* h, float meters) {
 }
 extern "C" int nascar_set_sensor_block(NascarHandle* h, int32_t threads) {
   if (!h) return fail("null argument");
-  if (threads != 0 && threads != 256 && threads != 512 && threads != 1024)
-    return fail("sensor workgroup size must be 0 (automatic: 512), 256, 512 or 1024 threads, got %d", threads);
-  h->sensor_block = threads ? threads : 512;
+  if (threads != 0 && threads != 64 && threads != 128 && threads != 256 && threads != 512 && threads != 1024)
+    return fail("sensor workgroup size must be 0 (automatic: 128), 64, 128, 256, 512 or 1024 threads, got %d", threads);
+  h->sensor_block = threads ? threads : 128;
   return 0;
 }
 extern "C" int nascar_set_sensor_lanes(NascarHandle* h, int32_t lanes) {
@@ -2681,7 +2696,7 @@ extern "C" int nascar_create(const NascarConfig* cfg, NascarHandle** out) {
   if (const char* ev = getenv("NASCAR_FUSE_ML")) h->fuse_ml = atoi(ev) != 0;
   if (const char* ev = getenv("NASCAR_RBLOCK")) {
     const int rb = atoi(ev);
-    if (rb == 256 || rb == 512 || rb == 1024) h->sensor_block = rb;
+    if (rb == 64 || rb == 128 || rb == 256 || rb == 512 || rb == 1024) h->sensor_block = rb;
   }
   if (const char* ev = getenv("NASCAR_BEAM_CELL")) {
     const float v = (float)atof(ev);
@@ -3078,6 +3093,16 @@ static void launch_sensors_impl(NascarHandle* h, const Params& P, int nb, float*
     const size_t rlds = h->max_sensor_lds;   // >= 2 float4 per wall
     const int cars = h->epb * h->C;          // cars per step-kernel workgroup
     if (ray_lpc(h) == 16) {
+      if (h->sensor_block < BLOCK) {   // 64 / 128 threads: the walls from the global image, no LDS
+        const int rb = h->sensor_block, sub = (cars + rb / 16 - 1) / (rb / 16);
+        if (rb == 64)
+          hipLaunchKernelGGL((ray_sensor_kernel<16, 64, true>), dim3(nb * sub), dim3(rb), 0, (hipStream_t)stream, P, obs,
+                             terminal_obs, passes, sub);
+        else
+          hipLaunchKernelGGL((ray_sensor_kernel<16, 128, true>), dim3(nb * sub), dim3(rb), 0, (hipStream_t)stream, P, obs,
+                             terminal_obs, passes, sub);
+        return;
+      }
       // every sensor workgroup stages the whole wall image: larger workgroups stage it for more cars
       int rb = h->sensor_block;
       while (rb > BLOCK && rb / 2 >= cars * 16) rb /= 2;   // no wider than a step workgroup's cars need (small batches)

@@ -198,22 +198,23 @@ def test_track_with_many_walls(tmp_path):
 
 
 def test_sensor_workgroup_sizes_identical():
-    """ray_sensor_kernel at 16 lanes per car in 256-, 512- (the default) and 1024-thread workgroups
-    (nascar_set_sensor_block) and at 4 lanes per car: the same sensor values on every pose, bit for bit."""
+    """ray_sensor_kernel at 16 lanes per car in 64- and 128-thread workgroups (the default; walls read from the global
+    image) and 256-, 512- and 1024-thread workgroups (walls staged in LDS; nascar_set_sensor_block), and at 4 lanes
+    per car: the same sensor values on every pose, bit for bit."""
     from nascargymnasium_amd.batched import BatchedCarEnv
     from nascargymnasium_amd.track import build_walls, load_track
     path = os.path.join(TRACKS, "martinsville.track")
     rng = np.random.default_rng(4242)
     poses = _poses(rng, build_walls(load_track(path)), 480 * 10)
     out = {}
-    for rb in ("256", "512", "1024"):
+    for rb in ("64", "128", "256", "512", "1024"):
         env = BatchedCarEnv(480, 10, path, device="cuda:0", envs_per_block=12)   # 120 cars per step workgroup
         env.set_sensor_block(int(rb))
         out[rb] = _device_sensors(env, poses, 1)
-        if rb == "512":
+        if rb == "128":
             env.set_sensor_lanes(4)
             out["lpc4"] = _device_sensors(env, poses, 1)
         env.close()
-    for k in ("256", "1024", "lpc4"):
-        bad = np.argwhere(out[k].view(np.uint32) != out["512"].view(np.uint32))
-        assert len(bad) == 0, f"{k} differs from 512-thread workgroups at {bad[:5].tolist()}"
+    for k in ("64", "256", "512", "1024", "lpc4"):
+        bad = np.argwhere(out[k].view(np.uint32) != out["128"].view(np.uint32))
+        assert len(bad) == 0, f"{k} differs from 128-thread workgroups at {bad[:5].tolist()}"

@@ -242,6 +242,16 @@ def main():
             print(f"  last-ending wave: model half {w[5] - w[0]:.0f} cycles (b2_step {w[4] - w[3]:.0f}), barrier wait "
                   f"{w[6] - w[5]:.0f}, loads + staging {w[7] - w[6]:.0f}, logic_run {w[8] - w[7]:.0f}; model end "
                   f"{(w[15] - rt0) / 100:.1f} us, logic end {(w[9] - rt0) / 100:.1f} us")
+            # logic_run's own stamps (LPROF 1-8, same wave rows) from the logic half's start (PROF 7)
+            lz = logic.copy()
+            lz[:, 0] = np.where((model[:, 7] != 0) & (model[:, 8] != 0), model[:, 7], 0)
+            lr = phases(lz, ["(entry)", "bank / impulse / stuck / lap timer", "barrier + env pass 1 + stuck disable",
+                             "car_obs", "rewards (progress)", "barrier + env pass 2 + barrier + flags", "reset / pose B / state store",
+                             "barrier + obs rows"], 0, "  model_logic_kernel logic_run")
+            if len(lr):
+                j = int(np.argmax(model[:, 9]))
+                if lz[j, 0] and lz[j, 8]:
+                    print("    last-ending wave's logic_run phases:", np.diff(lz[j, :9]).astype(int).tolist())
         phases(logic, LOGIC, 0, "logic_kernel")
         if a.raw:
             live = sens[sens[:, 0] != 0]

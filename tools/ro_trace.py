@@ -13,7 +13,7 @@ import glob
 
 ap = argparse.ArgumentParser()
 ap.add_argument("dir")
-ap.add_argument("--skip", type=int, default=60)
+ap.add_argument("--skip", type=int, default=60, help="shard dispatches to skip (the warm-up call)")
 ap.add_argument("--count", type=int, default=240)
 a = ap.parse_args()
 f = glob.glob(a.dir + "/**/*kernel_trace.csv", recursive=True)[0]
