@@ -26,17 +26,23 @@
 #ifdef NASCAR_PROFILE
 // profile build only: per-wave s_memtime stamps at phase boundaries of step_kernel
 __device__ unsigned long long* g_prof = nullptr;
+// the launch's first workgroup in the whole grid's numbering (the sharded rollout's shards start at Params.blk0), set by
+// every thread of the step and sensor kernels (PROF_B0) before their first stamp, so the shards' stamp rows do not
+// collide; rows are masked into their regions, so a kernel that never sets it still writes in bounds
+__shared__ int s_prof_b0;
+#define PROF_B0(v) (s_prof_b0 = (v))
+#define PROF_BLK ((size_t)((blockIdx.x + (unsigned)s_prof_b0) & 16383u))
 #define PROF(ph) do { unsigned long long _t = __builtin_amdgcn_s_memtime(); \
-    if (g_prof && (threadIdx.x & 63) == 0) g_prof[((size_t)blockIdx.x * (BLOCK / 64) + threadIdx.x / 64) * 16 + (ph)] = _t; } while (0)
+    if (g_prof && (threadIdx.x & 63) == 0) g_prof[(PROF_BLK * (BLOCK / 64) + threadIdx.x / 64) * 16 + (ph)] = _t; } while (0)
 #define PROFS(ph) do { unsigned long long _t = __builtin_amdgcn_s_memtime(); \
-    if (g_prof && (threadIdx.x & 63) == 0) g_prof[(65536 + (size_t)blockIdx.x * (BLOCK / 64) + threadIdx.x / 64) * 16 + (ph)] = _t; } while (0)
+    if (g_prof && (threadIdx.x & 63) == 0) g_prof[(65536 + PROF_BLK * (BLOCK / 64) + threadIdx.x / 64) * 16 + (ph)] = _t; } while (0)
 // ray_sensor_kernel stamps (any block size): rows of the sensor region by blockIdx.x * waves per block + wave
 #define PROFR(ph) do { unsigned long long _t = __builtin_amdgcn_s_memtime(); \
-    if (g_prof && (threadIdx.x & 63) == 0) g_prof[(65536 + (size_t)blockIdx.x * (blockDim.x >> 6) + threadIdx.x / 64) * 16 + (ph)] = _t; } while (0)
+    if (g_prof && (threadIdx.x & 63) == 0) g_prof[(65536 + PROF_BLK * (blockDim.x >> 6) + threadIdx.x / 64) * 16 + (ph)] = _t; } while (0)
 #define PROFR_RT(ph) do { unsigned long long _t = __builtin_amdgcn_s_memrealtime(); \
-    if (g_prof && (threadIdx.x & 63) == 0) g_prof[(65536 + (size_t)blockIdx.x * (blockDim.x >> 6) + threadIdx.x / 64) * 16 + (ph)] = _t; } while (0)
+    if (g_prof && (threadIdx.x & 63) == 0) g_prof[(65536 + PROF_BLK * (blockDim.x >> 6) + threadIdx.x / 64) * 16 + (ph)] = _t; } while (0)
 #define PROFS_RT(ph) do { unsigned long long _t = __builtin_amdgcn_s_memrealtime(); \
-    if (g_prof && (threadIdx.x & 63) == 0) g_prof[(65536 + (size_t)blockIdx.x * (BLOCK / 64) + threadIdx.x / 64) * 16 + (ph)] = _t; } while (0)
+    if (g_prof && (threadIdx.x & 63) == 0) g_prof[(65536 + PROF_BLK * (BLOCK / 64) + threadIdx.x / 64) * 16 + (ph)] = _t; } while (0)
 // event counters: same-address global atomics from every lane serialise (milliseconds per launch), so
 // they have their own build flag and never run in a stamp (timing) build
 #ifdef NASCAR_PROFILE_COUNT
@@ -52,7 +58,7 @@ __device__ unsigned long long* g_prof = nullptr;
 #define PROFU(ph) do { } while (0)
 #endif
 #define PROF_RT(slot) do { unsigned long long _t = __builtin_amdgcn_s_memrealtime(); \
-    if (g_prof && (threadIdx.x & 63) == 0) g_prof[((size_t)blockIdx.x * (BLOCK / 64) + threadIdx.x / 64) * 16 + (slot)] = _t; } while (0)
+    if (g_prof && (threadIdx.x & 63) == 0) g_prof[(PROF_BLK * (BLOCK / 64) + threadIdx.x / 64) * 16 + (slot)] = _t; } while (0)
 // actor_kernel stamps: region after the counters, 16 slots per wave (64-thread waves, any block size)
 #define APROF_BASE (2 * 65536 * 16 + 64)
 #define APROF(ph) do { unsigned long long _t = __builtin_amdgcn_s_memtime(); \
@@ -62,7 +68,7 @@ __device__ unsigned long long* g_prof = nullptr;
 // logic_kernel stamps: region after the actor's (4096 waves x 16 slots)
 #define LPROF_BASE (APROF_BASE + 4096 * 16)
 #define LPROF(ph) do { unsigned long long _t = __builtin_amdgcn_s_memtime(); \
-    if (g_prof && (threadIdx.x & 63) == 0) g_prof[LPROF_BASE + ((size_t)blockIdx.x * (SBLOCK / 64) + threadIdx.x / 64) * 16 + (ph)] = _t; } while (0)
+    if (g_prof && (threadIdx.x & 63) == 0) g_prof[LPROF_BASE + (PROF_BLK * (SBLOCK / 64) + threadIdx.x / 64) * 16 + (ph)] = _t; } while (0)
 // per-car counters of the Box2D step (model_kernel lane of car c.pid, no atomics): region after logic's
 #define CPROF_BASE (LPROF_BASE + 65536 * 16)
 // per-car slots (CPROF_STRIDE per car): non-returning atomics, so a count does not wait on memory (a read-modify-
@@ -81,6 +87,7 @@ __device__ unsigned long long* g_prof = nullptr;
 #define TCAP_BASE (RPROF_BASE + (size_t)65536 * 5)
 #define TCAP_MAX 16384
 #else
+#define PROF_B0(v) do { } while (0)
 #define CCOUNT(c, slot, v) do { } while (0)
 #define CTIME_BEGIN() do { } while (0)
 #define RPROF_ADD(slot, v) do { } while (0)

@@ -668,35 +668,30 @@ __device__ __forceinline__ float screen_d2(const ChordScreen& S, int k, float x,
   const float ex = rx - tt * g.z, ey = ry - tt * g.w;
   return ex * ex + ey * ey;
 }
-// squared screened distance above which a chord cannot be the nearest one
-__device__ inline float screen_cut(const ChordScreen& S, float x, float y) {
-  float m = INFINITY;
-  for (int k = 0; k < S.n; ++k) m = fminf(m, screen_d2(S, k, x, y));
+// The chords that pass the screen, as a bit mask (bit k: chord k; MAX_SEG <= 64): a chord whose squared screened
+// distance exceeds cut = (sqrt(min) + 2 screen_eps)^2 (x 1.0001) cannot be the nearest one.  The first SCREEN_R chords'
+// loads are issued together and their distances kept in registers for the mask (the bundled tracks have 7-9 chords;
+// a loop over the rest).
+#define SCREEN_R 16
+static_assert(MAX_SEG <= 64, "screen_candidates keeps one bit per chord");
+__device__ inline uint64_t screen_candidates(const ChordScreen& S, float x, float y) {
+  float d[SCREEN_R], m = INFINITY;
+#pragma unroll
+  for (int k = 0; k < SCREEN_R; ++k) { d[k] = k < S.n ? screen_d2(S, k, x, y) : INFINITY; m = fminf(m, d[k]); }
+  for (int k = SCREEN_R; k < S.n; ++k) m = fminf(m, screen_d2(S, k, x, y));
   const float r = __builtin_amdgcn_sqrtf(m) + 2.0f * screen_eps(x, y);
-  return r * r * 1.0001f;
+  const float cut = r * r * 1.0001f;
+  uint64_t mask = 0;
+#pragma unroll
+  for (int k = 0; k < SCREEN_R; ++k) if (k < S.n && !(d[k] > cut)) mask |= 1ull << k;
+  for (int k = SCREEN_R; k < S.n; ++k) if (!(screen_d2(S, k, x, y) > cut)) mask |= 1ull << k;
+  return mask;
 }
-// banking_at / track_progress restricted to the chords that pass the screen (same results)
-__device__ inline double banking_at_screened(const TrackDev& T, const ChordScreen& S, float cut, double px, double py) {
-  double best = INFINITY; int bi = -1;
-  for (int k = 0; k < T.nseg; ++k) {
-    if (screen_d2(S, k, (float)px, (float)py) > cut) continue;
-    const DSeg& s = T.segs[k];
-    double ll = P2(s.ex - s.sx) + P2(s.ey - s.sy), d;
-    if (ll == 0) d = sqrt(P2(px - s.sx) + P2(py - s.sy));
-    else {
-      double tt = ((px - s.sx) * (s.ex - s.sx) + (py - s.sy) * (s.ey - s.sy)) / ll;
-      tt = pymax(0.0, pymin(1.0, tt));
-      double qx = s.sx + tt * (s.ex - s.sx), qy = s.sy + tt * (s.ey - s.sy);
-      d = sqrt(P2(px - qx) + P2(py - qy));
-    }
-    if (d < best) { best = d; bi = k; }
-  }
-  return bi >= 0 ? T.segs[bi].banking : 0.0;
-}
-__device__ inline double track_progress_screened(const TrackDev& T, const ChordScreen& S, float cut, double px, double py) {
+// track_progress restricted to the screen's candidate chords (same results: the exact search in index order)
+__device__ inline double track_progress_screened(const TrackDev& T, uint64_t cand, double px, double py) {
   double best = INFINITY; int bi = 0; double bx = 0, by = 0;
-  for (int k = 0; k < T.nseg; ++k) {
-    if (screen_d2(S, k, (float)px, (float)py) > cut) continue;
+  for (uint64_t mk = cand; mk; mk &= mk - 1) {
+    const int k = __builtin_ctzll(mk);
     const DSeg& s = T.segs[k];
     double dx = s.ex - s.sx, dy = s.ey - s.sy, ll = dx * dx + dy * dy, qx, qy;
     if (ll < 1e-6) { qx = s.sx; qy = s.sy; }
@@ -709,6 +704,40 @@ __device__ inline double track_progress_screened(const TrackDev& T, const ChordS
   }
   const DSeg& s = T.segs[bi];
   return T.prefix[bi] + sqrt(P2(bx - s.sx) + P2(by - s.sy));
+}
+// banking_at and track_progress over the candidate chords in one pass (each search's own arithmetic and strict '<' in
+// index order, so the same results; the two chains interleave)
+__device__ inline double bank_and_progress_screened(const TrackDev& T, uint64_t cand, double px, double py, double& prog) {
+  double bbest = INFINITY; int bbi = -1;
+  double pbest = INFINITY; int pbi = 0; double bx = 0, by = 0;
+  for (uint64_t mk = cand; mk; mk &= mk - 1) {
+    const int k = __builtin_ctzll(mk);
+    const DSeg& s = T.segs[k];
+    {   // banking_at
+      double ll = P2(s.ex - s.sx) + P2(s.ey - s.sy), d;
+      if (ll == 0) d = sqrt(P2(px - s.sx) + P2(py - s.sy));
+      else {
+        double tt = ((px - s.sx) * (s.ex - s.sx) + (py - s.sy) * (s.ey - s.sy)) / ll;
+        tt = pymax(0.0, pymin(1.0, tt));
+        double qx = s.sx + tt * (s.ex - s.sx), qy = s.sy + tt * (s.ey - s.sy);
+        d = sqrt(P2(px - qx) + P2(py - qy));
+      }
+      if (d < bbest) { bbest = d; bbi = k; }
+    }
+    {   // track_progress
+      double dx = s.ex - s.sx, dy = s.ey - s.sy, ll = dx * dx + dy * dy, qx, qy;
+      if (ll < 1e-6) { qx = s.sx; qy = s.sy; }
+      else {
+        double tt = pymax(0.0, pymin(1.0, ((px - s.sx) * dx + (py - s.sy) * dy) / ll));
+        qx = s.sx + tt * dx; qy = s.sy + tt * dy;
+      }
+      double d2 = P2(px - qx) + P2(py - qy);
+      if (d2 < pbest) { pbest = d2; pbi = k; bx = qx; by = qy; }
+    }
+  }
+  const DSeg& sp = T.segs[pbi];
+  prog = T.prefix[pbi] + sqrt(P2(bx - sp.sx) + P2(by - sp.sy));
+  return bbi >= 0 ? T.segs[bbi].banking : 0.0;
 }
 // on_startline, decided by the screen unless the screened distance is within screen_eps of width / 2
 __device__ inline bool on_startline_screened(const TrackDev& T, const ChordScreen& S, double px, double py) {
@@ -979,6 +1008,7 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(SENS
                                                                                                         float* terminal_obs, int passes) {
   constexpr int CPW = BLOCK / LPC;          // cars per workgroup
   constexpr int RPL = 16 / LPC;             // rays whose end points / outputs a lane owns
+  PROF_B0(P.blk0 * ((SBLOCK + CPW - 1) / CPW));   // profile builds: stamp rows of the whole grid (launch_sensors_impl's sub)
   PROFS_RT(14);
   PROFS(0);
   __shared__ float s_p2[CPW * 32];          // [car][ray][x, y]: f32 ray end points (exact test)
@@ -1536,6 +1566,7 @@ ray_sensor_kernel(Params P, float* obs, float* terminal_obs, int passes, int SUB
   const int el = slot / C, car = slot - el * C;
   const int env = blk_env_of(P, el, b * P.epb + el);
   const TrackDev& T = P.tracks[blk_track_of(P, b)];
+  PROF_B0(P.blk0 * SUB);   // profile builds: stamp rows numbered over the whole grid (the sharded rollout's shards)
   PROFR_RT(14); PROFR(0);   // profile builds: stamp slots 0-7 (16 lanes per car: ray_lane's 2-6), realtime 14 / 15
   if constexpr (GW) {   // walls read from the track's global image: no staging, no LDS, no barrier
     PROFR(1);
@@ -1611,7 +1642,9 @@ __global__ void policy_kernel(int N, int policy, uint64_t seed, int64_t step, co
 // CarEnv action -> CarPhysics.step for one car whose physics state is loaded in c (src/car_env.py:733-740,
 // src/car_physics.py:341-384): BaseEnv._convert_to_internal_action of (tb, st), Car.update_physics, the
 // Box2D step; writes the model / body state back and the sensor pass-A pose.
-__device__ __forceinline__ void model_car(const Params& P, Car& c, int n, const TrackDev& T, float tb, float st, int want_term) {
+// logic_ahead (model_logic_kernel): the car's lap-timer / bookkeeping fields are requested right after its Box2D step
+__device__ __forceinline__ void model_car(const Params& P, Car& c, int n, const TrackDev& T, float tb, float st, int want_term,
+                                          bool logic_ahead = false) {
   const WallSet S{T.walls, T.nwall, T.bp, T.sn, T.wfat, P.ct};
   float a0, a1, a2 = st;
   if (tb >= 0) { a0 = tb; a1 = 0.0f; } else { a0 = 0.0f; a1 = -tb; }
@@ -1627,6 +1660,7 @@ __device__ __forceinline__ void model_car(const Params& P, Car& c, int n, const 
   PROF(3);
   b2_step(c, S, P.dt_f, P.friction);
   PROF(4);
+  if (logic_ahead) car_load_logic(P, n, c);   // used by the logic half (model_block)
   if (ct_in_lds(c)) {   // model_kernel's LDS records back to the car's global ones (live and dead, see ct_make_room)
     DContact* g = P.ct + (size_t)n * MAXC;
     for (int i = 0; i < c.ct_hw; ++i) g[i] = c.ct[i];
@@ -1652,16 +1686,31 @@ __device__ __forceinline__ void model_car(const Params& P, Car& c, int n, const 
 // current obs instead of the actions buffer -- the closed-loop driver's step without a policy_kernel launch.
 // Every thread of the block calls it (it holds the segment staging barrier); lanes without a car (env < 0) skip
 // the step (model_kernel: they return; FUSED, the model_logic_kernel, keeps them for the barriers after it).
+// FUSED (model_logic_kernel): the car's lap-timer / bookkeeping fields (car_load_logic) are requested right after its
+// Box2D step (held across it they spilled) and kept in c for the logic half, which continues from c (its body fields
+// are the ones car_store_body writes) instead of reloading them: the slowest wave's logic half no longer starts with
+// a memory round trip.
+// the track's segments, staged in LDS by the step kernels' model half (model_logic_kernel's logic half reads them too)
+__shared__ DSeg g_step_segs[MAX_SEG];
+// one segment's logic tables (chord prefix sum, f32 chord screen), held in registers by lane tid = segment from the
+// model half's staging to the logic half's (no global round trip there)
+struct SegReg { double prefix; float4 sg; float rll; };
+__device__ __forceinline__ void seg_tables(const DSeg& sg, double prefix, SegReg& r) {   // as stage_track_lds
+  r.prefix = prefix;
+  const double dx = sg.ex - sg.sx, dy = sg.ey - sg.sy, ll = dx * dx + dy * dy;
+  r.sg = make_float4((float)sg.sx, (float)sg.sy, (float)dx, (float)dy);
+  r.rll = ll < 1e-6 ? 0.0f : (float)(1.0 / ll);
+}
 template <bool FUSED>
 __device__ __forceinline__ void model_block(const Params& P, const void* actions, int discrete, int want_term, int policy,
-                                            uint64_t seed, int64_t step, const float* pobs, int tid, int env, int n) {
+                                            uint64_t seed, int64_t step, const float* pobs, int tid, int env, int n, Car& c,
+                                            SegReg& sr) {
+  PROF_B0(P.blk0);   // profile builds: stamp rows numbered over the whole grid (the sharded rollout's shards)
   PROF_RT(14);
   PROF(0);
 #if MODEL_PRIO == 1   // A/B: model_kernel's waves issue ahead of co-resident logic / sensor waves of other shards
   __builtin_amdgcn_s_setprio(2);
 #endif
-  __shared__ DSeg s_segs[MAX_SEG];
-  Car c;
   // car state and action requested before the segment staging barrier (their round trips overlap the
   // staging's instead of following it: 89 -> 84 us per step)
   if (env >= 0) car_load_phys(P, n, c);
@@ -1690,14 +1739,18 @@ __device__ __forceinline__ void model_block(const Params& P, const void* actions
     }
   }
   TrackDev T = P.tracks[blk_track_of(P, (blockIdx.x + P.blk0))];
-  if (tid < T.nseg) s_segs[tid] = ldg(T.segs + tid);
+  if (tid < T.nseg) {
+    const DSeg sg = ldg(T.segs + tid);
+    g_step_segs[tid] = sg;
+    if (FUSED) seg_tables(sg, ldg(T.prefix + tid), sr);
+  }
   __syncthreads();
-  T.segs = s_segs;   // (the wall table stays global: staged in LDS it measured neutral, and the LDS holds the contacts)
+  T.segs = g_step_segs;   // (the wall table stays global: staged in LDS it measured neutral, and the LDS holds the contacts)
   PROF(1);
   if (!FUSED && env < 0) return;
   if (env >= 0) {
     PROF(2);
-    model_car(P, c, n, T, tb, st, want_term);
+    model_car(P, c, n, T, tb, st, want_term, FUSED);
     PROF(5);
     PROF_RT(15);
   }
@@ -1708,7 +1761,9 @@ __global__ void __launch_bounds__(SBLOCK) __attribute__((amdgpu_waves_per_eu(MOD
   const int el = tid / C, car = tid - el * C;
   const int slot = (blockIdx.x + P.blk0) * P.epb + el;
   const int env = blk_env_of(P, el, slot);
-  model_block<false>(P, actions, discrete, want_term, policy, seed, step, pobs, tid, env, env >= 0 ? env * C + car : 0);
+  Car c;
+  SegReg sr;
+  model_block<false>(P, actions, discrete, want_term, policy, seed, step, pobs, tid, env, env >= 0 ? env * C + car : 0, c, sr);
 }
 
 // logic_kernel's shared memory: env reductions and the coalesced obs[:, 0:22] row store
@@ -1731,13 +1786,9 @@ __device__ __forceinline__ void stage_track_lds(const TrackDev& T, TrackLDS& TL,
 }
 // logic state of car n (body from model_kernel, lap timer / bookkeeping, tyres) and its env's time / pending /
 // reason words (read by car 0's lane in the env passes)
-__device__ __forceinline__ void logic_load(const Params& P, int env, int car, int n, Car& c, double& sim, int& pend_in,
-                                           int& reason_in) {
+__device__ __forceinline__ void logic_load_env(const Params& P, int env, int car, double& sim, int& pend_in, int& reason_in) {
   sim = 0.0; pend_in = 0; reason_in = 0;
   if (env >= 0) {
-    car_load_body(P, n, c);
-    car_load_logic(P, n, c);
-    car_reload_tyres(P, n, c);
     if (car == 0) {   // reason_in bit 8: the env was never reset (E_CREATED == 0)
       pend_in = P.env_i32[E_PENDING * P.E + env];
       reason_in = P.env_i32[E_REASON * P.E + env] | (P.env_i32[E_CREATED * P.E + env] == 0 ? 0x100 : 0);
@@ -1745,6 +1796,32 @@ __device__ __forceinline__ void logic_load(const Params& P, int env, int car, in
     sim = P.env_time[env];
   }
 }
+__device__ __forceinline__ void logic_load(const Params& P, int env, int car, int n, Car& c, double& sim, int& pend_in,
+                                           int& reason_in) {
+  if (env >= 0) {
+    car_load_body(P, n, c);
+    car_load_logic(P, n, c);
+    car_reload_tyres(P, n, c);
+  }
+  logic_load_env(P, env, car, sim, pend_in, reason_in);
+}
+// model_logic_kernel: the logic half continues from the model half's c (body fields as car_store_body stored them,
+// logic fields requested at the start, see model_block), with car_load_body's derived fields and global list pointers
+__device__ __forceinline__ void logic_from_model(const Params& P, int n, Car& c) {
+  car_reload_tyres(P, n, c);   // (written back before the Box2D step, not held across it)
+  if (P.car_contact) {         // car_contact_block rewrote velocities / impulses in the arena: reload the body
+    car_load_body(P, n, c);
+    return;
+  }
+  c.just_disabled = 0;
+  c.force = zero2(); c.torque = 0.0f; c.c0 = c.c; c.a0 = c.a; c.alpha0 = 0.0f; c.moved = 0;
+  c.ct = P.ct + (size_t)n * MAXC; c.act_key = P.act_key + (size_t)n * MAXC; c.act_n = P.act_n + (size_t)n * MAXC * 2;
+  c.acc = nullptr;
+}
+#ifndef LOGIC_OBS_LDS
+#define LOGIC_OBS_LDS 0   // 1: obs[:, 0:22] rows staged in LDS and stored coalesced after a barrier; 0: each lane stores
+                          // its row's 88 bytes directly (round 5, per-shard model_logic_kernel 103.8 -> 102.5 us)
+#endif
 // the rest of the env step for one block (every thread calls it; it holds block barriers): banking, impulse /
 // stuck / backward disable, lap timer, env pass 1, obs[0:22], rewards, env pass 2 (termination), auto-reset
 // (sensor pass-B pose), state write-back, coalesced obs rows.  T.segs / T.prefix point at TL.
@@ -1754,7 +1831,7 @@ __device__ __forceinline__ void logic_run(const Params& P, const TrackDev& T, co
                                           float* terminal_obs) {
   const int C = P.C;
   const ChordScreen CS{TL.sg, TL.rll, T.nseg};
-  float cut = INFINITY;
+  double prog_now = 0.0;   // track_progress at the step's final body position
   const int nw = T.nwall;
   const WallSet S{T.walls, nw, T.bp, T.sn, T.wfat};
   bool lapdone = false;
@@ -1762,8 +1839,10 @@ __device__ __forceinline__ void logic_run(const Params& P, const TrackDev& T, co
     L.dis_old[tid] = c.disabled;
     LPROF(1);
     L.laps_old[tid] = c.lt_laps;   // the lap count does not change before lap_update
-    cut = screen_cut(CS, c.xf.p.x, c.xf.p.y);   // the body position is final for this step
-    c.bank = T.has_banking ? banking_at_screened(T, CS, cut, c.xf.p.x, c.xf.p.y) : 0.0;
+    const uint64_t cand = screen_candidates(CS, c.xf.p.x, c.xf.p.y);   // the body position is final for this step
+    // the banking and the track progress (the rewards' _calculate_multi_rewards needs it below) in one chord pass
+    if (T.has_banking) c.bank = bank_and_progress_screened(T, cand, c.xf.p.x, c.xf.p.y, prog_now);
+    else { c.bank = 0.0; prog_now = track_progress_screened(T, cand, c.xf.p.x, c.xf.p.y); }
     if (!c.disabled) {   // _run_single_physics_step (src/car_env.py:582-638)
       double imp = c.imp_present ? c.imp : 0.0;
       if (imp > 50000.0) { c.disabled = 1; c.just_disabled = 1; }
@@ -1834,7 +1913,7 @@ __device__ __forceinline__ void logic_run(const Params& P, const TrackDev& T, co
       r += PH(P2(dx) + P2(dy)) * 0.15;
       c.prev_px = px; c.prev_py = py;
       if (!c.first_step) {
-        double prog = track_progress_screened(T, CS, cut, px, py);
+        double prog = prog_now;
         double L = T.total_length, pd = prog - c.prog_hist;
         if (pd > L / 2) pd -= L; else if (pd < -L / 2) pd += L;
         if (pd < 0) {
@@ -1848,7 +1927,7 @@ __device__ __forceinline__ void logic_run(const Params& P, const TrackDev& T, co
         } else { c.back = 0.0; c.prev_back = 0.0; }
         c.prog_hist = prog;
       } else {
-        c.prog_hist = track_progress_screened(T, CS, cut, px, py);
+        c.prog_hist = prog_now;
         c.first_step = 0;
       }
       if (c.lt_laps > c.prev_laps) { r += 0.0 * (c.lt_laps - c.prev_laps); c.prev_laps = c.lt_laps; }
@@ -1910,7 +1989,11 @@ __device__ __forceinline__ void logic_run(const Params& P, const TrackDev& T, co
     } else {
       P.pose[P.N + n] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
+#if LOGIC_OBS_LDS
     for (int i = 0; i < 22; ++i) L.obs[tid * 22 + i] = o[i];
+#else   // (A/B) the lane's 88 bytes of obs[n, 0:22] stored directly (8-byte aligned rows: 11 float2 stores)
+    for (int i = 0; i < 22; i += 2) *(float2*)(obs + (size_t)n * 38 + i) = make_float2(o[i], o[i + 1]);
+#endif
     if (reset_now) car_store(P, n, c);    // car_reset rewrote every field
     else car_store_logic(P, n, c);
     LPROF(7);
@@ -1921,6 +2004,7 @@ __device__ __forceinline__ void logic_run(const Params& P, const TrackDev& T, co
       P.env_i32[E_TERMINATED * P.E + env] = 0; P.env_i32[E_TRUNCATED * P.E + env] = 0;
     }
   }
+#if LOGIC_OBS_LDS
   L.rowbase[tid] = env >= 0 ? n * 38 : -1;
   __syncthreads();
   // obs[:, 0:22] rows of this workgroup, written 22 consecutive floats per row by consecutive lanes
@@ -1931,6 +2015,7 @@ __device__ __forceinline__ void logic_run(const Params& P, const TrackDev& T, co
     const int base = L.rowbase[row];
     if (base >= 0) obs[(size_t)base + col] = L.obs[i];
   }
+#endif
   LPROF(8);}
 
 // ------------------------------------------------------------------ car-car contact (build-only extension)
@@ -2015,6 +2100,7 @@ __global__ void __launch_bounds__(SBLOCK) LOGIC_ATTR logic_kernel(Params P, floa
   const int slot = (blockIdx.x + P.blk0) * P.epb + el;
   const int env = blk_env_of(P, el, slot);
   const int n = env >= 0 ? env * C + car : 0;
+  PROF_B0(P.blk0);
   LPROF(0);
   Car c;
   double sim;
@@ -2044,17 +2130,15 @@ __attribute__((noinline))
 __forceinline__
 #endif
 static __device__ void fused_logic_phase(const Params& P, int tid, int el, int car, int env, int n, float* obs, float* reward,
-                                         uint8_t* car_flags, uint8_t* env_flags, int auto_reset, float* terminal_obs) {
+                                         uint8_t* car_flags, uint8_t* env_flags, int auto_reset, float* terminal_obs,
+                                         Car& c, double sim, int pend_in, int reason_in, const SegReg& sr) {
   FusedLogicLDS& F = *(FusedLogicLDS*)smem;
-  Car c;
-  double sim;
-  int pend_in, reason_in;
-  logic_load(P, env, car, n, c, sim, pend_in, reason_in);
+  if (env >= 0) logic_from_model(P, n, c);
   TrackDev T = P.tracks[blk_track_of(P, (blockIdx.x + P.blk0))];
-  stage_track_lds(T, F.TL, tid);
+  if (tid < T.nseg) { F.TL.prefix[tid] = sr.prefix; F.TL.sg[tid] = sr.sg; F.TL.rll[tid] = sr.rll; }   // (model half's loads)
   __syncthreads();
   PROF(7);
-  T.segs = F.TL.segs; T.prefix = F.TL.prefix;
+  T.segs = g_step_segs; T.prefix = F.TL.prefix;   // the segments the model half staged (static LDS, still there)
   logic_run(P, T, F.TL, F.L, tid, el, car, env, n, c, sim, pend_in, reason_in, obs, reward, car_flags, env_flags, auto_reset,
             terminal_obs);
 }
@@ -2068,11 +2152,17 @@ model_logic_kernel(Params P, const void* actions, int discrete, int want_term, i
   const int slot = (blockIdx.x + P.blk0) * P.epb + el;
   const int env = blk_env_of(P, el, slot);
   const int n = env >= 0 ? env * C + car : 0;
-  model_block<true>(P, actions, discrete, want_term, policy, seed, step, pobs, tid, env, n);
+  Car c;
+  SegReg sr;
+  double sim;
+  int pend_in, reason_in;
+  logic_load_env(P, env, car, sim, pend_in, reason_in);
+  model_block<true>(P, actions, discrete, want_term, policy, seed, step, pobs, tid, env, n, c, sr);
   __syncthreads();   // the block's Box2D steps done: body state stored, contact slots written back (LDS free)
   PROF(6);           // profile builds: the fused kernel's logic half (stamp slots 6-9)
   if (P.car_contact) car_contact_block(P, tid, el, car, env, n);   // block-uniform; holds its own barrier
-  fused_logic_phase(P, tid, el, car, env, n, obs, reward, car_flags, env_flags, auto_reset, terminal_obs);
+  fused_logic_phase(P, tid, el, car, env, n, obs, reward, car_flags, env_flags, auto_reset, terminal_obs, c, sim, pend_in,
+                    reason_in, sr);
   PROF(8);
   PROF_RT(9);
 }
@@ -2149,6 +2239,7 @@ rollout_kernel(const Params* __restrict__ Pg, int K, int policy, uint64_t seed, 
                uint8_t* car_flags, uint8_t* env_flags, int auto_reset, int traj) {
   ParamsK Pk = (ParamsK)Pg;   // global -> constant address space (same addresses)
   const Params& P = *Pg;
+  PROF_B0(0);
   {
     const TrackDev T = P.tracks[blk_track_of(P, blockIdx.x)];
     stage_track_lds(T, g_ro_track, threadIdx.x);

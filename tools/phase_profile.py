@@ -43,6 +43,39 @@ def phases(rows, names, first, title, extra=""):
     return rows
 
 
+def shard_timeline(model, sens, env, a):
+    """per shard of the sharded rollout (workgroups [nb*s/S, nb*(s+1)/S)): realtime of its model_logic_kernel (start,
+    model half end, logic end) and ray_sensor_kernel waves, from the first stamp of any shard (us), and the sensor
+    waves' phase cycles"""
+    S = env.rollout_streams
+    cpb = (128 // a.cars) * a.cars                    # cars per step workgroup
+    nb = -(-a.envs * a.cars // cpb)
+    sub = 15 if cpb == 120 else None                  # 128-thread sensor workgroups: 8 cars each
+    if sub is None:
+        print("shard timeline: only for 120 cars per step workgroup")
+        return
+    t0 = min(model[model[:, 14] != 0, 14].min(), sens[sens[:, 14] != 0, 14].min())
+    us = lambda v: (v - t0) / 100
+    names = ["(staging)", "pose load", "beam cell lookup", "ray end point (f64)", "list head load", "walk", "store"]
+    print(f"sharded rollout timeline (last step of the call; us from the first stamp; {S} shards of ~{nb // S} workgroups):")
+    for s in range(S):
+        b0, b1 = nb * s // S, nb * (s + 1) // S
+        m = model[4 * b0:4 * b1]
+        m = m[(m[:, 14] != 0) & (m[:, 9] != 0)].astype(np.float64)
+        r = sens[2 * b0 * sub:2 * b1 * sub]
+        r = r[(r[:, 14] != 0) & (r[:, 15] != 0)].astype(np.float64)
+        if not len(m) or not len(r):
+            print(f"  shard {s}: no stamps")
+            continue
+        d = np.diff(r[:, 0:8], axis=1)
+        print(f"  shard {s}: model_logic start {us(m[:, 14].min()):7.1f} model-half end p50 {us(np.median(m[:, 15])):7.1f} "
+              f"last {us(m[:, 15].max()):7.1f}, logic end last {us(m[:, 9].max()):7.1f} | sensor waves {len(r)}: first start "
+              f"{us(r[:, 14].min()):7.1f} p50 start {us(np.median(r[:, 14])):7.1f} last start {us(r[:, 14].max()):7.1f} "
+              f"p50 end {us(np.median(r[:, 15])):7.1f} last end {us(r[:, 15].max()):7.1f}; wave us p50 "
+              f"{np.median(r[:, 15] - r[:, 14]) / 100:.1f}")
+        print("    sensor wave cycles (mean): " + ", ".join(f"{nm} {d[:, k].mean():.0f}" for k, nm in enumerate(names)))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--envs", type=int, default=8192)
@@ -61,6 +94,9 @@ def main():
                     "(per-wave phase cycles per step: model, logic, sensors, each up to its block barrier)")
     ap.add_argument("--capture", default=None, help="library built with -DNASCAR_TOI_CAPTURE: save every computed TOI job's "
                     "inputs (float32 [n, 16]: car sweep c0.xy c.xy, a0 a alpha0 -, wall px py qs qc hx hy ang key) to this .npy")
+    ap.add_argument("--sharded", type=int, default=0, help="step through the sharded rollout (nascar_rollout, R steps per "
+                    "profiled call, policy 3) instead of launch_step; the stamps are the last step's, and a per-shard "
+                    "timeline (model / logic / sensor realtime) is printed")
     ap.add_argument("--two-kernel", action="store_true", help="step through model_kernel + logic_kernel (the logic "
                     "kernel's own stamps) instead of the fused model_logic_kernel")
     ap.add_argument("--count", action="store_true", help="library built with -DNASCAR_PROFILE_COUNT (sensor event "
@@ -107,7 +143,10 @@ def main():
         acts = actions(k0 + a.warmup + s)
         buf.zero_()
         torch.cuda.synchronize()
-        env.launch_step(acts, auto_reset=True)
+        if a.sharded:
+            env.rollout(3, a.sharded, seed=0, step0=k0 + a.warmup + s * a.sharded)
+        else:
+            env.launch_step(acts, auto_reset=True)
         torch.cuda.synchronize()
         b = buf.cpu().numpy()
         if a.capture:   # -DNASCAR_TOI_CAPTURE builds: this step's b2TimeOfImpact jobs (sweep s0, s1, wall record)
@@ -280,6 +319,8 @@ def main():
             w = rs[np.argmax(rs[:, 15])]
             print("  last-ending wave: " + ", ".join(f"{nm} {w[k + 1] - w[k]:.0f}" for k, nm in enumerate(names)))
         phases(sens, SENSOR, 0, "sensor_kernel", extra)
+        if a.sharded and len(rs):
+            shard_timeline(model, sens, env, a)
         cb = b[2 * NW * 16 + 8:2 * NW * 16 + 16]
         if cb[4] or cb[5] or cb[6]:
             ncar = a.envs * a.cars
