@@ -39,6 +39,11 @@ __shared__ int s_prof_b0;
 // ray_sensor_kernel stamps (any block size): rows of the sensor region by blockIdx.x * waves per block + wave
 #define PROFR(ph) do { unsigned long long _t = __builtin_amdgcn_s_memtime(); \
     if (g_prof && (threadIdx.x & 63) == 0) g_prof[(65536 + PROF_BLK * (blockDim.x >> 6) + threadIdx.x / 64) * 16 + (ph)] = _t; } while (0)
+// the wave's XCD (HW_REG_XCC_ID, 1-based so 0 = unstamped) into stamp slot ph of the model / sensor rows
+#define PROF_XCC(ph) do { const unsigned long long _x = (__builtin_amdgcn_s_getreg((3 << 11) | 20) & 15) + 1; \
+    if (g_prof && (threadIdx.x & 63) == 0) g_prof[(PROF_BLK * (BLOCK / 64) + threadIdx.x / 64) * 16 + (ph)] = _x; } while (0)
+#define PROFR_XCC(ph) do { const unsigned long long _x = (__builtin_amdgcn_s_getreg((3 << 11) | 20) & 15) + 1; \
+    if (g_prof && (threadIdx.x & 63) == 0) g_prof[(65536 + PROF_BLK * (blockDim.x >> 6) + threadIdx.x / 64) * 16 + (ph)] = _x; } while (0)
 #define PROFR_RT(ph) do { unsigned long long _t = __builtin_amdgcn_s_memrealtime(); \
     if (g_prof && (threadIdx.x & 63) == 0) g_prof[(65536 + PROF_BLK * (blockDim.x >> 6) + threadIdx.x / 64) * 16 + (ph)] = _t; } while (0)
 #define PROFS_RT(ph) do { unsigned long long _t = __builtin_amdgcn_s_memrealtime(); \
@@ -95,6 +100,8 @@ __shared__ int s_prof_b0;
 #define PROF(ph) do { } while (0)
 #define PROFS(ph) do { } while (0)
 #define PROFR(ph) do { } while (0)
+#define PROF_XCC(ph) do { } while (0)
+#define PROFR_XCC(ph) do { } while (0)
 #define PROFR_RT(ph) do { } while (0)
 #define PROFS_RT(ph) do { } while (0)
 #define PROFB(ph) do { } while (0)

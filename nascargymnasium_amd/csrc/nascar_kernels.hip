@@ -1567,7 +1567,7 @@ ray_sensor_kernel(Params P, float* obs, float* terminal_obs, int passes, int SUB
   const int env = blk_env_of(P, el, b * P.epb + el);
   const TrackDev& T = P.tracks[blk_track_of(P, b)];
   PROF_B0(P.blk0 * SUB);   // profile builds: stamp rows numbered over the whole grid (the sharded rollout's shards)
-  PROFR_RT(14); PROFR(0);   // profile builds: stamp slots 0-7 (16 lanes per car: ray_lane's 2-6), realtime 14 / 15
+  PROFR_RT(14); PROFR(0); PROFR_XCC(8);   // profile builds: stamp slots 0-7 (16 lanes per car: ray_lane's 2-6), realtime 14 / 15
   if constexpr (GW) {   // walls read from the track's global image: no staging, no LDS, no barrier
     PROFR(1);
     if (env < 0) return;
@@ -1707,6 +1707,7 @@ __device__ __forceinline__ void model_block(const Params& P, const void* actions
                                             SegReg& sr) {
   PROF_B0(P.blk0);   // profile builds: stamp rows numbered over the whole grid (the sharded rollout's shards)
   PROF_RT(14);
+  PROF_XCC(10);
   PROF(0);
 #if MODEL_PRIO == 1   // A/B: model_kernel's waves issue ahead of co-resident logic / sensor waves of other shards
   __builtin_amdgcn_s_setprio(2);

@@ -74,6 +74,16 @@ def shard_timeline(model, sens, env, a):
               f"p50 end {us(np.median(r[:, 15])):7.1f} last end {us(r[:, 15].max()):7.1f}; wave us p50 "
               f"{np.median(r[:, 15] - r[:, 14]) / 100:.1f}")
         print("    sensor wave cycles (mean): " + ", ".join(f"{nm} {d[:, k].mean():.0f}" for k, nm in enumerate(names)))
+        # XCD placement (profile slot 10 of the model rows, 8 of the sensor rows: HW_REG_XCC_ID + 1): the rotation
+        # (xcc - launch-local block) mod 8 of each dispatch, and how many sensor waves run on their cars' model XCD
+        mx = model[4 * b0:4 * b1, 10].reshape(-1, 4)[:, 0].astype(np.int64)
+        rx = sens[2 * b0 * sub:2 * b1 * sub, 8].reshape(-1, 2)[:, 0].astype(np.int64)
+        if (mx > 0).all() and (rx > 0).all():
+            mo = np.bincount((mx - 1 - np.arange(len(mx))) % 8, minlength=8)
+            ro = np.bincount((rx - 1 - np.arange(len(rx))) % 8, minlength=8)
+            same = (rx - 1 == np.repeat(mx - 1, sub)[:len(rx)]).mean()
+            print(f"    XCD rotation (xcc - block) mod 8: model {mo.tolist()}, sensor {ro.tolist()}; sensor workgroups on "
+                  f"their cars' model XCD {100 * same:.0f} %")
 
 
 def main():
