@@ -1,5 +1,5 @@
 #!/bin/bash
-# round 5 A/B session: per-kernel mean durations from one saved steady state (tools/kt_ss.sh, KT_LIBS), the driver's
+# A/B session: per-kernel mean durations from one saved steady state (tools/kt_ss.sh, KT_LIBS), the driver's
 # command alternated over libraries (tools/ab3.sh, AB3_LIBS, ROUNDS), the driver's command at S env shards on S hardware
 # queues (QUEUES="4 6 8", ROUNDS), a kernel-trace timeline of the sharded rollout (TRACE=1, tools/ro_trace.sh), then GPU
 # tests (TESTS, pytest paths/args).
