@@ -93,13 +93,14 @@ def test_cfg2_one_car_layouts_vs_oracle():
 
 
 @pytest.mark.timeout(600)
-def test_cfg3_car_contact_at_talladega_10_cars():
-    """cfg3's extension at its shape (talladega, 10 cars per env -- a 5-row start grid -- 256 envs): impulses are
-    reported, the sharded rollout equals the per-step path bit for bit with contact on, and with contact off again
-    the engine equals a reference-behaviour engine started from the same state."""
+@pytest.mark.parametrize("E", [256, 8192])
+def test_cfg3_car_contact_at_talladega_10_cars(E):
+    """cfg3's extension (talladega, 10 cars per env -- a 5-row start grid), at 256 envs and at cfg3's own 8192: impulses
+    are reported, the sharded rollout (4 shards at 8192) equals the per-step path bit for bit with contact on, and with
+    contact off again the engine equals a reference-behaviour engine started from the same state."""
     from nascargymnasium_amd.batched import BatchedCarEnv
     from nascargymnasium_amd import _lib
-    E, C = 256, 10
+    C = 10
     path = os.path.join(TRACKS, "talladega.track")
     F = _lib.INFO_INDEX
     env = BatchedCarEnv(E, C, path, device="cuda:0")
