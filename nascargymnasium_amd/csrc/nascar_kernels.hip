@@ -953,6 +953,12 @@ __device__ __forceinline__ V2 ray_end(const Params& P, double px, double py, dou
   ray_end_f32(px, py, ang, c0, s0, i, (const double (*)[2])P.ray_cs, dx, dy, fx, fy);
   return V(fx, fy);
 }
+__device__ __forceinline__ V2 ray_end_k(double px, double py, double ang, double c0, double s0, int i, double2 rk,
+                                        double& dx, double& dy) {   // rk = ray_cs[i], loaded by the caller
+  float fx, fy;
+  ray_end_f32_k(px, py, ang, c0, s0, i, rk.x, rk.y, dx, dy, fx, fy);
+  return V(fx, fy);
+}
 
 // rays (pi/8 apart, ray i along ang - i*pi/8) that can meet a circle (center r from the car, radius R)
 __device__ __forceinline__ unsigned ray_mask(float rx, float ry, float d, float R, float angf) {
@@ -1374,6 +1380,8 @@ __device__ __forceinline__ void ray_lane(const Params& P, const TrackDev& T, con
   // lookup too, measured 2.5 / 9 us slower (registers held across the staging)
   // each pass loads its own pose (pass B's only for auto-reset cars): no pose is held across the other pass's
   // walks (held, both had been spilled to scratch at 80 VGPRs); pass B's mode word is read up front
+  // one ray per lane: its offset's cos / sin requested first, beside the pose loads (not behind the cell lookup)
+  const double2 rk = LPC == 16 ? ldg((const double2*)P.ray_cs + r) : make_double2(0.0, 0.0);
   int mode = 0;
   if (passes & 2) mode = __float_as_int(P.pose[P.N + n].w) & PM_B_OBS;
   const BeamGrid G = T.beam;
@@ -1421,7 +1429,8 @@ __device__ __forceinline__ void ray_lane(const Params& P, const TrackDev& T, con
       double dxd, dyd;
       float fx = ps.x, fy = ps.y, fa = ps.z;   // widened per ray: three floats live across the walks, not three doubles
       asm volatile("" : "+v"(fx), "+v"(fy), "+v"(fa));
-      const V2 p2 = ray_end(P, (double)fx, (double)fy, (double)fa, cs.x, cs.y, i, dxd, dyd);
+      const V2 p2 = LPC == 16 ? ray_end_k((double)fx, (double)fy, (double)fa, cs.x, cs.y, i, rk, dxd, dyd)
+                              : ray_end(P, (double)fx, (double)fy, (double)fa, cs.x, cs.y, i, dxd, dyd);
       const float dx = (p2.x - p1.x) * 0.004f, dy = (p2.y - p1.y) * 0.004f;   // cull only
       float bi = 2.0f;
       if (base >= 0) {
@@ -1767,12 +1776,10 @@ __global__ void __launch_bounds__(SBLOCK) __attribute__((amdgpu_waves_per_eu(MOD
   model_block<false>(P, actions, discrete, want_term, policy, seed, step, pobs, tid, env, env >= 0 ? env * C + car : 0, c, sr);
 }
 
-// logic_kernel's shared memory: env reductions and the coalesced obs[:, 0:22] row store
+// logic_kernel's shared memory: the env passes' per-car words
 struct LogicLDS {
   int laps_old[SBLOCK], dis_old[SBLOCK], laps_new[SBLOCK], dis_new[SBLOCK], lapdone[SBLOCK];
   int dis_final[SBLOCK], below[SBLOCK], envdone[SBLOCK];
-  float obs[SBLOCK * 22];
-  int rowbase[SBLOCK];
 };
 // the block's track segments in LDS (f64 segments, chord prefix sums, f32 chord screens)
 struct TrackLDS { DSeg segs[MAX_SEG]; double prefix[MAX_SEG]; float4 sg[MAX_SEG]; float rll[MAX_SEG]; };
@@ -1819,10 +1826,6 @@ __device__ __forceinline__ void logic_from_model(const Params& P, int n, Car& c)
   c.ct = P.ct + (size_t)n * MAXC; c.act_key = P.act_key + (size_t)n * MAXC; c.act_n = P.act_n + (size_t)n * MAXC * 2;
   c.acc = nullptr;
 }
-#ifndef LOGIC_OBS_LDS
-#define LOGIC_OBS_LDS 0   // 1: obs[:, 0:22] rows staged in LDS and stored coalesced after a barrier; 0: each lane stores
-                          // its row's 88 bytes directly (round 5, per-shard model_logic_kernel 103.8 -> 102.5 us)
-#endif
 // the rest of the env step for one block (every thread calls it; it holds block barriers): banking, impulse /
 // stuck / backward disable, lap timer, env pass 1, obs[0:22], rewards, env pass 2 (termination), auto-reset
 // (sensor pass-B pose), state write-back, coalesced obs rows.  T.segs / T.prefix point at TL.
@@ -1945,7 +1948,15 @@ __device__ __forceinline__ void logic_run(const Params& P, const TrackDev& T, co
     const double st = sim + P.dt_d;   // env_time is written only here
     P.env_time[env] = st;
     int ndis = 0, active = 0, below = 0, term = 0, trunc = 0, reason = reason_in & 0xFF;
-    for (int j = 0; j < C; ++j) { ndis += L.dis_final[tid + j]; if (!L.dis_final[tid + j]) { active++; below += L.below[tid + j]; } }
+    for (int j0 = 0; j0 < C; j0 += 8) {   // 8 cars' words requested together per round
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        if (j0 + u >= C) break;
+        const int d = L.dis_final[tid + j0 + u], b = L.below[tid + j0 + u];
+        ndis += d;
+        if (!d) { active++; below += b; }
+      }
+    }
     if (ndis >= C) { term = 1; reason = 1; }
     else if (active > 0 && below == active) { term = 1; reason = 2; }
     else if (P.reset_on_lap && st > 60.0) { term = 1; reason = 3; }
@@ -1990,11 +2001,9 @@ __device__ __forceinline__ void logic_run(const Params& P, const TrackDev& T, co
     } else {
       P.pose[P.N + n] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
-#if LOGIC_OBS_LDS
-    for (int i = 0; i < 22; ++i) L.obs[tid * 22 + i] = o[i];
-#else   // (A/B) the lane's 88 bytes of obs[n, 0:22] stored directly (8-byte aligned rows: 11 float2 stores)
+    // the lane's 88 bytes of obs[n, 0:22], stored directly (8-byte aligned rows: 11 float2 stores; staging the block's
+    // rows in LDS for coalesced stores cost a barrier: per-shard model_logic_kernel 103.8 -> 102.5 us without it)
     for (int i = 0; i < 22; i += 2) *(float2*)(obs + (size_t)n * 38 + i) = make_float2(o[i], o[i + 1]);
-#endif
     if (reset_now) car_store(P, n, c);    // car_reset rewrote every field
     else car_store_logic(P, n, c);
     LPROF(7);
@@ -2005,18 +2014,6 @@ __device__ __forceinline__ void logic_run(const Params& P, const TrackDev& T, co
       P.env_i32[E_TERMINATED * P.E + env] = 0; P.env_i32[E_TRUNCATED * P.E + env] = 0;
     }
   }
-#if LOGIC_OBS_LDS
-  L.rowbase[tid] = env >= 0 ? n * 38 : -1;
-  __syncthreads();
-  // obs[:, 0:22] rows of this workgroup, written 22 consecutive floats per row by consecutive lanes
-#pragma unroll
-  for (int k = 0; k < 22; ++k) {   // unrolled: the 22 LDS reads are issued back to back
-    const int i = tid + k * SBLOCK;
-    const int row = i / 22, col = i - row * 22;
-    const int base = L.rowbase[row];
-    if (base >= 0) obs[(size_t)base + col] = L.obs[i];
-  }
-#endif
   LPROF(8);}
 
 // ------------------------------------------------------------------ car-car contact (build-only extension)

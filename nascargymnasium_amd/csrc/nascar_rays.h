@@ -41,13 +41,13 @@ __host__ __device__ __attribute__((noinline)) inline void ray_end_direct(double 
   fx = (float)(px + ex * 250.0);
   fy = (float)(py + ey * 250.0);
 }
-__host__ __device__ inline int ray_end_f32(double px, double py, double ang, double c0, double s0, int i,
-                                           const double (*cs)[2], double& dx, double& dy, float& fx, float& fy) {
+// (ck, sk) = cs[i]: the ray offset's cos / sin from the table, passed in so a caller can request it early
+__host__ __device__ inline int ray_end_f32_k(double px, double py, double ang, double c0, double s0, int i, double ck,
+                                             double sk, double& dx, double& dy, float& fx, float& fy) {
   const double k = (double)i * (360.0 / 16) * (3.141592653589793 / 180.0);
   const double sa = -k + ang;
   const double bb = sa - ang;
   const double err = (ang - (sa - bb)) + (-k - bb);
-  const double ck = cs[i][0], sk = cs[i][1];
   const double cd = c0 * ck + s0 * sk, sd = s0 * ck - c0 * sk;   // cos, sin(ang - k)
   dx = cd + sd * err;                                           // cos(ang - k - err)
   dy = sd - cd * err;
@@ -58,4 +58,8 @@ __host__ __device__ inline int ray_end_f32(double px, double py, double ang, dou
   if (okx && oky) return 0;
   ray_end_direct(px, py, sa, fx, fy);
   return 1;
+}
+__host__ __device__ inline int ray_end_f32(double px, double py, double ang, double c0, double s0, int i,
+                                           const double (*cs)[2], double& dx, double& dy, float& fx, float& fy) {
+  return ray_end_f32_k(px, py, ang, c0, s0, i, cs[i][0], cs[i][1], dx, dy, fx, fy);
 }

@@ -127,6 +127,21 @@ def main():
               f"> 7 entries {np.mean(walked[m] > 7):.3f}")
     print(f"no-hit rays settled by a free sub-bin ({a.sub} per bin): {free_sub[~hit].mean():.3f}; hit rays wrongly free: "
           f"{free_sub[hit].sum()}")
+    # one ray per lane (16 lanes per car): a wave is 4 consecutive cars' 64 rays and runs as long as its longest walk;
+    # a wave-cooperative continuation would cost the longest head walk (<= 3 entries) plus rounds of the wave's
+    # continuation entries (4 per continuing ray per round, spread over the 64 lanes)
+    nw = len(walked) // 64
+    wv = walked[:nw * 64].reshape(nw, 64)
+    head = np.minimum(wv, 3).max(1)
+    cont = np.maximum(wv - 3, 0)
+    rounds = np.zeros(nw)
+    left = cont.copy()
+    while (left > 0).any():
+        jobs = np.minimum(left, 4).sum(1)
+        rounds += np.where(jobs > 0, np.ceil(jobs / 64), 0)
+        left = np.maximum(left - 4, 0)
+    print(f"waves {nw}: longest walk per wave mean {wv.max(1).mean():.2f} p90 {np.percentile(wv.max(1), 90):.0f}; "
+          f"cooperative continuation: head {head.mean():.2f} + rounds {rounds.mean():.2f} = {(head + rounds).mean():.2f}")
     lane = walked.reshape(-1, 4, 4).sum(1)    # lane r: rays r, r+4, r+8, r+12 -> per-lane sequential walk total
     print(f"per-lane walk totals: mean {lane.mean():.1f} p99 {np.percentile(lane, 99):.0f} max {lane.max()}")
     w2 = np.where(free_sub & ~hit, 0, walked).reshape(-1, 4, 4).sum(1)
