@@ -1322,9 +1322,11 @@ __device__ __forceinline__ void quad_transpose(const float v[4], float o[4], int
 // the head, the rest of the list only when all of them were walked; stops at the first entry whose distance
 // bound lies beyond the best hit.  Returns the best b2PolygonShape::RayCast fraction (2 = no hit).
 // GW: the wall image sw is the track's global one (read through the L2), else the workgroup's LDS copy.
-template <bool GW>
+// COOP: only the head is walked here; *kc gets the continuation's ent[] index when the walk goes on (0: done), for
+// ray_walk_coop
+template <bool GW, bool COOP = false>
 __device__ __forceinline__ float ray_walk(const BeamGrid& G, const float4* __restrict__ sw, int li, const BeamHead& h, V2 p1,
-                                          V2 p2, float dx, float dy) {
+                                          V2 p2, float dx, float dy, uint32_t* kc = nullptr) {
   float bi = 2.0f;
   uint32_t hv[4 * BEAM_HW];
 #pragma unroll
@@ -1340,6 +1342,7 @@ __device__ __forceinline__ float ray_walk(const BeamGrid& G, const float4* __res
                : wall_cast(sw[2 * j], sw[2 * j + 1], p1, p2.x, p2.y, dx, dy, bi);
   }
   const uint32_t tail = hv[BEAM_HEAD];
+  if (COOP) { *kc = more ? tail : 0u; return bi; }
   if (more && tail != 0u) {
     for (uint32_t k = tail;; k += RAY_CHUNK) {   // RAY_CHUNK entries requested together, walked in order to the sentinel
       uint32_t v4[RAY_CHUNK];
@@ -1356,6 +1359,70 @@ __device__ __forceinline__ float ray_walk(const BeamGrid& G, const float4* __res
                : wall_cast(sw[2 * j], sw[2 * j + 1], p1, p2.x, p2.y, dx, dy, bi);
       }
       if (stop) break;
+    }
+  }
+  return bi;
+}
+// The list continuations of a whole wave's rays, walked by the whole wave (one ray per lane, every lane active): per
+// round the rays still walking (k != 0) share the 64 lanes, E = 64 / 2^ceil(log2 n) lanes each, and every lane casts
+// one entry of its ray's next E entries.  The entries past a list's sentinel (or past the array, padded by
+// BEAM_COOP_PAD sentinels) are skipped; a ray is done once its round met the sentinel or a bound beyond its new best.
+// Casting entries the sequential walk would not reach changes nothing: their bounds exceed the best hit (the margin
+// the sequential stop test uses), so wall_cast's min keeps the same value; results are those of ray_walk, bit for bit.
+// A wave's continuation then costs a few rounds instead of its longest list's entries one after another.
+#define BEAM_COOP_PAD 64
+#ifndef RAY_COOP_WALK
+#define RAY_COOP_WALK 1
+#endif
+template <bool GW>
+__device__ __forceinline__ float ray_walk_coop(const BeamGrid& G, const float4* __restrict__ sw, uint32_t k, float bi, V2 p1,
+                                               V2 p2, float dx, float dy) {
+  const int lane = __lane_id();
+  const unsigned long long below = lane ? (~0ull >> (64 - lane)) : 0ull;
+  for (int round = 0; round < 4096; ++round) {   // (a finite list ends every walk; the bound is a safety net)
+    const unsigned long long m = __ballot(k != 0u);
+    if (!m) break;
+    const int na = __popcll(m);
+    const int lg = na > 1 ? 32 - __clz(na - 1) : 0;      // ceil(log2 na)
+    const int E = 64 >> lg;                               // lanes per walking ray
+    const int q = lane >> (6 - lg), o = lane & (E - 1);   // this lane's ray (q-th walking one) and entry offset
+    const bool serve = q < na;
+    int owner = 0;
+    {   // the q-th set bit of m (binary search on popcounts)
+      unsigned long long mm = m; int qq = q;
+#pragma unroll
+      for (int sh = 32; sh >= 1; sh >>= 1) {
+        const int c = __popcll(mm & ((1ull << sh) - 1ull));
+        if (qq >= c) { qq -= c; mm >>= sh; owner += sh; }
+      }
+      if (!serve) owner = lane;
+    }
+    const uint32_t ko = __shfl(k, owner);
+    const float bo = __shfl(bi, owner);
+    const V2 po = V(__shfl(p1.x, owner), __shfl(p1.y, owner)), qo = V(__shfl(p2.x, owner), __shfl(p2.y, owner));
+    const float dxo = __shfl(dx, owner), dyo = __shfl(dy, owner);
+    const uint32_t v = serve ? ldg(G.ent + ko + o) : BEAM_PAD;
+    const unsigned long long pm = __ballot(v == BEAM_PAD);
+    const unsigned long long gm = (lg == 0 ? ~0ull : ((1ull << E) - 1ull)) << (q * E & 63);
+    const bool valid = serve && v != BEAM_PAD && !(pm & gm & below);
+    float c = bo;
+    if (valid) {
+      const int j = (int)(v & 0xFFFFu);
+      PCOUNT(10, 1);
+      c = GW ? wall_cast(ldg(sw + 2 * j), ldg(sw + 2 * j + 1), po, qo.x, qo.y, dxo, dyo, bo)
+             : wall_cast(sw[2 * j], sw[2 * j + 1], po, qo.x, qo.y, dxo, dyo, bo);
+    }
+    for (int sh = 1; sh < E; sh <<= 1) c = fminf(c, __shfl_xor(c, sh));   // the group's best (min over its lanes)
+    // this lane's own ray: its group's best, sentinel, and the bound of the group's last entry
+    const int qm = __popcll(m & below);                  // rank of this lane's ray among the walking ones
+    const int g0 = (qm * E) & 63;
+    const float gb = __shfl(c, g0);
+    const uint32_t vl = __shfl(v, g0 + E - 1);
+    const unsigned long long gmo = (lg == 0 ? ~0ull : ((1ull << E) - 1ull)) << g0;
+    if (k != 0u) {
+      bi = gb;
+      const bool stop = (pm & gmo) != 0ull || (float)(vl >> 16) * 0.01f > bi * 250.0f * 1.00001f + 0.01f;
+      k = stop ? 0u : k + (uint32_t)E;
     }
   }
   return bi;
@@ -1433,6 +1500,8 @@ __device__ __forceinline__ void ray_lane(const Params& P, const TrackDev& T, con
                               : ray_end(P, (double)fx, (double)fy, (double)fa, cs.x, cs.y, i, dxd, dyd);
       const float dx = (p2.x - p1.x) * 0.004f, dy = (p2.y - p1.y) * 0.004f;   // cull only
       float bi = 2.0f;
+      uint32_t kc = 0u;   // (wave-cooperative continuation: this ray's next ent[] index, 0 when its walk is done)
+      const bool coop = LPC == 16 && RAY_COOP_WALK && __ballot(1) == ~0ull;   // every lane active: wave-uniform
       if (base >= 0) {
         const int sl = slot_of(i);
 #if RAY_HEADS_AHEAD
@@ -1444,15 +1513,18 @@ __device__ __forceinline__ void ray_lane(const Params& P, const TrackDev& T, con
 #ifdef NASCAR_PROFILE
         const BeamHead hh = beam_head(G, base + sl);
         if (LPC == 16 && pass == 0) { PROFR(4); asm volatile("" :: "v"(hh.w[0].x)); PROFR(5); }   // end points; head loaded
-        bi = ray_walk<GW>(G, sw, base + sl, hh, p1, p2, dx, dy);
+        if (LPC == 16 && coop) bi = ray_walk<GW, true>(G, sw, base + sl, hh, p1, p2, dx, dy, &kc);
+        else bi = ray_walk<GW>(G, sw, base + sl, hh, p1, p2, dx, dy);
 #else
-        bi = ray_walk<GW>(G, sw, base + sl, beam_head(G, base + sl), p1, p2, dx, dy);
+        if (LPC == 16 && coop) bi = ray_walk<GW, true>(G, sw, base + sl, beam_head(G, base + sl), p1, p2, dx, dy, &kc);
+        else bi = ray_walk<GW>(G, sw, base + sl, beam_head(G, base + sl), p1, p2, dx, dy);
 #endif
 #endif
       } else {
         PCOUNT(9, 1);
         bi = ray_fallback(T, p1, p2.x, p2.y, dx, dy, ps.z, i);
       }
+      if (LPC == 16 && coop) bi = ray_walk_coop<GW>(G, sw, kc, bi, p1, p2, dx, dy);   // (wave-uniform branch)
       PCOUNT(8, 1);
       if constexpr (RPL == 4) put4(v, q, sensor_value(bi));
       else v[q] = sensor_value(bi);
@@ -2584,7 +2656,8 @@ static void build_beams(HostTrack& t, const float cell) {
   // per list (cell-major, slot order, beam_slot): the head record holds its first BEAM_HEAD entries (BEAM_PAD
   // filled) and, when the list is longer, in its last word the ent[] index of the continuation -- the remaining
   // entries followed by one BEAM_PAD sentinel (bound 655.35 m stops every walk), so a walk needs no list end.
-  // ent[0] is a sentinel (tail word 0 = no continuation); RAY_CHUNK sentinels close the array (chunk over-read).
+  // ent[0] is a sentinel (tail word 0 = no continuation); BEAM_COOP_PAD sentinels close the array (the chunked and the
+  // wave-cooperative walks read past a list's sentinel).
   const size_t nlist = (size_t)ncell * BEAM_NB;
   B.head.assign(nlist * BEAM_HW, make_uint4(BEAM_PAD, BEAM_PAD, BEAM_PAD, BEAM_PAD));
   B.ent.assign(1, BEAM_PAD);
@@ -2604,7 +2677,7 @@ static void build_beams(HostTrack& t, const float cell) {
       }
       for (int k = 0; k < BEAM_HW; ++k) B.head[s * BEAM_HW + k] = make_uint4(h[4 * k], h[4 * k + 1], h[4 * k + 2], h[4 * k + 3]);
     }
-  for (int k = 0; k < RAY_CHUNK; ++k) B.ent.push_back(BEAM_PAD);
+  for (int k = 0; k < (RAY_CHUNK > BEAM_COOP_PAD ? RAY_CHUNK : BEAM_COOP_PAD); ++k) B.ent.push_back(BEAM_PAD);
   B.nlist = nlist;
   B.build_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
 }
