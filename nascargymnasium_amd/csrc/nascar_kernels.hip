@@ -1322,6 +1322,29 @@ __device__ __forceinline__ void quad_transpose(const float v[4], float o[4], int
 // the head, the rest of the list only when all of them were walked; stops at the first entry whose distance
 // bound lies beyond the best hit.  Returns the best b2PolygonShape::RayCast fraction (2 = no hit).
 // GW: the wall image sw is the track's global one (read through the L2), else the workgroup's LDS copy.
+// A list's continuation from ent[] index k on, walked by this lane alone: RAY_CHUNK entries requested together, walked
+// in order to the sentinel or to the first bound beyond the best hit.
+template <bool GW>
+__device__ __forceinline__ float ray_walk_rest(const BeamGrid& G, const float4* __restrict__ sw, uint32_t k, float bi, V2 p1,
+                                               V2 p2, float dx, float dy) {
+  for (;; k += RAY_CHUNK) {
+    uint32_t v4[RAY_CHUNK];
+#pragma unroll
+    for (int q = 0; q < RAY_CHUNK; ++q) v4[q] = ldg(G.ent + k + q);
+    bool stop = false;
+#pragma unroll
+    for (int q = 0; q < RAY_CHUNK; ++q) {
+      const uint32_t v = v4[q];
+      if ((float)(v >> 16) * 0.01f > bi * 250.0f * 1.00001f + 0.01f) { stop = true; break; }
+      const int j = (int)(v & 0xFFFFu);
+      PCOUNT(10, 1);
+      bi = GW ? wall_cast(ldg(sw + 2 * j), ldg(sw + 2 * j + 1), p1, p2.x, p2.y, dx, dy, bi)
+             : wall_cast(sw[2 * j], sw[2 * j + 1], p1, p2.x, p2.y, dx, dy, bi);
+    }
+    if (stop) break;
+  }
+  return bi;
+}
 // COOP: only the head is walked here; *kc gets the continuation's ent[] index when the walk goes on (0: done), for
 // ray_walk_coop
 template <bool GW, bool COOP = false>
@@ -1343,24 +1366,7 @@ __device__ __forceinline__ float ray_walk(const BeamGrid& G, const float4* __res
   }
   const uint32_t tail = hv[BEAM_HEAD];
   if (COOP) { *kc = more ? tail : 0u; return bi; }
-  if (more && tail != 0u) {
-    for (uint32_t k = tail;; k += RAY_CHUNK) {   // RAY_CHUNK entries requested together, walked in order to the sentinel
-      uint32_t v4[RAY_CHUNK];
-#pragma unroll
-      for (int q = 0; q < RAY_CHUNK; ++q) v4[q] = ldg(G.ent + k + q);
-      bool stop = false;
-#pragma unroll
-      for (int q = 0; q < RAY_CHUNK; ++q) {
-        const uint32_t v = v4[q];
-        if ((float)(v >> 16) * 0.01f > bi * 250.0f * 1.00001f + 0.01f) { stop = true; break; }
-        const int j = (int)(v & 0xFFFFu);
-        PCOUNT(10, 1);
-        bi = GW ? wall_cast(ldg(sw + 2 * j), ldg(sw + 2 * j + 1), p1, p2.x, p2.y, dx, dy, bi)
-               : wall_cast(sw[2 * j], sw[2 * j + 1], p1, p2.x, p2.y, dx, dy, bi);
-      }
-      if (stop) break;
-    }
-  }
+  if (more && tail != 0u) bi = ray_walk_rest<GW>(G, sw, tail, bi, p1, p2, dx, dy);
   return bi;
 }
 // The list continuations of a whole wave's rays, walked by the whole wave (one ray per lane, every lane active): per
@@ -1379,7 +1385,7 @@ __device__ __forceinline__ float ray_walk_coop(const BeamGrid& G, const float4* 
                                                V2 p2, float dx, float dy) {
   const int lane = __lane_id();
   const unsigned long long below = lane ? (~0ull >> (64 - lane)) : 0ull;
-  for (int round = 0; round < 4096; ++round) {   // (a finite list ends every walk; the bound is a safety net)
+  for (int round = 0; round < 1024; ++round) {   // (a finite list ends every walk; past 1024 rounds, see below)
     const unsigned long long m = __ballot(k != 0u);
     if (!m) break;
     const int na = __popcll(m);
@@ -1425,6 +1431,7 @@ __device__ __forceinline__ float ray_walk_coop(const BeamGrid& G, const float4* 
       k = stop ? 0u : k + (uint32_t)E;
     }
   }
+  if (k != 0u) bi = ray_walk_rest<GW>(G, sw, k, bi, p1, p2, dx, dy);   // (only lists of thousands of entries get here)
   return bi;
 }
 __device__ __forceinline__ int beam_slot0(double ang) {   // list slot of ray 0's direction bin (see ray_lane)
