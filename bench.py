@@ -267,6 +267,31 @@ def launch_ranks(n, argv):
     return subprocess.run(cmd, env=env).returncode
 
 
+def track_cache_prebuild(files, rank, world, beam_cell):
+    """Multi-rank runs share one build per track (verdict r05 item 5): the host-built track tables go to an on-disk cache
+    (NASCAR_TRACK_CACHE, default <tmp>/nascargymnasium_amd_tracks_<uid> when world > 1) and each rank prebuilds the
+    job's tracks there before its engine starts -- host only, in an order rotated by the rank, so the ranks build
+    different tracks at once and load the others' (a lock file per track: each is built once per node).  Returns
+    (directory, built, loaded, seconds) or None (world 1 with no cache set: the engine builds in memory)."""
+    import tempfile
+    d = os.environ.get("NASCAR_TRACK_CACHE")
+    if not d:
+        if world <= 1:
+            return None
+        d = os.path.join(tempfile.gettempdir(), f"nascargymnasium_amd_tracks_{os.getuid()}")
+        os.environ["NASCAR_TRACK_CACHE"] = d
+    from nascargymnasium_amd import _lib
+    _lib.set_track_cache(int(os.environ.get("NASCAR_TRACK_RETAIN", "8")), d)
+    uniq = sorted(set(files))
+    t0, built, loaded = time.perf_counter(), 0, 0
+    for k in range(len(uniq)):
+        if _lib.prebuild_track(uniq[(k + rank) % len(uniq)], beam_cell if beam_cell is not None else 1.0):
+            loaded += 1
+        else:
+            built += 1
+    return d, built, loaded, time.perf_counter() - t0
+
+
 def throughput(world, envs, cars, steps, elapsed_max):
     """whole-job car-steps/s under weak scaling: every rank steps its own envs x cars."""
     return world * envs * cars * steps / elapsed_max
@@ -558,6 +583,111 @@ def kernel_pass(env, step, first, KR):
     return {name: sum(r[k] for r in t) / KR for k, name in enumerate(("model_kernel", "logic_kernel", "ray_sensor_kernel"))}
 
 
+def _window(fn, first, K, dev):
+    """K calls fn(i) back to back between device synchronisations (this rank only): seconds"""
+    sync(dev)
+    t0 = time.perf_counter()
+    for i in range(first, first + K):
+        fn(i)
+    sync(dev)
+    return time.perf_counter() - t0
+
+
+def drop_in_pass(E, C, track, rank, dev, steady, K=100, W=10, settle_steps=EPISODE_STEPS):
+    """The drop-in API's throughput (secondary, beside the headline): VecCarEnv.step -- the SB3 VecEnv that replaces
+    learn/ppo.py's SubprocVecEnv(Monitor(CarEnv)) -- with device tensors (return_tensors=True), actions from the device
+    noisy rule driver on the observation the previous step returned (one nascar_policy_actions launch: the learner's
+    policy stands here), timed against the engine's per-step path on the same state and actions
+    (policy_actions + BatchedCarEnv.launch_step with auto-reset and terminal observations).
+      single_track: `track`, E x C, from the headline's settled state `steady`;
+      random_track_{C}car: track_file=None, learn/ppo.py's configuration (every reset draws a new track, on the
+        device), E x C, settled by its own 10 800 noisy-driver steps with staggered resets; the engine's per-step path
+        is timed with random tracks on (the draws / fresh worlds / layout kernels after each step) and off.
+    Each variant starts from the same state (engine arena, obs, env -> track map, draw counters)."""
+    import numpy as np
+    import torch
+    from nascargymnasium_amd import VecCarEnv
+    from nascargymnasium_amd.batched import BatchedCarEnv
+    out = {}
+
+    def vec_rate(venv):
+        eng = venv.engine
+        n = eng.E * eng.C
+        holder = [eng.obs]
+
+        def one(i):
+            o = holder[0]
+            a = eng.policy_actions(3, seed=rank, step=i, obs=o)
+            holder[0] = venv.step(a)[0]
+        _window(one, 0, W, dev)
+        return n * K / _window(one, W, K, dev)
+
+    def eng_rate(eng):
+        def one(i):
+            eng.launch_step(eng.policy_actions(3, seed=rank, step=i), auto_reset=True, terminal_obs=True)
+        _window(one, 0, W, dev)
+        return eng.E * eng.C * K / _window(one, W, K, dev)
+
+    def load(eng, snap, random_tracks=None):
+        """an engine that has not stepped yet, brought to snapshot (state, obs, track files, draws)"""
+        state, obs, files, draws, seeds = snap
+        if eng.random_track_ids is not None:
+            eng.clear_random_tracks()
+        eng.set_env_tracks(files)          # (applies at once: the engine has not been reset or stepped)
+        eng.set_state(state)
+        eng.obs.copy_(obs)
+        if random_tracks is not None:
+            eng.set_random_tracks(random_tracks, seeds, draws=draws)
+
+    # single track, from the headline's steady state
+    if steady is not None:
+        blob, _, gobs, _, _ = steady
+        venv = VecCarEnv(E, track, num_cars=C, return_tensors=True, device=dev)
+        snap = (torch.from_numpy(blob).to(dev), torch.from_numpy(gobs).to(dev), [track] * E, None, None)
+        load(venv.engine, snap)
+        rv = vec_rate(venv)
+        venv.close()
+        eng = BatchedCarEnv(E, C, track, device=dev)
+        load(eng, snap)
+        re = eng_rate(eng)
+        eng.close()
+        out["single_track"] = {"config": f"{os.path.basename(track)[:-6]} {E} envs x {C} cars, steady state",
+                               "vec_env": rv, "engine_per_step": re, "ratio": re / rv}
+    from nascargymnasium_amd.track import available_tracks
+    tracks = available_tracks()
+    for c in sorted({1, C}):
+        venv = VecCarEnv(E, None, num_cars=c, return_tensors=True, seed=1000 + rank, device=dev)
+        eng = venv.engine
+        venv.reset()
+        t0 = time.perf_counter()
+        settle(eng, Stepper(eng, "noisy", rank, None, None, 0), settle_steps, True, dev)
+        sync(dev)
+        t_settle = time.perf_counter() - t0
+        ids, draws = eng.env_track_ids()
+        snap = (eng.get_state(), eng.obs.clone(), [eng._track_files_by_id[int(i)] for i in ids], draws, venv._seeds)
+        resets0 = int(draws.sum())
+        rv = vec_rate(venv)
+        resets = int(eng.env_track_ids()[1].sum()) - resets0
+        venv.close()
+        e2 = BatchedCarEnv(E, c, snap[2], device=dev)
+        load(e2, snap, tracks)
+        re = eng_rate(e2)
+        e2.close()
+        e3 = BatchedCarEnv(E, c, snap[2], device=dev)
+        load(e3, snap)
+        r_off = eng_rate(e3)
+        e3.close()
+        out[f"random_track_{c}car"] = {
+            "config": f"track_file=None (learn/ppo.py:65-78), {E} envs x {c} cars, steady state after {settle_steps} "
+                      f"noisy-driver steps ({t_settle:.1f} s)",
+            "vec_env": rv, "engine_per_step": re, "ratio": re / rv, "engine_per_step_tracks_fixed": r_off,
+            "track_switches_in_vec_window": resets}
+    out["note"] = (f"car-steps/s of the drop-in VecCarEnv.step (device tensors, SB3 Monitor bookkeeping and action checks "
+                   f"on the device, lazy infos) vs the engine's per-step path (policy_actions + launch_step, auto-reset, "
+                   f"terminal obs) on the same state; ratio = engine / vec_env; {K} steps after {W} warm-up each")
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=None,
@@ -590,6 +720,9 @@ def main():
     ap.add_argument("--car-contact", action="store_true", help="BUILD-ONLY EXTENSION: car-car contact inside each env "
                     "(cfg3's 'car-car collision on'; no reference counterpart, reported as its own row)")
     ap.add_argument("--no-secondary", action="store_true", help="skip the uniform-from-reset secondary measurement")
+    ap.add_argument("--no-drop-in", action="store_true", help="skip the drop-in API (VecCarEnv) secondary measurement")
+    ap.add_argument("--beam-cell", type=float, default=None, help="the sensors' beam-list cell size in m (default 1; "
+                    "identical results at any size)")
     ap.add_argument("--cpu-threads", type=int, default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
@@ -626,16 +759,19 @@ def main():
     if args.load_state:
         S = 0
     tpath = track_path(args.track)
+    if args.mixed:
+        from nascargymnasium_amd.track import available_tracks
+        names = available_tracks()
+        env_files = [names[e % len(names)] for e in range(E)]
+    else:
+        env_files = [tpath] * E
+    tcache = track_cache_prebuild(env_files, rank, world, args.beam_cell)
 
     def make_env():
         if args.plumbing:
             return PlumbingEngine(E, C, rank, dev)
         from nascargymnasium_amd.batched import BatchedCarEnv
-        if args.mixed:
-            from nascargymnasium_amd.track import available_tracks
-            names = available_tracks()
-            return BatchedCarEnv(E, C, [names[e % len(names)] for e in range(E)], device=dev)
-        return BatchedCarEnv(E, C, tpath, device=dev)
+        return BatchedCarEnv(E, C, env_files if args.mixed else tpath, device=dev, beam_cell=args.beam_cell)
 
     env = make_env()
     if args.rollout_streams is not None:
@@ -785,11 +921,15 @@ def main():
         out["per_step"] = {"value": throughput(world, E, C, K, per_step), "ms_per_step": per_step / K * 1e3,
                            "note": "secondary: the same envs and driver stepped by one whole-batch launch per step "
                                    "(nascar_step_driven), every step waiting for the batch's slowest car"}
-    steady = None   # the steady state the CPU baseline continues from (rank 0 of a 1-GPU run, noisy driver, one track)
+    steady = None   # the steady state the CPU baseline and the drop-in pass continue from (rank 0 of a 1-GPU run)
     cpu_leg = rank == 0 and world == 1 and not args.no_cpu_baseline and not args.plumbing
-    if cpu_leg and args.policy == "noisy" and not args.mixed:
+    drop_in = (rank == 0 and world == 1 and not args.no_drop_in and not args.plumbing and args.policy == "noisy"
+               and not args.mixed and not args.gather and not args.car_contact)
+    if (cpu_leg or drop_in) and args.policy == "noisy" and not args.mixed:
         sync(dev)
         steady = (env.get_state().cpu().numpy(), E, env.obs.cpu().numpy().reshape(E, C, 38).copy(), next_step, rank)
+    if drop_in:
+        out["drop_in"] = drop_in_pass(E, C, tpath, rank, dev, steady)
     if not args.no_secondary and args.policy != "uniform" and not args.gather:
         # secondary, labelled: round 1's workload (uniform U[-1,1]^2 from reset) on a fresh engine
         del step
@@ -806,6 +946,11 @@ def main():
                                      "note": "secondary: uniform actions from reset (cars stay on the start "
                                              "straight; no contacts, laps or resets) -- an upper bound, not the headline"}
         env = env2
+    if tcache is not None:   # (after every timed window: the per-rank cache statistics of the engine starts)
+        out["track_cache"] = {"dir": tcache[0], "built": gather_all(tcache[1], dev), "loaded": gather_all(tcache[2], dev),
+                              "prebuild_s": gather_all(tcache[3], dev),
+                              "note": "per rank: tracks built into / loaded from the node's on-disk track cache before "
+                                      "the engine started (each track built once per node)"}
     if args.plumbing:   # every rank must have issued the same collectives in the same order
         seq = list(COLLECTIVES)
         h = int(hashlib.sha256("|".join(seq).encode()).hexdigest()[:12], 16)
@@ -813,7 +958,8 @@ def main():
         out["metric"] = "plumbing (no GPU, not a measurement)"
         out["collectives"] = {"rank0": seq, "all_ranks_equal": len(set(hs)) == 1, "ranks": len(hs)}
     if cpu_leg:
-        out["cpu_baseline"] = cpu_baseline(tpath, C, args.cpu_budget, args.cpu_threads, steady)
+        out["cpu_baseline"] = cpu_baseline(tpath, C, args.cpu_budget, args.cpu_threads,
+                                           steady if args.policy == "noisy" and not args.mixed else None)
     if rank == 0:
         print(json.dumps(out), flush=True)
     env.close()

@@ -47,11 +47,60 @@ const char* nascar_last_error(void);
  * are derived on the host here.  Returns the track id (>= 0). */
 int nascar_add_track(NascarHandle* h, const double* segments, int32_t nseg, double total_length,
                      const double* walls, int32_t nwall);
-/* per-env track ids (host array of E ints); envs are grouped per track into workgroups.  A changed id takes
+/* Track build cache (no reference counterpart: the reference rebuilds its walls per CarPhysics, src/car_physics.py:118,
+ * and each SubprocVecEnv worker does so on its own, learn/ppo.py:77).  A track's tables (walls, grids and ~0.8 GB of
+ * beam lists at 1 m cells, ~2 s of 16 host threads) are shared by every handle of the process; `retain` (default 8)
+ * builds stay alive after their last handle closes, most recently used first (0: freed with the last handle).  `dir`
+ * (NULL or "" = none, the default) holds on-disk copies of the host tables keyed by the track's arrays and cell size:
+ * a process finding one loads it instead of building, one that builds writes it (temporary file + rename), and the
+ * processes building one key serialise on a lock file, so the ranks of a node build each track once. */
+int nascar_set_track_cache(int32_t retain, const char* dir);
+/* Host only (no device): the host tables of one track (arguments as nascar_add_track, plus the beam-list cell size)
+ * into the disk cache -- returns 1 if they were already there, 0 if built and written now, < 0 on error (no cache
+ * directory set included).  A launcher prebuilds a job's tracks once before its ranks start. */
+int nascar_prebuild_track(const double* segments, int32_t nseg, double total_length, const double* walls, int32_t nwall,
+                          float beam_cell);
+
+/* per-env track ids (host array of E ints); envs are grouped per track into workgroups (each track's workgroups spread
+ * evenly over the workgroup order, so every shard of the sharded rollout holds a share of every track).  A changed id takes
  * effect at that env's next nascar_reset (fresh physics worlds on the new track, as CarEnv.reset recreates
  * CarPhysics, src/car_env.py:375-394); until then the env keeps stepping on its old track.  On a handle that has
  * not been reset, stepped or restored yet the ids apply at once. */
 int nascar_set_env_tracks(NascarHandle* h, const int32_t* env_track);
+
+/* Random-track mode, CarEnv(track_file=None) (src/car_env.py:243-303 _select_random_track / _load_random_track,
+ * :331-333 and :375-394 in reset; learn/ppo.py:65-78 builds every training env this way).  With ntracks > 0, every
+ * reset of an env -- nascar_reset of its mask bit, or the auto-reset inside nascar_step / nascar_step_driven /
+ * nascar_rollout -- first draws its next track from the `ntracks` distinct track ids in `tracks` (nascar_add_track ids),
+ * uniformly among those that are not its current track (all of them when it is not in the set), and an env whose
+ * track changes gets fresh physics worlds there.  Draw k of env e (k counts its draws since seeding, starting at
+ * draws[e], NULL = 0) is nascar_track_draw(seeds[e], k, current): a counter hash, reproducible on the host (the
+ * reference re-seeds Python's `random` from pid + clock per draw).  The env -> track map, the counters and the
+ * workgroup layout live on the device and are updated there (no host synchronisation per step).  ntracks = 0 ends
+ * the mode (envs keep their current tracks).  While it is on, nascar_set_env_tracks fails, nascar_rollout runs one
+ * shard, and the state snapshot (nascar_get_state) does not carry the env -> track map.  Host arrays; synchronises
+ * `stream` once. */
+int nascar_set_random_tracks(NascarHandle* h, const int32_t* tracks, int32_t ntracks, const uint64_t* seeds,
+                             const int32_t* draws, void* stream);
+/* The env -> track ids and the draws taken per env (device int32 [E] each, either may be NULL), on `stream`: the
+ * device's in random-track mode, otherwise the host's assignment and zeros. */
+int nascar_get_env_tracks(NascarHandle* h, int32_t* env_track, int32_t* draws, void* stream);
+/* Host function (no device): the random-track draw for n envs -- out[i] = draw k[i] of seed seeds[i] from an env on
+ * track current[i] (-1: none) over tracks[0 .. ntracks). */
+int nascar_track_draw(int32_t n, const uint64_t* seeds, const int32_t* k, const int32_t* current, const int32_t* tracks,
+                      int32_t ntracks, int32_t* out);
+
+/* SB3 VecEnv glue of the drop-in VecCarEnv (stable_baselines3 Monitor + VecEnv around CarEnv.step, learn/ppo.py:65-78),
+ * one launch per step on device buffers:
+ * nascar_vec_post: done[e] = terminated | truncated (from env_flags); ep_ret [E*C] float64 += reward, ep_len [E] int64
+ *   += 1, their new values copied to snap_ret / snap_len (Monitor's info["episode"] r / l for an env that just ended),
+ *   then zeroed for the done envs.
+ * nascar_check_actions: *bad (device int32) = 1 if any action is outside the action space (continuous: not in
+ *   [-1, 1] or NaN; discrete int32: not in {0..4}) -- CarEnv.step's assert self.action_space.contains(action)
+ *   (src/car_env.py:694), read by the caller when it next synchronises. */
+int nascar_vec_post(NascarHandle* h, const float* reward, const uint8_t* env_flags, double* ep_ret, int64_t* ep_len,
+                    uint8_t* done, double* snap_ret, int64_t* snap_len, void* stream);
+int nascar_check_actions(NascarHandle* h, const void* actions, int32_t discrete, int32_t* bad, void* stream);
 
 /* CarEnv.reset (src/car_env.py:316-535) for the envs whose env_mask[e] != 0 (device uint8[E];
  * NULL = all envs).  Writes obs [E*C*38] float32 of the reset envs. */

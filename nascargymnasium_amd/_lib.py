@@ -127,17 +127,73 @@ def lib():
     L.nascar_debug_sincosf.restype = ctypes.c_int
     L.nascar_debug_sensors.argtypes = [vp, vp, vp, i32, vp]
     L.nascar_debug_sensors.restype = ctypes.c_int
+    i32p, u64p = ctypes.POINTER(i32), ctypes.POINTER(u64)
+    L.nascar_track_draw.argtypes = [i32, u64p, i32p, i32p, i32p, i32, i32p]
+    L.nascar_track_draw.restype = ctypes.c_int
+    L.nascar_set_random_tracks.argtypes = [vp, i32p, i32, u64p, i32p, vp]
+    L.nascar_set_random_tracks.restype = ctypes.c_int
+    L.nascar_get_env_tracks.argtypes = [vp, vp, vp, vp]
+    L.nascar_get_env_tracks.restype = ctypes.c_int
+    L.nascar_vec_post.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, vp]
+    L.nascar_vec_post.restype = ctypes.c_int
+    L.nascar_check_actions.argtypes = [vp, vp, i32, vp, vp]
+    L.nascar_check_actions.restype = ctypes.c_int
+    L.nascar_set_track_cache.argtypes = [i32, ctypes.c_char_p]
+    L.nascar_set_track_cache.restype = ctypes.c_int
+    L.nascar_prebuild_track.argtypes = [d_p, i32, ctypes.c_double, d_p, i32, ctypes.c_float]
+    L.nascar_prebuild_track.restype = ctypes.c_int
     _lib = L
+    # track build cache: NASCAR_TRACK_CACHE names an on-disk cache directory (none by default; bench.py sets one for
+    # multi-rank runs), NASCAR_TRACK_RETAIN the builds kept alive after their last handle (default 8)
+    set_track_cache(int(os.environ.get("NASCAR_TRACK_RETAIN", "8")), os.environ.get("NASCAR_TRACK_CACHE", ""))
     return L
 
 
 EXPORTED = ["nascar_create", "nascar_destroy", "nascar_last_error", "nascar_add_track", "nascar_set_env_tracks",
             "nascar_reset", "nascar_step", "nascar_step_driven", "nascar_rollout", "nascar_get_info", "nascar_set_perf_history", "nascar_set_car_contact", "nascar_set_rollout_streams", "nascar_get_rollout_streams", "nascar_set_envs_per_block", "nascar_get_envs_per_block", "nascar_set_sensor_lanes", "nascar_set_sensor_block", "nascar_set_beam_cell", "nascar_set_fused_logic", "nascar_get_fused_logic", "nascar_state_bytes", "nascar_get_state",
             "nascar_set_state", "nascar_policy_actions", "nascar_set_step_events", "nascar_set_actor", "nascar_set_actor_precision", "nascar_actor_forward",
-            "nascar_debug_sincosf", "nascar_debug_sensors"]
+            "nascar_debug_sincosf", "nascar_debug_sensors", "nascar_track_draw", "nascar_set_random_tracks",
+            "nascar_get_env_tracks", "nascar_vec_post", "nascar_check_actions", "nascar_set_track_cache",
+            "nascar_prebuild_track"]
 
 
 def check(rc):
     if rc < 0:
         raise RuntimeError("libnascar: " + lib().nascar_last_error().decode())
     return rc
+
+
+def track_draw(seeds, k, current, tracks):
+    """nascar_track_draw (host): the random-track mode's draw k of each env -- its next track id given its seed and
+    current track (-1: none), uniform over `tracks` minus the current one (CarEnv._select_random_track,
+    src/car_env.py:264-287).  Vectorised over the envs; returns an int32 array."""
+    import numpy as np
+    seeds = np.ascontiguousarray(seeds, np.uint64).ravel()
+    n = seeds.size
+    k = np.ascontiguousarray(np.broadcast_to(np.asarray(k, np.int32), (n,)))
+    cur = np.ascontiguousarray(np.broadcast_to(np.asarray(current, np.int32), (n,)))
+    tr = np.ascontiguousarray(tracks, np.int32)
+    out = np.empty(n, np.int32)
+    i32p, u64p = ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_uint64)
+    check(lib().nascar_track_draw(n, seeds.ctypes.data_as(u64p), k.ctypes.data_as(i32p), cur.ctypes.data_as(i32p),
+                                  tr.ctypes.data_as(i32p), tr.size, out.ctypes.data_as(i32p)))
+    return out
+
+
+def set_track_cache(retain=8, directory=""):
+    """nascar_set_track_cache: `retain` track builds kept alive after their last handle; `directory` the on-disk cache of
+    host-built track tables ("" = none)."""
+    check(lib().nascar_set_track_cache(int(retain), (directory or "").encode()))
+
+
+def prebuild_track(path, beam_cell=1.0):
+    """nascar_prebuild_track (host only, no GPU): the track's tables into the disk cache.  True if they were there
+    already, False if built now."""
+    import numpy as np
+    from .track import build_walls, load_track, track_path
+    t = load_track(track_path(path))
+    seg = np.ascontiguousarray(t.segment_table())
+    walls = np.ascontiguousarray(build_walls(t)[:, :4])
+    dp = ctypes.POINTER(ctypes.c_double)
+    return bool(check(lib().nascar_prebuild_track(seg.ctypes.data_as(dp), seg.shape[0], float(t.total_length),
+                                                  walls.ctypes.data_as(dp), walls.shape[0], float(beam_cell))))

@@ -63,7 +63,8 @@ class BatchedCarEnv:
             self.set_envs_per_block(envs_per_block)
         if beam_cell is not None:     # before the tracks are added: their beam lists are built at this cell size
             _lib.check(self.L.nascar_set_beam_cell(self.h, float(beam_cell)))
-        self.tracks, self._track_id = [], {}
+        self.tracks, self._track_id, self._track_files_by_id = [], {}, {}
+        self.random_track_ids = None
         for p in uniq:
             self._add_track(p)
         self.set_env_tracks(files)
@@ -146,6 +147,7 @@ class BatchedCarEnv:
                                                      walls.ctypes.data_as(dp), walls.shape[0]))
         self.tracks.append(t)
         self._track_id[path] = tid
+        self._track_files_by_id[tid] = path
         return tid
 
     def set_env_tracks(self, files: Sequence[str]):
@@ -161,6 +163,53 @@ class BatchedCarEnv:
         _lib.check(self.L.nascar_set_env_tracks(self.h, env_track.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))))
         self.env_track = env_track
         self.track_files = [track_path(f) for f in files]
+
+    # ------------------------------------------------------------------ random-track mode (src/car_env.py:243-303)
+    def set_random_tracks(self, files: Sequence[str], seeds, draws=None):
+        """Random-track mode on the device (CarEnv(track_file=None), src/car_env.py:243-303, 331-398; learn/ppo.py:65-78
+        trains every env this way): every reset of an env -- `reset(mask)` or the auto-reset inside a step -- first draws
+        its next track from `files` (any but its current one, CarEnv._select_random_track) and a changed track gets fresh
+        worlds; the block map is rebuilt on the device, so a step makes no host round trip.  Draw k of env e is
+        `_lib.track_draw(seeds[e], k, current, ids)`; `draws` (default 0) are the per-env draw counters to continue from.
+        Files not loaded yet are loaded here.  While the mode is on, `set_env_tracks` raises; `clear_random_tracks` ends
+        it (the envs keep their current tracks)."""
+        ids = np.array([self._add_track(f) for f in files], np.int32)
+        seeds = np.ascontiguousarray(np.asarray(seeds, dtype=np.uint64).ravel())
+        if seeds.size != self.E:
+            raise ValueError(f"need one seed per env ({self.E}), got {seeds.size}")
+        dr = None
+        if draws is not None:
+            dr = np.ascontiguousarray(np.broadcast_to(np.asarray(draws, np.int32), (self.E,)))
+        i32p, u64p = ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_uint64)
+        with torch.cuda.device(self.device):
+            _lib.check(self.L.nascar_set_random_tracks(self.h, ids.ctypes.data_as(i32p), int(ids.size),
+                                                       seeds.ctypes.data_as(u64p),
+                                                       dr.ctypes.data_as(i32p) if dr is not None else None, _stream()))
+        self.random_track_ids = ids
+        self.random_track_files = [track_path(f) for f in files]
+
+    def clear_random_tracks(self):
+        """End random-track mode: the envs keep the tracks they are on, managed by `set_env_tracks` again."""
+        with torch.cuda.device(self.device):
+            _lib.check(self.L.nascar_set_random_tracks(self.h, None, 0, None, None, _stream()))
+        self.random_track_ids = None
+        ids, _ = self.env_track_ids()
+        self.env_track = ids
+        self.track_files = [self._track_files_by_id[i] for i in ids]
+
+    def env_track_ids(self):
+        """(track id per env, draws taken per env) as numpy int32 arrays -- the device's in random-track mode (one host
+        synchronisation), else the host's assignment and zeros."""
+        t = torch.empty(2, self.E, dtype=torch.int32, device=self.device)
+        with torch.cuda.device(self.device):
+            _lib.check(self.L.nascar_get_env_tracks(self.h, _ptr(t[0]), _ptr(t[1]), _stream()))
+        a = t.cpu().numpy()
+        return a[0].copy(), a[1].copy()
+
+    def env_track_files(self):
+        """the .track path each env is on now"""
+        ids, _ = self.env_track_ids()
+        return [self._track_files_by_id[i] for i in ids]
 
     # ------------------------------------------------------------------ core API
     def reset(self, env_mask: Optional[torch.Tensor] = None) -> torch.Tensor:

@@ -22,6 +22,11 @@
 #include <memory>
 #include <mutex>
 #include <unordered_map>
+#include <deque>
+#include <fcntl.h>
+#include <sys/file.h>
+#include <sys/stat.h>
+#include <unistd.h>
 #include <vector>
 
 #include "../../include/nascar.h"
@@ -1027,6 +1032,7 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(SENS
   const int slot = sub * CPW + lc;          // car slot within the step kernel's workgroup b
   const int el = slot / C, car = slot - el * C;
   const int env = blk_env_of(P, el, b * P.epb + el);
+  if (blk_track_of(P, b) < 0) return;   // an empty workgroup of a device-built block map (random-track mode)
   const TrackDev T = P.tracks[blk_track_of(P, b)];
   const int nw = T.nwall, ng = T.ngroup;
   // walls and groups read straight from the track's global image (L1/L2-resident, shared by every
@@ -1380,12 +1386,18 @@ __device__ __forceinline__ float ray_walk(const BeamGrid& G, const float4* __res
 #ifndef RAY_COOP_WALK
 #define RAY_COOP_WALK 1
 #endif
+// rounds of the cooperative walk before a ray still walking finishes on its own lane (ray_walk_rest).  No bundled
+// track's lists come near it; a tools build with a cap of 1 (build(): tools/build/libnascar_coop1.so) sends every long
+// walk down that path, and tests/test_gpu_sensors.py checks its values against the product build's
+#ifndef RAY_COOP_ROUNDS
+#define RAY_COOP_ROUNDS 1024
+#endif
 template <bool GW>
 __device__ __forceinline__ float ray_walk_coop(const BeamGrid& G, const float4* __restrict__ sw, uint32_t k, float bi, V2 p1,
                                                V2 p2, float dx, float dy) {
   const int lane = __lane_id();
   const unsigned long long below = lane ? (~0ull >> (64 - lane)) : 0ull;
-  for (int round = 0; round < 1024; ++round) {   // (a finite list ends every walk; past 1024 rounds, see below)
+  for (int round = 0; round < RAY_COOP_ROUNDS; ++round) {   // (a finite list ends every walk; past the cap, see below)
     const unsigned long long m = __ballot(k != 0u);
     if (!m) break;
     const int na = __popcll(m);
@@ -1431,7 +1443,7 @@ __device__ __forceinline__ float ray_walk_coop(const BeamGrid& G, const float4* 
       k = stop ? 0u : k + (uint32_t)E;
     }
   }
-  if (k != 0u) bi = ray_walk_rest<GW>(G, sw, k, bi, p1, p2, dx, dy);   // (only lists of thousands of entries get here)
+  if (k != 0u) bi = ray_walk_rest<GW>(G, sw, k, bi, p1, p2, dx, dy);   // (product build: lists of thousands of entries)
   return bi;
 }
 __device__ __forceinline__ int beam_slot0(double ang) {   // list slot of ray 0's direction bin (see ray_lane)
@@ -1653,6 +1665,7 @@ ray_sensor_kernel(Params P, float* obs, float* terminal_obs, int passes, int SUB
   const int slot = sub * CPW + lc;
   const int el = slot / C, car = slot - el * C;
   const int env = blk_env_of(P, el, b * P.epb + el);
+  if (blk_track_of(P, b) < 0) return;   // an empty workgroup of a device-built block map (random-track mode)
   const TrackDev& T = P.tracks[blk_track_of(P, b)];
   PROF_B0(P.blk0 * SUB);   // profile builds: stamp rows numbered over the whole grid (the sharded rollout's shards)
   PROFR_RT(14); PROFR(0); PROFR_XCC(8);   // profile builds: stamp slots 0-7 (16 lanes per car: ray_lane's 2-6), realtime 14 / 15
@@ -1850,6 +1863,7 @@ __global__ void __launch_bounds__(SBLOCK) __attribute__((amdgpu_waves_per_eu(MOD
   const int el = tid / C, car = tid - el * C;
   const int slot = (blockIdx.x + P.blk0) * P.epb + el;
   const int env = blk_env_of(P, el, slot);
+  if (blk_track_of(P, blockIdx.x + P.blk0) < 0) return;   // empty workgroup (device-built block map)
   Car c;
   SegReg sr;
   model_block<false>(P, actions, discrete, want_term, policy, seed, step, pobs, tid, env, env >= 0 ? env * C + car : 0, c, sr);
@@ -2177,6 +2191,7 @@ __global__ void __launch_bounds__(SBLOCK) LOGIC_ATTR logic_kernel(Params P, floa
   const int slot = (blockIdx.x + P.blk0) * P.epb + el;
   const int env = blk_env_of(P, el, slot);
   const int n = env >= 0 ? env * C + car : 0;
+  if (blk_track_of(P, blockIdx.x + P.blk0) < 0) return;   // empty workgroup (device-built block map)
   PROF_B0(P.blk0);
   LPROF(0);
   Car c;
@@ -2229,6 +2244,7 @@ model_logic_kernel(Params P, const void* actions, int discrete, int want_term, i
   const int slot = (blockIdx.x + P.blk0) * P.epb + el;
   const int env = blk_env_of(P, el, slot);
   const int n = env >= 0 ? env * C + car : 0;
+  if (blk_track_of(P, blockIdx.x + P.blk0) < 0) return;   // empty workgroup (device-built block map)
   Car c;
   SegReg sr;
   double sim;
@@ -2316,6 +2332,7 @@ rollout_kernel(const Params* __restrict__ Pg, int K, int policy, uint64_t seed, 
                uint8_t* car_flags, uint8_t* env_flags, int auto_reset, int traj) {
   ParamsK Pk = (ParamsK)Pg;   // global -> constant address space (same addresses)
   const Params& P = *Pg;
+  if (blk_track_of(P, blockIdx.x) < 0) return;   // empty workgroup (device-built block map)
   PROF_B0(0);
   {
     const TrackDev T = P.tracks[blk_track_of(P, blockIdx.x)];
@@ -2359,6 +2376,7 @@ __global__ void __launch_bounds__(SBLOCK) reset_kernel(Params P, const uint8_t* 
   const int el = tid / C, car = tid - el * C;
   const int slot = blockIdx.x * P.epb + el;
   int env = blk_env_of(P, el, slot);
+  if (blk_track_of(P, blockIdx.x) < 0) return;   // empty workgroup (device-built block map)
   if (env >= 0 && mask && !mask[env]) { P.pose[env * C + car] = make_float4(0.f, 0.f, 0.f, __int_as_float(0)); env = -1; }
   const TrackDev T = P.tracks[blk_track_of(P, blockIdx.x)];
   const WallSet S{T.walls, T.nwall, T.bp, T.sn, T.wfat};
@@ -2387,9 +2405,9 @@ __global__ void __launch_bounds__(SBLOCK) info_kernel(Params P, double* info) {
   const int el = tid / C, car = tid - el * C;
   const int slot = blockIdx.x * P.epb + el;
   const int env = blk_env_of(P, el, slot);
+  if (env < 0 || blk_track_of(P, blockIdx.x) < 0) return;
   const TrackDev T = P.tracks[blk_track_of(P, blockIdx.x)];
   const WallSet S{T.walls, T.nwall, T.bp, T.sn, T.wfat};
-  if (env < 0) return;
   const int n = env * C + car;
   Car c;
   car_load(P, n, c);
@@ -2424,6 +2442,187 @@ __global__ void __launch_bounds__(SBLOCK) info_kernel(Params P, double* info) {
   } else {
     o[INFO_PERF_COUNT] = -1.0; o[INFO_PERF_MAX] = 0.0; o[INFO_PERF_FIRST] = -1.0;
   }
+}
+
+// ------------------------------------------------------------------ random-track mode (CarEnv(track_file=None))
+// CarEnv._select_random_track (src/car_env.py:264-287): a uniform choice over the bundled tracks, excluding the env's
+// current track when it is one of them; every CarEnv.reset draws again (src/car_env.py:331-333) and a changed track
+// gets fresh physics worlds (src/car_env.py:375-394).  learn/ppo.py:65-78 trains every env this way.  The reference
+// re-seeds Python's global `random` from pid + wall clock before each draw, so its sequence is not reproducible; here
+// draw k of an env is a counter hash of (the env's seed, k) -- reproducible on the host through nascar_track_draw.
+__host__ __device__ inline uint32_t rt_mix32(uint64_t x) {   // splitmix64 finaliser
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  x ^= x >> 31;
+  return (uint32_t)(x >> 32);
+}
+__host__ __device__ inline int rt_draw(uint64_t seed, int32_t k, int cur, const int* tracks, int nt) {
+  if (nt <= 0) return cur;
+  int pos = -1;
+  for (int i = 0; i < nt; ++i) pos = (pos < 0 && tracks[i] == cur) ? i : pos;
+  const bool excl = nt > 1 && pos >= 0;      // "if len(available_tracks) > 1 and previous_track in available_tracks"
+  const uint32_t m = (uint32_t)(excl ? nt - 1 : nt);
+  const uint32_t u = rt_mix32(seed ^ (0xD1B54A32D192ED03ull * ((uint64_t)(uint32_t)k + 1ull)));
+  int j = (int)(((uint64_t)u * m) >> 32);    // uniform index into the candidates (random.choice)
+  if (excl && j >= pos) ++j;
+  return tracks[j];
+}
+// device state of the mode (nascar_set_random_tracks): per env its track, draws taken since seeding and seed
+struct RtDev {
+  int* env_track; int* draws; const uint64_t* seed; const int* tracks; int ntracks;
+  int* dirty;   // set when an env changed track: block_map_kernel rebuilds the workgroup layout, then clears it
+};
+// nascar_reset: each reset env draws its next track; a changed one clears E_CREATED, so reset_kernel builds it fresh worlds
+__global__ void __launch_bounds__(256) rt_reset_draw_kernel(Params P, RtDev R, const uint8_t* mask) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= P.E || (mask && !mask[e])) return;
+  const int cur = R.env_track[e], k = R.draws[e];
+  R.draws[e] = k + 1;
+  const int t = rt_draw(R.seed[e], k, cur, R.tracks, R.ntracks);
+  if (t != cur) {
+    R.env_track[e] = t;
+    P.env_i32[E_CREATED * P.E + e] = 0;
+    *R.dirty = 1;
+  }
+}
+// After a step with auto-reset: every env the step reset (env flag EF_RESET: reset in the launch on its old track) draws
+// its next track; an env whose track changes is reset again on the new one with fresh worlds (Car() + CarPhysics,
+// exactly reset_kernel's fresh path: every car field rewritten), its reset observation rewritten (obs[0:22] here, the 16
+// sensors by pass-B ray walks on the new track).  A 256-thread workgroup per 64 envs: the first wave draws (one lane per
+// env) and lists the switching envs in LDS; then every thread takes one car of them for the reset and one ray of them
+// for the walks, so an env's whole reset and sensor work run in parallel (few envs switch per step: one per episode).
+// The terminal observation (the old track's, written by the step) is untouched.
+#define RT_SWITCH_BLOCK 256
+__global__ void __launch_bounds__(RT_SWITCH_BLOCK) rt_switch_kernel(Params P, RtDev R, const uint8_t* env_flags, float* obs) {
+  __shared__ int s_env[64], s_tr[64], s_n;
+  const int tid = threadIdx.x, C = P.C;
+  if (tid < 64) {
+    const int e = blockIdx.x * 64 + tid;
+    int nt = -1;
+    if (e < P.E && (env_flags[e] & EF_RESET)) {
+      const int cur = R.env_track[e], k = R.draws[e];
+      R.draws[e] = k + 1;
+      const int t = rt_draw(R.seed[e], k, cur, R.tracks, R.ntracks);
+      if (t != cur) { R.env_track[e] = t; nt = t; }
+    }
+    const unsigned long long m = __ballot(nt >= 0);
+    const int lane = tid;
+    if (nt >= 0) {
+      const int q = __popcll(m & (lane ? (~0ull >> (64 - lane)) : 0ull));
+      s_env[q] = e; s_tr[q] = nt;
+    }
+    if (lane == 0) { s_n = __popcll(m); if (m) *R.dirty = 1; }
+  }
+  __syncthreads();
+  const int ns = s_n;
+  if (ns == 0) return;                    // (block-uniform)
+  for (int t = tid; t < ns * C; t += RT_SWITCH_BLOCK) {   // one car per thread: the fresh reset on the new track
+    const int q = t / C, car = t - q * C, n = s_env[q] * C + car;
+    const TrackDev T = P.tracks[s_tr[q]];   // segments from global memory (as reset_kernel)
+    const WallSet S{T.walls, T.nwall, T.bp, T.sn, T.wfat};
+    Car c;
+    car_load(P, n, c);
+    car_reset(P, c, n, true, S, T);
+    float o[22];
+    car_obs(c, o);
+    for (int i = 0; i < 22; ++i) obs[(size_t)n * 38 + i] = o[i];
+    set_pose(P, (size_t)P.N + n, c, PM_B_OBS);
+    car_store(P, n, c);
+  }
+  __threadfence();
+  __syncthreads();                        // the pass-B poses stored before the walks read them
+  for (int t = tid; t < ns * C * 16; t += RT_SWITCH_BLOCK) {   // one ray per thread
+    const int cc = t >> 4, q = cc / C, car = cc - q * C;
+    const TrackDev T = P.tracks[s_tr[q]];
+    ray_lane<16, true>(P, T, T.swall, s_env[q] * C + car, t & 15, obs, nullptr, 2);
+  }
+}
+// The workgroup layout rebuilt on the device (random-track mode; prepare() builds it on the host otherwise): envs
+// grouped by track in ascending env order, each track's envs in whole workgroups of epb envs, tracks in id order, the
+// workgroups past the last one empty (track -1) -- the host layout's order, with a fixed grid of nb_cap workgroups so
+// no launch waits for the host.  One 1024-thread workgroup: per-track counts (LDS atomics), block offsets, then each
+// env's rank among its track's envs by ballots over 1024-env chunks.  Does nothing unless *dirty (or force).
+#define RT_MAX_TRACKS 64
+__global__ void __launch_bounds__(1024) block_map_kernel(int E, int epb, int ntr, const int* env_track, int* blk_track,
+                                                         int* blk_env, int nb_cap, int* dirty, int force) {
+  __shared__ int cnt[RT_MAX_TRACKS], boff[RT_MAX_TRACKS + 1], run[RT_MAX_TRACKS], woff[16][RT_MAX_TRACKS];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  if (!force && *dirty == 0) return;      // (every thread reads it before thread 0 clears it, after the barriers below)
+  for (int t = tid; t < ntr; t += 1024) { cnt[t] = 0; run[t] = 0; }
+  __syncthreads();
+  for (int e = tid; e < E; e += 1024) atomicAdd(&cnt[env_track[e]], 1);
+  __syncthreads();
+  if (tid == 0) {
+    int b = 0;
+    for (int t = 0; t < ntr; ++t) { boff[t] = b; b += (cnt[t] + epb - 1) / epb; }
+    boff[ntr] = b;
+  }
+  __syncthreads();
+  auto track_of = [&](int b) {
+    int tr = -1;
+    for (int t = 0; t < ntr; ++t) tr = (b >= boff[t] && b < boff[t + 1]) ? t : tr;
+    return tr;
+  };
+  for (int b = tid; b < nb_cap; b += 1024) blk_track[b] = track_of(b);
+  for (int s = tid; s < nb_cap * epb; s += 1024) {   // the slots no env fills
+    const int b = s / epb, t = track_of(b);
+    if (t < 0 || s - boff[t] * epb >= cnt[t]) blk_env[s] = -1;
+  }
+  const unsigned long long below = lane ? (~0ull >> (64 - lane)) : 0ull;
+  for (int c0 = 0; c0 < E; c0 += 1024) {
+    const int e = c0 + tid;
+    const int t = e < E ? env_track[e] : -1;
+    int rk = 0;
+    for (int tt = 0; tt < ntr; ++tt) {
+      const unsigned long long mm = __ballot(t == tt);
+      if (lane == 0) woff[w][tt] = __popcll(mm);
+      if (t == tt) rk = __popcll(mm & below);
+    }
+    __syncthreads();
+    if (tid < ntr) {   // exclusive scan over the 16 waves, continuing the previous chunks' count
+      int r = run[tid];
+      for (int ww = 0; ww < 16; ++ww) { const int x = woff[ww][tid]; woff[ww][tid] = r; r += x; }
+      run[tid] = r;
+    }
+    __syncthreads();
+    if (t >= 0) blk_env[boff[t] * epb + woff[w][t] + rk] = e;
+    __syncthreads();
+  }
+  if (tid == 0) *dirty = 0;
+}
+
+// ------------------------------------------------------------------ SB3 VecEnv bookkeeping (VecCarEnv, device tensors)
+// The per-step work of SB3's Monitor + VecEnv around CarEnv.step (stable_baselines3 Monitor.step: the episode return as
+// the float64 sum of the float32 rewards, the episode length; learn/ppo.py:65-78 wraps every env in Monitor) in one
+// launch: done = terminated | truncated; the running return / length advanced, their values at this step written to
+// the caller's snapshot buffers (what info["episode"] reports for an env that finished), then zeroed for finished envs.
+__global__ void __launch_bounds__(256) vec_post_kernel(int E, int C, const float* reward, const uint8_t* env_flags,
+                                                       double* ep_ret, int64_t* ep_len, uint8_t* done, double* snap_ret,
+                                                       int64_t* snap_len) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= E) return;
+  const bool d = (env_flags[e] & (EF_TERMINATED | EF_TRUNCATED)) != 0;
+  for (int c = 0; c < C; ++c) {
+    const size_t n = (size_t)e * C + c;
+    const double r = ep_ret[n] + (double)reward[n];
+    snap_ret[n] = r;
+    ep_ret[n] = d ? 0.0 : r;
+  }
+  const int64_t l = ep_len[e] + 1;
+  snap_len[e] = l;
+  ep_len[e] = d ? 0 : l;
+  done[e] = d ? 1 : 0;
+}
+// BaseEnv action-space check (assert self.action_space.contains(action), src/car_env.py:694): any action outside
+// [-1, 1] (or NaN), or a discrete one outside {0..4}, sets *bad (read by the caller whenever it synchronises).
+__global__ void __launch_bounds__(256) action_check_kernel(int n, const void* actions, int discrete, int* bad) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  bool b;
+  if (discrete) { const int a = ((const int*)actions)[i]; b = a < 0 || a > 4; }
+  else { const float a = ((const float*)actions)[i]; b = !(a >= -1.0f && a <= 1.0f); }
+  if (b) *bad = 1;
 }
 
 // ------------------------------------------------------------------ synthetic action sources (bench)
@@ -2787,6 +2986,12 @@ struct NascarHandle {
   size_t cap_tracks = 0, cap_blocks = 0, cap_blk_env = 0;
   void* h_stage = nullptr; size_t stage_bytes = 0;
   hipEvent_t ev_stage = nullptr;
+  // random-track mode (nascar_set_random_tracks): the env -> track map, draw counters and seeds live on the device and
+  // the block map is rebuilt there (block_map_kernel) after every launch that may change a track -- no host round trip
+  int rt_on = 0, rt_ntracks = 0;
+  void* d_rt = nullptr;             // one allocation: the arrays below
+  int* d_rt_env_track = nullptr; int* d_rt_draws = nullptr; uint64_t* d_rt_seed = nullptr; int* d_rt_tracks = nullptr;
+  int* d_rt_dirty = nullptr; uint8_t* d_rt_flags = nullptr;   // flags: env flags of a step whose caller passed none
 };
 
 static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
@@ -2922,27 +3127,25 @@ extern "C" void nascar_destroy(NascarHandle* h) {
   for (auto ev : h->ev_join) hipEventDestroy(ev);
   if (h->ev_fork) hipEventDestroy(h->ev_fork);
   hipFree(h->d_ro_act);
+  hipFree(h->d_rt);
   delete h;
 }
 
 static int sensor_lds_reserve(size_t need);
-static int build_track(HostTrack& t, size_t& lds_out, const double* segments, int32_t nseg, double total_length,
-                       const double* walls, int32_t nwall, float beam_cell);
+static int host_track(HostTrack& t, const std::string& key, const double* segments, int32_t nseg, double total_length,
+                      const double* walls, int32_t nwall, float beam_cell, int* loaded = nullptr);
+static std::string track_key(const double* segments, int32_t nseg, double total_length, const double* walls,
+                             int32_t nwall, float beam_cell);
+static int upload_track(HostTrack& t, size_t& lds_out);
+static void retain_build(const std::shared_ptr<TrackBuild>& tb);
 // wall table exactly as Box2D sees it (float32 transform via glibc sinf/cosf, fat AABB, key)
 extern "C" int nascar_add_track(NascarHandle* h, const double* segments, int32_t nseg, double total_length,
                                 const double* walls, int32_t nwall) {
   if (!h || !segments || !walls) return fail("null argument");
   if (nseg < 1 || nseg > MAX_SEG) return fail("segment count %d out of range", nseg);
   if (nwall < 1) return fail("track has no walls");
-  std::string key;
-  {
-    const int32_t dims[3] = {h->cfg.device, nseg, nwall};
-    key.append((const char*)dims, sizeof dims);
-    key.append((const char*)&total_length, sizeof total_length);
-    key.append((const char*)&h->beam_cell, sizeof h->beam_cell);   // builds at different cell sizes differ
-    key.append((const char*)segments, sizeof(double) * 13 * (size_t)nseg);
-    key.append((const char*)walls, sizeof(double) * 4 * (size_t)nwall);
-  }
+  const std::string dkey = track_key(segments, nseg, total_length, walls, nwall, h->beam_cell);   // (disk cache key)
+  const std::string key = std::string((const char*)&h->cfg.device, sizeof h->cfg.device) + dkey;
   std::lock_guard<std::mutex> lk(g_track_mu);
   std::shared_ptr<TrackBuild> tb;
   {
@@ -2955,11 +3158,13 @@ extern "C" int nascar_add_track(NascarHandle* h, const double* segments, int32_t
     int cur = 0;
     HIPCHK(hipGetDevice(&cur));
     if (cur != h->cfg.device) HIPCHK(hipSetDevice(h->cfg.device));
-    const int rc = build_track(tb->t, tb->lds, segments, nseg, total_length, walls, nwall, h->beam_cell);
+    int rc = host_track(tb->t, dkey, segments, nseg, total_length, walls, nwall, h->beam_cell);
+    if (rc == 0) rc = upload_track(tb->t, tb->lds);
     if (cur != h->cfg.device) hipSetDevice(cur);
     if (rc < 0) return rc;
     g_track_cache[key] = tb;
   }
+  retain_build(tb);
   const HostTrack& t = tb->t;
   const size_t need = 2 * sizeof(float4) * t.walls.size() + sizeof(float4) * t.groups.size();
   if (need > h->max_sensor_lds) {   // on the handle's device (the attribute is per device), cached track or not
@@ -2996,9 +3201,9 @@ static int sensor_lds_reserve(size_t need) {
   }
   return 0;
 }
-// the device tables of one track (nascar_add_track, on the current device); lds: model_kernel's wall table bytes
-static int build_track(HostTrack& t, size_t& lds_out, const double* segments, int32_t nseg, double total_length,
-                       const double* walls, int32_t nwall, float beam_cell) {
+// the host tables of one track (nascar_add_track): walls as Box2D sees them, segments, grids, beam lists, wall groups
+static int host_build_track(HostTrack& t, const double* segments, int32_t nseg, double total_length,
+                            const double* walls, int32_t nwall, float beam_cell) {
   t.total_length = total_length;
   t.startline = -1; t.has_banking = 0;
   double pre = 0.0;
@@ -3041,8 +3246,14 @@ static int build_track(HostTrack& t, size_t& lds_out, const double* segments, in
     else L.key = it->second;
     t.walls.push_back(L);
   }
-  size_t lds = sizeof(LWall) * t.walls.size();
-  if (t.walls.size() > 65535) return fail("track has %d walls; the beam lists index at most 65535", nwall);
+  if (nwall > 65535) return fail("track has %d walls (grid and beam-list indices are 16-bit)", nwall);
+  build_grids(t);
+  build_beams(t, beam_cell);
+  return 0;
+}
+// the device tables of a host-built (or cache-loaded) track, on the current device; lds: model_kernel's wall table bytes.
+// The beam lists' host copies are released afterwards (the device copies are all the kernels use).
+static int upload_track(HostTrack& t, size_t& lds_out) {
   {
     std::vector<LWall> dw(t.walls.begin(), t.walls.end());
     std::vector<float4> fat(t.walls.size());
@@ -3056,10 +3267,7 @@ static int build_track(HostTrack& t, size_t& lds_out, const double* segments, in
   HIPCHK(hipMemcpy(t.d_segs, t.segs.data(), sizeof(DSeg) * t.segs.size(), hipMemcpyHostToDevice));
   HIPCHK(hipMalloc(&t.d_prefix, sizeof(double) * t.prefix.size()));
   HIPCHK(hipMemcpy(t.d_prefix, t.prefix.data(), sizeof(double) * t.prefix.size(), hipMemcpyHostToDevice));
-  if (nwall > 65535) return fail("track has %d walls (grid indices are 16-bit)", nwall);
-  build_grids(t);
   if (upload_grid(t.bp) < 0 || upload_grid(t.sn) < 0) return -1;
-  build_beams(t, beam_cell);
   if (upload_beams(t) < 0) return -1;
   HIPCHK(hipMalloc(&t.d_groups, sizeof(float4) * t.groups.size()));
   HIPCHK(hipMemcpy(t.d_groups, t.groups.data(), sizeof(float4) * t.groups.size(), hipMemcpyHostToDevice));
@@ -3074,17 +3282,155 @@ static int build_track(HostTrack& t, size_t& lds_out, const double* segments, in
     HIPCHK(hipMemcpy(t.d_swall, sw.data(), sizeof(float4) * sw.size(), hipMemcpyHostToDevice));
   }
   if (getenv("NASCAR_VERBOSE"))
-    fprintf(stderr, "nascar_add_track: %d walls, %zu groups; broadphase grid %dx%d (%zu entries), sensor grid %dx%d "
-            "(%zu entries, mean %.1f per cell)\n", nwall, t.groups.size(), t.bp.g.nx, t.bp.g.ny, t.bp.idx.size(),
+    fprintf(stderr, "nascar_add_track: %zu walls, %zu groups; broadphase grid %dx%d (%zu entries), sensor grid %dx%d "
+            "(%zu entries, mean %.1f per cell)\n", t.walls.size(), t.groups.size(), t.bp.g.nx, t.bp.g.ny, t.bp.idx.size(),
             t.sn.g.nx, t.sn.g.ny, t.sn.idx.size(), (double)t.sn.idx.size() / ((double)t.sn.g.nx * t.sn.g.ny));
   if (getenv("NASCAR_VERBOSE"))
     fprintf(stderr, "nascar_add_track: beam grid %dx%d (%.2f m cells), %zu cells with lists, %zu entries (mean %.2f per "
             "list), heads %.1f MB + continuations %.1f MB + cell map %.1f MB, built in %.2f s\n", t.beam.g.nx, t.beam.g.ny,
-            (double)beam_cell, t.beam.nlist / BEAM_NB, t.beam.entries, (double)t.beam.entries / std::max<size_t>(1, t.beam.nlist),
-            16.0 * t.beam.head.size() / 1e6, 4.0 * t.beam.ent.size() / 1e6, 4.0 * t.beam.cell.size() / 1e6, t.beam.build_s);
-  t.beam.cell.clear(); t.beam.ent.clear(); t.beam.head.clear();   // the device copies are all the kernels use
+            1.0 / (double)t.beam.g.inv_cell, t.beam.nlist / BEAM_NB, t.beam.entries,
+            (double)t.beam.entries / std::max<size_t>(1, t.beam.nlist), 16.0 * t.beam.head.size() / 1e6,
+            4.0 * t.beam.ent.size() / 1e6, 4.0 * t.beam.cell.size() / 1e6, t.beam.build_s);
+  t.beam.cell.clear(); t.beam.ent.clear(); t.beam.head.clear();
   t.beam.cell.shrink_to_fit(); t.beam.ent.shrink_to_fit(); t.beam.head.shrink_to_fit();
-  lds_out = lds;
+  lds_out = sizeof(LWall) * t.walls.size();
+  return 0;
+}
+
+// ------------------------------------------------------------------ track cache on disk (nascar_set_track_cache)
+// A host build (walls, grids and ~0.8 GB of beam lists per track at 1 m cells: ~2 s of 16 threads) written once and read
+// by every later process: ranks of one node (bench.py --gpus N, learn/ppo.py-style SubprocVecEnv runs) share one build
+// per track.  File = magic, format version, the full key (segments, walls, total length, cell size: compared byte for
+// byte on load, so a hash collision can only miss), then the host tables.  Written to a temporary name and renamed; the
+// builders of one key serialise on an flock'ed lock file, so concurrent ranks build each track once and the others load.
+static const uint32_t TRACK_FILE_VERSION = 1;
+static std::string g_cache_dir;                       // "" = no disk cache (default)
+static int g_retain = 8;                              // builds kept alive after their last handle (most recent first)
+static std::deque<std::shared_ptr<TrackBuild>>* g_retained = new std::deque<std::shared_ptr<TrackBuild>>();
+// (never destroyed: freeing device memory from a static destructor would run after the HIP runtime's own teardown)
+static void retain_build(const std::shared_ptr<TrackBuild>& tb) {   // (g_track_mu held) most recently used first
+  if (g_retain <= 0) return;
+  auto& R = *g_retained;
+  for (auto it = R.begin(); it != R.end(); ++it)
+    if (*it == tb) { R.erase(it); break; }
+  R.push_front(tb);
+  while ((int)R.size() > g_retain) R.pop_back();
+}
+
+static uint64_t fnv1a64(const std::string& s, uint64_t h) {
+  for (unsigned char c : s) { h ^= c; h *= 0x100000001B3ull; }
+  return h;
+}
+struct Sink {
+  FILE* f; bool ok = true;
+  void raw(const void* p, size_t n) { if (ok && n && fwrite(p, 1, n, f) != n) ok = false; }
+  template <class T> void pod(const T& v) { raw(&v, sizeof v); }
+  template <class T> void vec(const std::vector<T>& v) { const uint64_t n = v.size(); pod(n); raw(v.data(), n * sizeof(T)); }
+};
+struct Source {
+  FILE* f; bool ok = true;
+  void raw(void* p, size_t n) { if (ok && n && fread(p, 1, n, f) != n) ok = false; }
+  template <class T> void pod(T& v) { raw(&v, sizeof v); }
+  template <class T> void vec(std::vector<T>& v) {
+    uint64_t n = 0; pod(n);
+    if (!ok || n > ((uint64_t)1 << 40) / sizeof(T)) { ok = false; return; }
+    v.resize(n); raw(v.data(), n * sizeof(T));
+  }
+};
+template <class IO, class HT> static void track_io(IO& io, HT& t) {   // the host tables, in file order
+  io.vec(t.walls); io.vec(t.segs); io.vec(t.prefix);
+  io.pod(t.total_length); io.pod(t.startline); io.pod(t.has_banking);
+  io.pod(t.bp.g); io.vec(t.bp.start); io.vec(t.bp.idx); io.vec(t.bp.box);
+  io.pod(t.sn.g); io.vec(t.sn.start); io.vec(t.sn.idx); io.vec(t.sn.box);
+  io.pod(t.beam.g); io.vec(t.beam.cell); io.vec(t.beam.ent); io.vec(t.beam.head);
+  io.pod(t.beam.entries); io.pod(t.beam.nlist); io.pod(t.beam.build_s);
+  io.vec(t.groups);
+}
+static bool load_track_file(const std::string& path, const std::string& key, HostTrack& t) {
+  FILE* f = fopen(path.c_str(), "rb");
+  if (!f) return false;
+  Source in{f};
+  char magic[8] = {0}; uint32_t ver = 0; std::string k;
+  in.raw(magic, 8); in.pod(ver);
+  std::vector<char> kb; in.vec(kb);
+  bool ok = in.ok && !memcmp(magic, "NASCARTK", 8) && ver == TRACK_FILE_VERSION && kb.size() == key.size() &&
+            !memcmp(kb.data(), key.data(), key.size());
+  if (ok) { track_io(in, t); ok = in.ok; }
+  fclose(f);
+  if (!ok) t = HostTrack();
+  return ok;
+}
+static void save_track_file(const std::string& path, const std::string& key, HostTrack& t) {
+  const std::string tmp = path + ".tmp." + std::to_string((long)getpid());
+  FILE* f = fopen(tmp.c_str(), "wb");
+  if (!f) return;                        // (a cache that cannot be written is only slower)
+  Sink out{f};
+  out.raw("NASCARTK", 8); out.pod(TRACK_FILE_VERSION);
+  std::vector<char> kb(key.begin(), key.end()); out.vec(kb);
+  track_io(out, t);
+  const bool ok = out.ok && fclose(f) == 0;
+  if (ok) rename(tmp.c_str(), path.c_str());
+  else unlink(tmp.c_str());
+}
+// the track's inputs and the beam-list cell size (builds at different cell sizes differ): the disk cache's key
+static std::string track_key(const double* segments, int32_t nseg, double total_length, const double* walls,
+                             int32_t nwall, float beam_cell) {
+  std::string k;
+  const int32_t dims[2] = {nseg, nwall};
+  k.append((const char*)dims, sizeof dims);
+  k.append((const char*)&total_length, sizeof total_length);
+  k.append((const char*)&beam_cell, sizeof beam_cell);
+  k.append((const char*)segments, sizeof(double) * 13 * (size_t)nseg);
+  k.append((const char*)walls, sizeof(double) * 4 * (size_t)nwall);
+  return k;
+}
+// host tables of a track: from the disk cache when it holds this key (*loaded = 1), else built (and written there)
+static int host_track(HostTrack& t, const std::string& key, const double* segments, int32_t nseg, double total_length,
+                      const double* walls, int32_t nwall, float beam_cell, int* loaded) {
+  if (loaded) *loaded = 0;
+  if (g_cache_dir.empty()) return host_build_track(t, segments, nseg, total_length, walls, nwall, beam_cell);
+  char name[64];
+  snprintf(name, sizeof name, "track_%016llx%016llx.nbt", (unsigned long long)fnv1a64(key, 0xCBF29CE484222325ull),
+           (unsigned long long)fnv1a64(key, 0x84222325CBF29CE4ull));
+  const std::string path = g_cache_dir + "/" + name;
+  if (load_track_file(path, key, t)) { if (loaded) *loaded = 1; return 0; }
+  mkdir(g_cache_dir.c_str(), 0777);       // (one level; an existing directory is fine)
+  const int lk = open((path + ".lock").c_str(), O_CREAT | O_RDWR, 0666);
+  if (lk >= 0) flock(lk, LOCK_EX);       // another process may be building this key: wait for it, then load
+  int rc = 0;
+  if (lk >= 0 && load_track_file(path, key, t)) {
+    if (loaded) *loaded = 1;
+  } else {
+    rc = host_build_track(t, segments, nseg, total_length, walls, nwall, beam_cell);
+    if (rc == 0) save_track_file(path, key, t);
+  }
+  if (lk >= 0) { flock(lk, LOCK_UN); close(lk); }
+  return rc;
+}
+// host only (no device): the track's tables into the disk cache -- loaded (returns 1) when a file for this key exists,
+// else built and written (returns 0); a launcher prebuilds a job's tracks once before its ranks start
+extern "C" int nascar_prebuild_track(const double* segments, int32_t nseg, double total_length, const double* walls,
+                                     int32_t nwall, float beam_cell) {
+  if (!segments || !walls) return fail("null argument");
+  if (nseg < 1 || nseg > MAX_SEG) return fail("segment count %d out of range", nseg);
+  if (nwall < 1) return fail("track has no walls");
+  if (!(beam_cell >= BEAM_CELL_MIN && beam_cell <= BEAM_CELL_MAX))
+    return fail("beam cell size must be in [%.1f, %.1f] m, got %g", (double)BEAM_CELL_MIN, (double)BEAM_CELL_MAX, (double)beam_cell);
+  std::lock_guard<std::mutex> lk(g_track_mu);
+  if (g_cache_dir.empty()) return fail("no track cache directory (nascar_set_track_cache)");
+  HostTrack t;
+  int loaded = 0;
+  const int rc = host_track(t, track_key(segments, nseg, total_length, walls, nwall, beam_cell), segments, nseg,
+                            total_length, walls, nwall, beam_cell, &loaded);
+  return rc < 0 ? rc : loaded;
+}
+extern "C" int nascar_set_track_cache(int32_t retain, const char* dir) {
+  if (retain < 0) return fail("retain must be >= 0, got %d", retain);
+  std::lock_guard<std::mutex> lk(g_track_mu);
+  g_retain = retain;
+  while ((int)g_retained->size() > g_retain) g_retained->pop_back();
+  g_cache_dir = dir ? dir : "";
+  while (g_cache_dir.size() > 1 && g_cache_dir.back() == '/') g_cache_dir.pop_back();
   return 0;
 }
 
@@ -3092,6 +3438,7 @@ extern "C" int nascar_set_env_tracks(NascarHandle* h, const int32_t* env_track) 
   if (!h || !env_track) return fail("null argument");
   for (int e = 0; e < h->E; ++e)
     if (env_track[e] < 0 || env_track[e] >= (int)h->tracks.size()) return fail("env %d: bad track id %d", e, env_track[e]);
+  if (h->rt_on) return fail("random-track mode is on (nascar_set_random_tracks): the device draws every env's track");
   // recorded only: an env moves to its new track at its next nascar_reset, with fresh physics worlds (CarEnv.reset
   // recreates CarPhysics on a track change, src/car_env.py:375-394); until then it keeps stepping on its old track
   // (its Box2D contacts hold wall indices of that track)
@@ -3151,12 +3498,66 @@ static int prepare(NascarHandle* h, hipStream_t stream) {
   }
   // workgroups hold whole envs of one track: group envs by track, pad each group to a block
   std::vector<int> blk_track, blk_env;
-  for (int tr = 0; tr < (int)h->tracks.size(); ++tr) {
-    std::vector<int> envs;
-    for (int e = 0; e < h->E; ++e) if (h->env_track[e] == tr) envs.push_back(e);
-    for (size_t i = 0; i < envs.size(); i += h->epb) {
-      blk_track.push_back(tr);
-      for (int k = 0; k < h->epb; ++k) blk_env.push_back(i + k < envs.size() ? envs[i + k] : -1);
+  if (h->rt_on) {   // random-track mode: the device builds the map (block_map_kernel) into a fixed grid of nb_cap blocks
+    const size_t nt = td.size(), nb = (size_t)(h->E + h->epb - 1) / h->epb + nt;
+    if (nt > RT_MAX_TRACKS) return fail("random-track mode supports at most %d loaded tracks", RT_MAX_TRACKS);
+    if (nt > h->cap_tracks || nb > h->cap_blocks || nb * h->epb > h->cap_blk_env) {
+      HIPCHK(hipDeviceSynchronize());
+      if (nt > h->cap_tracks) {
+        hipFree(h->d_tracks); h->d_tracks = nullptr;
+        const size_t cap = std::max(nt, (size_t)8);
+        HIPCHK(hipMalloc(&h->d_tracks, sizeof(TrackDev) * cap));
+        h->cap_tracks = cap;
+      }
+      if (nb > h->cap_blocks || nb * h->epb > h->cap_blk_env) {
+        hipFree(h->d_blk_track); hipFree(h->d_blk_env); h->d_blk_track = h->d_blk_env = nullptr;
+        h->cap_blocks = h->cap_blk_env = 0;
+        HIPCHK(hipMalloc(&h->d_blk_track, sizeof(int) * nb));
+        HIPCHK(hipMalloc(&h->d_blk_env, sizeof(int) * nb * h->epb));
+        h->cap_blocks = nb; h->cap_blk_env = nb * h->epb;
+      }
+    }
+    const size_t b_tr = sizeof(TrackDev) * nt;
+    if (h->ev_stage) HIPCHK(hipEventSynchronize(h->ev_stage));
+    if (b_tr > h->stage_bytes) {
+      if (h->h_stage) hipHostFree(h->h_stage);
+      h->h_stage = nullptr; h->stage_bytes = 0;
+      HIPCHK(hipHostMalloc(&h->h_stage, b_tr));
+      h->stage_bytes = b_tr;
+    }
+    memcpy(h->h_stage, td.data(), b_tr);
+    HIPCHK(hipMemcpyAsync(h->d_tracks, h->h_stage, b_tr, hipMemcpyHostToDevice, stream));
+    if (!h->ev_stage) HIPCHK(hipEventCreateWithFlags(&h->ev_stage, hipEventDisableTiming));
+    HIPCHK(hipEventRecord(h->ev_stage, stream));
+    hipLaunchKernelGGL(block_map_kernel, dim3(1), dim3(1024), 0, stream, h->E, h->epb, (int)nt, h->d_rt_env_track,
+                       h->d_blk_track, h->d_blk_env, (int)nb, h->d_rt_dirty, 1);
+    HIPCHK(hipGetLastError());
+    h->nblocks = (int)nb;
+    h->map_identity = 0; h->one_track = -1;
+    h->dirty_tracks = false;
+    return 0;
+  }
+  // Each track's workgroups are spread evenly over the workgroup order (workgroup i of a track with n of them sorts at
+  // (i + 1/2) / n): the sharded rollout cuts the order into contiguous shards, and with the tracks in id order one shard
+  // held ~2 whole tracks of a mixed batch -- the shard with the tight tracks (more wall contacts and TOI events) set
+  // every rollout call's length.  Interleaved, every shard gets its share of every track.  One track: the env order.
+  {
+    std::vector<std::vector<int>> per(h->tracks.size());
+    for (int e = 0; e < h->E; ++e) per[h->env_track[e]].push_back(e);
+    struct Blk { double key; int tr, i; };
+    std::vector<Blk> order;
+    for (int tr = 0; tr < (int)per.size(); ++tr) {
+      const int nbt = (int)((per[tr].size() + h->epb - 1) / h->epb);
+      for (int i = 0; i < nbt; ++i) order.push_back({(i + 0.5) / nbt, tr, i});
+    }
+    std::stable_sort(order.begin(), order.end(), [](const Blk& a, const Blk& b) { return a.key < b.key; });
+    for (const Blk& b : order) {
+      const std::vector<int>& envs = per[b.tr];
+      blk_track.push_back(b.tr);
+      for (int k = 0; k < h->epb; ++k) {
+        const size_t j = (size_t)b.i * h->epb + k;
+        blk_env.push_back(j < envs.size() ? envs[j] : -1);
+      }
     }
   }
   const size_t nt = td.size(), nb = blk_track.size();
@@ -3301,12 +3702,39 @@ static void launch_sensors(NascarHandle* h, const Params& P, float* obs, float* 
   launch_sensors_impl(h, P, h->nblocks, obs, terminal_obs, passes, stream, sensor_impl());
 }
 
+static RtDev rt_dev(const NascarHandle* h) {
+  RtDev R;
+  R.env_track = h->d_rt_env_track; R.draws = h->d_rt_draws; R.seed = h->d_rt_seed; R.tracks = h->d_rt_tracks;
+  R.ntracks = h->rt_ntracks; R.dirty = h->d_rt_dirty;
+  return R;
+}
+// the device-side block map rebuild (random-track mode): a no-op launch unless an env changed track since the last one
+static int rt_block_map(NascarHandle* h, hipStream_t s, int force) {
+  hipLaunchKernelGGL(block_map_kernel, dim3(1), dim3(1024), 0, s, h->E, h->epb, (int)h->tracks.size(), h->d_rt_env_track,
+                     h->d_blk_track, h->d_blk_env, h->nblocks, h->d_rt_dirty, force);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+// random-track mode, after a step with auto-reset (env_flags: that step's, non-null): the reset envs draw their next
+// tracks, the switching ones are reset there (rt_switch_kernel), and the block map follows
+static int rt_after_step(NascarHandle* h, const Params& P, const uint8_t* env_flags, float* obs, hipStream_t s) {
+  hipLaunchKernelGGL(rt_switch_kernel, dim3((h->E + 63) / 64), dim3(RT_SWITCH_BLOCK), 0, s, P, rt_dev(h), env_flags, obs);
+  HIPCHK(hipGetLastError());
+  return rt_block_map(h, s, 0);
+}
+
 extern "C" int nascar_reset(NascarHandle* h, const uint8_t* env_mask, float* obs, void* stream) {
   if (!h || !obs) return fail("null argument");
   h->pristine = false;
-  if (apply_pending_tracks(h, env_mask, stream)) return -1;
+  if (!h->rt_on && apply_pending_tracks(h, env_mask, stream)) return -1;
   if (prepare(h, (hipStream_t)stream)) return -1;
   Params P = make_params(h);
+  if (h->rt_on) {   // CarEnv.reset in random-track mode: a new track per reset env first (src/car_env.py:331-333)
+    hipLaunchKernelGGL(rt_reset_draw_kernel, dim3((h->E + 255) / 256), dim3(256), 0, (hipStream_t)stream, P, rt_dev(h),
+                       env_mask);
+    HIPCHK(hipGetLastError());
+    if (rt_block_map(h, (hipStream_t)stream, 0)) return -1;
+  }
   hipLaunchKernelGGL(reset_kernel, dim3(h->nblocks), dim3(SBLOCK), 0, (hipStream_t)stream, P, env_mask, obs);
   HIPCHK(hipGetLastError());
   launch_sensors(h, P, obs, nullptr, 1, stream);
@@ -3338,13 +3766,15 @@ enum { PH_MODEL = 1, PH_LOGIC = 2, PH_SENSOR = 4, PH_ALL = 7 };
 static int launch_step_range(NascarHandle* h, const Params& P, int nb, const void* actions, int32_t discrete, int policy,
                              uint64_t seed, int64_t step, const float* obs_in, float* obs, float* reward,
                              uint8_t* car_flags, uint8_t* env_flags, int32_t auto_reset, float* terminal_obs,
-                             hipStream_t s, int phases = PH_ALL) {
+                             hipStream_t s, int phases = PH_ALL, bool model_issued = false) {
   const bool timed = h->step_ev[0] && nb == h->nblocks;   // nascar_set_step_events: whole-grid steps only
   if (h->fuse_ml) {   // model + logic in one launch (model_logic_kernel); the logic phase is part of PH_MODEL
-    // Contract: under the fused kernel the logic phase IS part of PH_MODEL's launch, so a PH_LOGIC-only request
-    // enqueues nothing -- correct only for callers that request PH_MODEL for the same step and range first, as the
-    // sharded rollout's phase-major loop does (1 << ph for ph = 0, 1, 2); nascar_step / nascar_step_driven pass
-    // PH_ALL.  A logic-only launch (the two-kernel build's logic_kernel alone) needs nascar_set_fused_logic(h, 0).
+    // Under the fused kernel the logic phase IS part of PH_MODEL's launch, so a PH_LOGIC-only request enqueues nothing:
+    // only a caller that has already requested PH_MODEL for the same step and range may make it (model_issued: the
+    // sharded rollout's phase-major loop, 1 << ph for ph = 0, 1, 2); anyone else gets an error, not a silently
+    // skipped env logic.  nascar_step / nascar_step_driven pass PH_ALL.
+    if ((phases & PH_LOGIC) && !(phases & PH_MODEL) && !model_issued)
+      return fail("the logic phase alone cannot run under the fused model + logic kernel (nascar_set_fused_logic(h, 0))");
     if (phases & PH_MODEL) {
       if (timed) HIPCHK(hipEventRecord(h->step_ev[0], s));
       hipLaunchKernelGGL(model_logic_kernel, dim3(nb), dim3(SBLOCK), MODEL_LOGIC_LDS_BYTES, s, P, actions, discrete,
@@ -3400,8 +3830,12 @@ static int step_impl(NascarHandle* h, const void* actions, int32_t discrete, int
   // Whole grid on the caller's stream: splitting one step over streams needs a fork and a join per step, and
   // the per-step barrier measured slower than one grid (tools/streams_exp.py: 2 / 4 shards 0.252 / 0.277 ms vs
   // 0.224 ms).  Shards pay off only when they run many steps unsynchronised: the sharded nascar_rollout.
-  return launch_step_range(h, P, h->nblocks, actions, discrete, policy, seed, step, obs, obs, reward, car_flags,
-                           env_flags, auto_reset, terminal_obs, (hipStream_t)stream);
+  const bool rt = h->rt_on && auto_reset;
+  uint8_t* ef = (rt && !env_flags) ? h->d_rt_flags : env_flags;
+  if (launch_step_range(h, P, h->nblocks, actions, discrete, policy, seed, step, obs, obs, reward, car_flags, ef, auto_reset,
+                        terminal_obs, (hipStream_t)stream))
+    return -1;
+  return rt ? rt_after_step(h, P, ef, obs, (hipStream_t)stream) : 0;
 }
 
 // Sharded rollout: the workgroups split into S contiguous ranges (shards of whole envs), each stepped `steps`
@@ -3420,6 +3854,8 @@ static int rollout_sharded(NascarHandle* h, int S, int32_t policy, uint64_t seed
                            float* reward, uint8_t* car_flags, uint8_t* env_flags, int32_t auto_reset, int32_t traj,
                            hipStream_t stream) {
   S = std::max(1, std::min(S, h->nblocks));
+  const bool rt = h->rt_on && auto_reset;
+  if (h->rt_on) S = 1;   // random-track mode: the block map changes between steps, so no shard owns a fixed set of envs
   const bool actor = policy == 2;
   if (actor) {
     if (!h->d_actor) return fail("policy 2 needs an actor (nascar_set_actor)");
@@ -3471,11 +3907,13 @@ static int rollout_sharded(NascarHandle* h, int S, int32_t policy, uint64_t seed
           }
           if (launch_step_range(h, P, b1 - b0, actor ? h->d_ro_act : nullptr, 0, actor ? -1 : policy, seed, step0 + k,
                                 o_in, o_out, reward + ko * NC,
-                                car_flags ? car_flags + ko * NC : nullptr, env_flags ? env_flags + ko * E : nullptr,
-                                auto_reset, nullptr, shard_stream(s), 1 << ph))
+                                car_flags ? car_flags + ko * NC : nullptr,
+                                env_flags ? env_flags + ko * E : (rt ? h->d_rt_flags : nullptr),
+                                auto_reset, nullptr, shard_stream(s), 1 << ph, ph == 1))
             return -1;
         }
       }
+      if (rt && rt_after_step(h, P0, env_flags ? env_flags + ko * E : h->d_rt_flags, o_out, stream)) return -1;
     }
     return 0;
   };
@@ -3505,6 +3943,8 @@ extern "C" int nascar_rollout(NascarHandle* h, int32_t policy, uint64_t seed, in
   if (!h || !obs || !reward) return fail("null argument");
   if (policy < 0 || policy > 3) return fail("rollout policy must be 0, 1, 2 or 3 (got %d)", policy);
   if (policy == 2 && h->ro_streams == 0) return fail("the fused rollout kernel has no actor (policy 2): use the sharded rollout");
+  if (h->rt_on && h->ro_streams == 0)
+    return fail("random-track mode needs the sharded rollout (rollout streams >= 1): the fused kernel keeps one block map");
   if (traj & ~(NASCAR_TRAJ_RECORDS | NASCAR_TRAJ_OBS)) return fail("unknown trajectory flags 0x%x", traj);
   if ((traj & NASCAR_TRAJ_OBS) && !(traj & NASCAR_TRAJ_RECORDS)) return fail("an obs trajectory needs the per-step records (traj bit 0)");
   if ((traj & NASCAR_TRAJ_OBS) && h->ro_streams == 0) return fail("obs trajectories need the sharded rollout (rollout streams >= 1)");
@@ -3536,6 +3976,95 @@ extern "C" int nascar_get_info(NascarHandle* h, double* info, void* stream) {
   if (prepare(h, (hipStream_t)stream)) return -1;
   Params P = make_params(h);
   hipLaunchKernelGGL(info_kernel, dim3(h->nblocks), dim3(SBLOCK), 0, (hipStream_t)stream, P, info);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+// ------------------------------------------------------------------ random-track mode (host side)
+extern "C" int nascar_track_draw(int32_t n, const uint64_t* seeds, const int32_t* k, const int32_t* current,
+                                 const int32_t* tracks, int32_t ntracks, int32_t* out) {
+  if (n < 0 || (n > 0 && (!seeds || !k || !current || !out)) || (ntracks > 0 && !tracks)) return fail("bad argument");
+  for (int32_t i = 0; i < n; ++i) out[i] = rt_draw(seeds[i], k[i], current[i], tracks, ntracks);
+  return 0;
+}
+extern "C" int nascar_set_random_tracks(NascarHandle* h, const int32_t* tracks, int32_t ntracks, const uint64_t* seeds,
+                                        const int32_t* draws, void* stream) {
+  if (!h) return fail("null argument");
+  const hipStream_t s = (hipStream_t)stream;
+  const size_t E = (size_t)h->E;
+  if (ntracks == 0) {   // off: the device's assignment becomes the host's, the host builds the block map again
+    if (h->rt_on) {
+      std::vector<int> et(E);
+      HIPCHK(hipMemcpyAsync(et.data(), h->d_rt_env_track, sizeof(int) * E, hipMemcpyDeviceToHost, s));
+      HIPCHK(hipStreamSynchronize(s));
+      h->env_track = et;
+      h->rt_on = 0; h->rt_ntracks = 0; h->dirty_tracks = true;
+    }
+    return 0;
+  }
+  if (!tracks || !seeds) return fail("null argument");
+  if (ntracks < 0 || ntracks > RT_MAX_TRACKS) return fail("random tracks: %d ids (at most %d)", ntracks, RT_MAX_TRACKS);
+  if ((int)h->tracks.size() > RT_MAX_TRACKS) return fail("random-track mode supports at most %d loaded tracks", RT_MAX_TRACKS);
+  for (int i = 0; i < ntracks; ++i) {
+    if (tracks[i] < 0 || tracks[i] >= (int)h->tracks.size()) return fail("random tracks: bad track id %d", tracks[i]);
+    for (int j = 0; j < i; ++j) if (tracks[j] == tracks[i]) return fail("random tracks: track id %d listed twice", tracks[i]);
+  }
+  if (draws) for (size_t e = 0; e < E; ++e) if (draws[e] < 0) return fail("env %zu: negative draw count", e);
+  if (!h->pending_track.empty()) {
+    for (size_t e = 0; e < E; ++e)
+      if (h->pending_track[e] != h->env_track[e])
+        return fail("env %zu has a track change pending (nascar_set_env_tracks): reset it before random-track mode", e);
+    h->pending_track.clear();
+  }
+  if (!h->d_rt) {
+    const size_t o_dr = align256(sizeof(int) * E), o_sd = o_dr + align256(sizeof(int) * E),
+                 o_tr = o_sd + align256(sizeof(uint64_t) * E), o_dy = o_tr + align256(sizeof(int) * RT_MAX_TRACKS),
+                 o_fl = o_dy + 256, total = o_fl + align256(E);
+    HIPCHK(hipMalloc(&h->d_rt, total));
+    HIPCHK(hipMemsetAsync(h->d_rt, 0, total, s));
+    char* b = (char*)h->d_rt;
+    h->d_rt_env_track = (int*)b; h->d_rt_draws = (int*)(b + o_dr); h->d_rt_seed = (uint64_t*)(b + o_sd);
+    h->d_rt_tracks = (int*)(b + o_tr); h->d_rt_dirty = (int*)(b + o_dy); h->d_rt_flags = (uint8_t*)(b + o_fl);
+  }
+  std::vector<int> dr(E, 0);
+  if (draws) for (size_t e = 0; e < E; ++e) dr[e] = draws[e];
+  if (!h->rt_on) HIPCHK(hipMemcpyAsync(h->d_rt_env_track, h->env_track.data(), sizeof(int) * E, hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(h->d_rt_draws, dr.data(), sizeof(int) * E, hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(h->d_rt_seed, seeds, sizeof(uint64_t) * E, hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(h->d_rt_tracks, tracks, sizeof(int) * ntracks, hipMemcpyHostToDevice, s));
+  HIPCHK(hipStreamSynchronize(s));   // (pageable, caller-owned host arrays)
+  h->rt_on = 1; h->rt_ntracks = ntracks; h->dirty_tracks = true;
+  return 0;
+}
+extern "C" int nascar_get_env_tracks(NascarHandle* h, int32_t* env_track, int32_t* draws, void* stream) {
+  if (!h) return fail("null argument");
+  const hipStream_t s = (hipStream_t)stream;
+  const size_t bytes = sizeof(int) * (size_t)h->E;
+  if (h->rt_on) {
+    if (env_track) HIPCHK(hipMemcpyAsync(env_track, h->d_rt_env_track, bytes, hipMemcpyDeviceToDevice, s));
+    if (draws) HIPCHK(hipMemcpyAsync(draws, h->d_rt_draws, bytes, hipMemcpyDeviceToDevice, s));
+    return 0;
+  }
+  if (env_track) {
+    HIPCHK(hipMemcpyAsync(env_track, h->env_track.data(), bytes, hipMemcpyHostToDevice, s));
+    HIPCHK(hipStreamSynchronize(s));
+  }
+  if (draws) HIPCHK(hipMemsetAsync(draws, 0, bytes, s));
+  return 0;
+}
+extern "C" int nascar_vec_post(NascarHandle* h, const float* reward, const uint8_t* env_flags, double* ep_ret,
+                               int64_t* ep_len, uint8_t* done, double* snap_ret, int64_t* snap_len, void* stream) {
+  if (!h || !reward || !env_flags || !ep_ret || !ep_len || !done || !snap_ret || !snap_len) return fail("null argument");
+  hipLaunchKernelGGL(vec_post_kernel, dim3((h->E + 255) / 256), dim3(256), 0, (hipStream_t)stream, h->E, h->C, reward,
+                     env_flags, ep_ret, ep_len, done, snap_ret, snap_len);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+extern "C" int nascar_check_actions(NascarHandle* h, const void* actions, int32_t discrete, int32_t* bad, void* stream) {
+  if (!h || !actions || !bad) return fail("null argument");
+  const int n = h->N * (discrete ? 1 : 2);
+  hipLaunchKernelGGL(action_check_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, n, actions,
+                     (int)(discrete != 0), bad);
   HIPCHK(hipGetLastError());
   return 0;
 }

@@ -122,8 +122,9 @@ __host__ __device__ inline void glibc_sincosf(float y, float* sp, float* cp) {
   // reduce_fast's n = 0 case (x - 0 * pi/2 == x exactly, sign +1, first table row), and both polynomials are
   // evaluated side by side and assigned by the quadrant's parity (glibc evaluates the same two polynomials on the
   // same values), so the dependent chain is one polynomial deep instead of two plus branches.  |y| < 2^-12 returns
-  // (y, 1) as glibc does (also keeping sin(-0) = -0).  Bit-identical to the branchy form over all 2^32 floats
-  // (tests/test_sincos_cpu.py).
+  // (y, 1) as glibc does (also keeping sin(-0) = -0).  Bit-identical to the host glibc over all 2^32 floats
+  // (tests/test_rays_cpu.py::test_glibc_sincosf_restatement_matches_host_libm: every 61st pattern by default,
+  // every pattern with NASCAR_SINCOS_STRIDE=1: 4 278 190 080 finite floats, 0 mismatches, 26 s on 8 threads).
   const uint32_t t = top12(y);
   if (t >= top12(120.0f)) {
     uint32_t xi = f_as_u(y);

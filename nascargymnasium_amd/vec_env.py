@@ -9,14 +9,16 @@ launch, and the final observation of a finished episode is returned in
 
 ``track_file=None`` is the reference's random-track mode (``CarEnv(track_file=None)``,
 src/car_env.py:243-303, 331-398, as learn/ppo.py:67-72 trains): every env draws a new
-track at each reset -- any bundled track but the one it just drove -- from its own
-generator, seeded ``seed + env index`` (``seed()``), as SB3 seeds sub-envs.  Finished
-envs are then reset after the step (their workgroups regroup by track between launches)
-instead of inside it, since one workgroup never mixes tracks.
+track at each reset -- any bundled track but the one it just drove -- keyed by its own
+seed, ``seed + env index`` (``seed()``, as SB3 seeds sub-envs).  The draws, the fresh
+worlds on the new track and the regrouping of the workgroups by track all happen on the
+device, in the auto-reset of the step launch and two small kernels after it
+(``BatchedCarEnv.set_random_tracks``): a step makes no host round trip in either mode.
 
 ``return_tensors=False`` (default) returns numpy arrays like an SB3 VecEnv;
 ``return_tensors=True`` keeps obs / rewards / dones on the device and makes no host
-synchronisation per step in single-track mode: actions are validated on the device
+synchronisation per step: each step writes fresh output tensors (no copies), SB3
+Monitor's episode bookkeeping runs in one device launch, actions are validated on the device
 (an invalid action raises AssertionError, as the reference's ``assert
 self.action_space.contains(action)``, src/car_env.py:694, at the next point that reads
 the host: ``infos``, ``reset``, ``check_actions()``, or at the latest ``check_every``
@@ -24,6 +26,7 @@ steps later -- one small host read per ``check_every`` steps), and ``infos`` is 
 built from device copies the first time it is read.  The env state after an invalid
 action is undefined (the reference never steps one).
 """
+import ctypes
 import random
 import time
 from collections import deque
@@ -90,67 +93,85 @@ class VecCarEnv:
         self.return_tensors = return_tensors
         self.random_tracks = track_file is None
         self._tracks = available_tracks()
-        self.seed(seed)
         if self.random_tracks:
-            # CarEnv.__init__ in random mode picks a track (src/car_env.py:158-163); reset() draws again
-            self.env_tracks = [self._rngs[e].choice(self._tracks) for e in range(self.num_envs)]
-            files = self.env_tracks
+            files = [self._tracks[0]] * self.num_envs      # replaced by each env's first draw in seed() below
+            self._env_tracks = None
         else:
             files = track_file
-            self.env_tracks = ([track_path(track_file)] * self.num_envs if isinstance(track_file, str)
-                               else [track_path(f) for f in track_file])
+            self._env_tracks = ([track_path(track_file)] * self.num_envs if isinstance(track_file, str)
+                                else [track_path(f) for f in track_file])
         self.engine = BatchedCarEnv(self.num_envs, self.num_cars, files, reset_on_lap=reset_on_lap, device=device)
         self.device = self.engine.device
+        self._L, self._h = self.engine.L, self.engine.h
+        if self.random_tracks:
+            self._ids = np.array([self.engine._add_track(f) for f in self._tracks], np.int32)
         self._actions = None
+        self._discrete_actions = 0
         self._t0 = time.time()
         self._ep_ret = torch.zeros(self.num_envs, self.num_cars, dtype=torch.float64, device=self.device)
         self._ep_len = torch.zeros(self.num_envs, dtype=torch.int64, device=self.device)
-        self._bad = torch.zeros((), dtype=torch.bool, device=self.device)    # invalid action seen (device flag)
+        self._bad = torch.zeros((), dtype=torch.int32, device=self.device)   # invalid action seen (device flag)
         self.check_every = max(1, int(check_every))   # return_tensors: read the flag at least this often
         self._unchecked = 0
         self._attrs = [dict() for _ in range(self.num_envs)]
-        # per env, the tracks of its last 64 episodes (random-track mode)
-        self.episode_tracks = [deque(maxlen=64) for _ in range(self.num_envs)]
+        self.seed(seed)
 
     # ------------------------------------------------------------------ random-track mode (src/car_env.py:243-303)
-    def _draw_track(self, e: int) -> str:
-        """CarEnv._select_random_track: any bundled track but the current one, from env e's generator."""
-        cands = self._tracks
-        if len(cands) > 1 and self.env_tracks[e] in cands:
-            cands = [t for t in cands if t != self.env_tracks[e]]
-        return self._rngs[e].choice(cands)
+    @property
+    def env_tracks(self) -> List[str]:
+        """the .track file each env is on (random-track mode: read from the device)"""
+        return self.engine.env_track_files() if self.random_tracks else list(self._env_tracks)
 
-    def _redraw(self, envs):
-        for e in envs:
-            self.env_tracks[e] = self._draw_track(e)
-        self.engine.set_env_tracks(self.env_tracks)     # applied by the masked reset that follows
+    @property
+    def episode_tracks(self) -> List[deque]:
+        """random-track mode: per env, the tracks of its last (up to 64) episodes since it was seeded, the current one
+        last -- replayed on the host from its seed and the device's draw count (draw k: _lib.track_draw)."""
+        out = [deque(maxlen=64) for _ in range(self.num_envs)]
+        if not self.random_tracks:
+            return out
+        ids, draws = self.engine.env_track_ids()
+        cur = self._seq_t0.copy()
+        for k in range(int(self._seq_k0.min()), int(draws.max()) if draws.size else 0):
+            live = (self._seq_k0 <= k) & (k < draws)
+            if not live.any():
+                continue
+            nxt = _lib.track_draw(self._seeds, k, cur, self._ids)
+            cur = np.where(live, nxt, cur)
+            for e in np.nonzero(live)[0]:
+                out[e].append(self.engine._track_files_by_id[int(cur[e])])
+        assert np.array_equal(cur, ids), "random-track replay disagrees with the device"
+        return out
 
     # ------------------------------------------------------------------ SB3 VecEnv API
     def reset(self):
         self.check_actions()
-        if self.random_tracks:
-            self._redraw(range(self.num_envs))
-        obs = self.engine.reset()
-        if self.random_tracks:
-            for e in range(self.num_envs):
-                self.episode_tracks[e].append(self.env_tracks[e])
+        obs = self.engine.reset()     # random-track mode: every env draws its next track on the device first
         self._ep_ret.zero_()
         self._ep_len.zero_()
         return self._out(obs.clone())
 
     def step_async(self, actions):
         torch = self._torch
-        a = actions.to(self.device) if isinstance(actions, torch.Tensor) else \
-            torch.as_tensor(np.asarray(actions), device=self.device)
-        if self.discrete_action_space:
-            a = a.reshape(self.num_envs, self.num_cars)
-            bad = (a < 0) | (a > 4) | (a != a.trunc()) if a.is_floating_point() else (a < 0) | (a > 4)
-            a = a.to(torch.int32)
+        if isinstance(actions, torch.Tensor):
+            a = actions if actions.device == self.device else actions.to(self.device)
         else:
-            a = a.to(torch.float32).reshape(self.num_envs, self.num_cars, 2)
-            bad = (a < -1) | (a > 1) | torch.isnan(a)
-        self._bad |= bad.any()             # device-side check, read at the next host synchronisation
-        self._actions = a.contiguous()
+            a = torch.as_tensor(np.asarray(actions), device=self.device)
+        E, C = self.num_envs, self.num_cars
+        if self.discrete_action_space:
+            a = a.reshape(E, C)
+            if a.dtype != torch.int32:     # checked before the conversion (a float 2.5 or an int64 2**32 + 1 is invalid)
+                bad = (a < 0) | (a > 4) | (a != a.trunc()) if a.is_floating_point() else (a < 0) | (a > 4)
+                self._bad |= bad.any().to(torch.int32)
+                a = a.to(torch.int32)
+        else:
+            a = a.reshape(E, C, 2)
+            if a.dtype != torch.float32:
+                a = a.to(torch.float32)
+        if not a.is_contiguous():
+            a = a.contiguous()
+        self._discrete_actions = int(self.discrete_action_space)
+        self._on_device(self._launch_check, a)    # range / NaN check on the device (action_check_kernel)
+        self._actions = a
         self._unchecked += 1
         if not self.return_tensors or self._unchecked >= self.check_every:
             self.check_actions()
@@ -159,7 +180,7 @@ class VecCarEnv:
         """Raise AssertionError (the reference's `assert self.action_space.contains(action)`, src/car_env.py:694)
         if any action handed to step_async since the last check was outside the action space."""
         self._unchecked = 0
-        if bool(self._bad):
+        if int(self._bad.item()):
             self._bad.zero_()
             raise AssertionError("Invalid action: continuous actions must be in [-1, 1], discrete in {0..4}")
 
@@ -167,54 +188,54 @@ class VecCarEnv:
         if self._actions is None:
             raise RuntimeError("step_async() must be called before step_wait()")
         torch = self._torch
-        eng = self.engine
-        auto = not self.random_tracks
-        obs, rew, term, trunc = eng.step(self._actions, auto_reset=auto, terminal_obs=auto)
+        E, C, dev = self.num_envs, self.num_cars, self.device
+        # fresh output tensors written by the step launch itself (the caller may keep them)
+        obs = torch.empty(E, C, 38, dtype=torch.float32, device=dev)
+        tobs = torch.empty(E, C, 38, dtype=torch.float32, device=dev)
+        rew = torch.empty(E, C, dtype=torch.float32, device=dev)
+        ef = torch.empty(E, dtype=torch.uint8, device=dev)
+        done = torch.empty(E, dtype=torch.bool, device=dev)
+        sret = torch.empty(E, C, dtype=torch.float64, device=dev)
+        slen = torch.empty(E, dtype=torch.int64, device=dev)
+        self._on_device(self._launch_step, obs, tobs, rew, ef, done, sret, slen)
         self._actions = None
-        done = term | trunc
-        self._ep_ret += rew.to(torch.float64)
-        self._ep_len += 1
         now = round(time.time() - self._t0, 6)
-        if self.random_tracks:
-            # host sync: the finished envs draw their next tracks, then a masked reset moves them there
-            done_np = done.cpu().numpy()
-            idx = np.nonzero(done_np)[0].tolist()
-            snap = self._snapshot(idx, eng.obs, term, trunc)
-            if idx:
-                self._redraw(idx)
-                eng.reset(done.to(torch.uint8))
-                for e in idx:
-                    self.episode_tracks[e].append(self.env_tracks[e])
-            infos = self._infos(snap, now)
-        elif self.return_tensors:
-            # no host sync: device copies of what the finished envs' infos need, materialised on first read
-            snap = (done.clone(), eng.terminal_obs.clone(), self._ep_ret.clone(), self._ep_len.clone(), term.clone(),
-                    trunc.clone(), eng.termination_reason().clone())
-            infos = _LazyInfos(lambda: self._infos(self._snapshot_dev(*snap), now))
-        else:
-            idx = torch.nonzero(done).flatten().tolist()
-            infos = self._infos(self._snapshot(idx, eng.terminal_obs, term, trunc), now)
-        self._ep_ret.masked_fill_(done[:, None], 0.0)     # masked fills: no host sync
-        self._ep_len.masked_fill_(done, 0)
-        if self.return_tensors:
-            r = rew if self.num_cars > 1 else rew[:, 0]
-            return self._out(obs.clone()), r.clone(), done.clone(), infos
+        snap = (done, tobs, sret, slen, ef)
+        if self.return_tensors:    # no host sync: the infos are built from these tensors the first time they are read
+            infos = _LazyInfos(lambda: self._infos(self._snapshot(*snap, check=True), now))
+            return self._out(obs), (rew if C > 1 else rew[:, 0]), done, infos
+        infos = self._infos(self._snapshot(*snap), now)
         r = rew.cpu().numpy()
-        return self._out(obs), (r if self.num_cars > 1 else r[:, 0]), done.cpu().numpy(), infos
+        return self._out(obs), (r if C > 1 else r[:, 0]), done.cpu().numpy(), infos
 
-    def _snapshot(self, idx, term_obs, term, trunc):
-        if not idx:
-            return idx, None, None, None, None, None, None
-        return (idx, term_obs[idx].cpu().numpy(), self._ep_ret[idx].cpu().numpy(), self._ep_len[idx].cpu().numpy(),
-                term[idx].cpu().numpy(), trunc[idx].cpu().numpy(), self.engine.termination_reason()[idx].cpu().numpy())
+    def _on_device(self, fn, *args):
+        """fn(stream, *args) with the env's device current (switched, and back, only when another one is)"""
+        torch = self._torch
+        if torch.cuda.current_device() == self.device.index:
+            return fn(ctypes.c_void_p(torch.cuda.current_stream().cuda_stream), *args)
+        with torch.cuda.device(self.device):
+            return fn(ctypes.c_void_p(torch.cuda.current_stream().cuda_stream), *args)
 
-    def _snapshot_dev(self, done, term_obs, ret, length, term, trunc, reason):
-        self.check_actions()
+    def _launch_check(self, st, a):
+        _lib.check(self._L.nascar_check_actions(self._h, a.data_ptr(), self._discrete_actions, self._bad.data_ptr(), st))
+
+    def _launch_step(self, st, obs, tobs, rew, ef, done, sret, slen):
+        # CarEnv.step with SB3-style auto-reset in the launch (random-track mode: new tracks on the device too)
+        _lib.check(self._L.nascar_step(self._h, self._actions.data_ptr(), self._discrete_actions, obs.data_ptr(),
+                                       rew.data_ptr(), None, ef.data_ptr(), 1, tobs.data_ptr(), st))
+        # Monitor / VecEnv bookkeeping: done, episode return and length (vec_post_kernel)
+        _lib.check(self._L.nascar_vec_post(self._h, rew.data_ptr(), ef.data_ptr(), self._ep_ret.data_ptr(),
+                                           self._ep_len.data_ptr(), done.data_ptr(), sret.data_ptr(), slen.data_ptr(), st))
+
+    def _snapshot(self, done, tobs, ret, length, ef, check=False):
+        if check:
+            self.check_actions()
         idx = self._torch.nonzero(done).flatten().tolist()
         if not idx:
             return idx, None, None, None, None, None, None
-        return (idx, term_obs[idx].cpu().numpy(), ret[idx].cpu().numpy(), length[idx].cpu().numpy(),
-                term[idx].cpu().numpy(), trunc[idx].cpu().numpy(), reason[idx].cpu().numpy())
+        f = ef[idx].cpu().numpy()
+        return (idx, tobs[idx].cpu().numpy(), ret[idx].cpu().numpy(), length[idx].cpu().numpy(),
+                (f & 1) != 0, (f & 2) != 0, (f >> 4) & 7)
 
     def _infos(self, snap, now):
         idx, tobs, rets, lens, te, tr, reasons = snap
@@ -241,11 +262,33 @@ class VecCarEnv:
 
     # ------------------------------------------------------------------ the rest of SB3's VecEnv surface
     def seed(self, seed: Optional[int] = None) -> list:
-        """SB3 VecEnv.seed: sub-env i is seeded seed + i (the generators of the random-track draws)."""
+        """SB3 VecEnv.seed: sub-env i is seeded seed + i -- in random-track mode the key of its track draws (its next
+        reset takes draw 0 of the new seed; at construction each env's first track is draw 0, as CarEnv.__init__
+        picks one, src/car_env.py:158-163, and the first reset takes draw 1)."""
         if seed is None:
             seed = random.randint(0, 2 ** 31 - 1)
-        self._rngs = [random.Random(seed + e) for e in range(self.num_envs)]
-        return [seed + e for e in range(self.num_envs)]
+        seeds = [seed + e for e in range(self.num_envs)]
+        if self.random_tracks:
+            self._set_seeds(np.array(seeds, np.uint64), None)
+        return seeds
+
+    def _set_seeds(self, seeds, envs):
+        """(re)key the random-track draws: all envs (envs None) or the listed ones restart their draw counters"""
+        eng = self.engine
+        if eng.random_track_ids is None:    # construction: each env's first track is draw 0 (applied at once)
+            first = _lib.track_draw(seeds, 0, -1, self._ids)
+            eng.set_env_tracks([eng._track_files_by_id[int(t)] for t in first])
+            self._seeds, self._seq_k0, self._seq_t0 = seeds.copy(), np.ones(self.num_envs, np.int64), first.copy()
+            eng.set_random_tracks(self._tracks, self._seeds, draws=1)
+            return
+        ids, draws = eng.env_track_ids()
+        sel = np.arange(self.num_envs) if envs is None else np.asarray(envs, np.int64)
+        self._seeds[sel] = seeds[sel] if envs is None else seeds
+        draws = draws.astype(np.int64)
+        draws[sel] = 0
+        self._seq_k0[sel] = 0
+        self._seq_t0[sel] = ids[sel]
+        eng.set_random_tracks(self._tracks, self._seeds, draws=draws.astype(np.int32))
 
     def _indices(self, indices):
         if indices is None:
@@ -254,11 +297,12 @@ class VecCarEnv:
 
     def get_attr(self, name, indices=None):
         out = []
+        tracks = self.env_tracks if name == "track_file" else None
         for e in self._indices(indices):
             if name in self._attrs[e]:
                 out.append(self._attrs[e][name])
             elif name == "track_file":
-                out.append(self.env_tracks[e])
+                out.append(tracks[e])
             else:
                 out.append(getattr(self, name))
         return out
@@ -275,7 +319,11 @@ class VecCarEnv:
         return [fn(e, *args, **kwargs) for e in self._indices(indices)]
 
     def _env_seed(self, e, seed_value=None):
-        self._rngs[e] = random.Random(seed_value)
+        """CarEnv.seed on sub-env e: re-keys its random-track draws (random.Random(seed_value) in the reference's spirit)"""
+        if seed_value is None:
+            seed_value = random.randint(0, 2 ** 31 - 1)
+        if self.random_tracks:
+            self._set_seeds(np.array([seed_value], np.uint64), [e])
         return [seed_value]
 
     def _env_render(self, e, *a, **k):

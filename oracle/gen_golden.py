@@ -25,6 +25,9 @@ import types
 
 import numpy as np
 
+# the reference's modules are imported from /root/reference (read-only): never leave bytecode there
+sys.dont_write_bytecode = True
+
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 sys.path.insert(0, os.path.join(ROOT, "tests"))

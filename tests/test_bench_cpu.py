@@ -1,4 +1,6 @@
 """Host logic of bench.py and the host restatement of the device action sources (no GPU)."""
+import os
+
 import numpy as np
 import pytest
 
@@ -96,11 +98,12 @@ def test_gpus_n_runs_main_on_n_ranks(gather):
     assert seq[:4] == ["barrier"] * 4
     assert seq[4:9] == ["all_gather[1]", "all_reduce_max[2]", "all_reduce_max[2]", "all_reduce_max[1]",
                         "all_reduce_sum[7]"], seq
+    cache = ["all_gather[1]"] * 3      # the per-rank track-cache statistics (multi-rank runs), after every window
     if gather:
-        assert len(seq) == 9 and "uniform_from_reset" not in d
+        assert seq[9:] == cache and "uniform_from_reset" not in d
         assert "RCCL gather" in d["config"]["parallelism"]
     else:   # the secondary pass: its own barrier-bracketed window and MAX
-        assert seq[9:] == ["barrier", "barrier", "all_reduce_max[1]"], seq
+        assert seq[9:] == ["barrier", "barrier", "all_reduce_max[1]"] + cache, seq
         assert d["uniform_from_reset"]["ms_per_step"] >= 2.0
     assert set(d["roofline"]["kernel_times_ms"]) == {"model_logic_kernel", "ray_sensor_kernel"}
     assert d["per_step"]["ms_per_step"] >= 2.0
@@ -146,3 +149,26 @@ def test_host_driver_global_ids_match_the_device_keys():
     obs[:, 22] = 1.0
     a = d.actions(obs, step)
     assert np.array_equal(a[fm[ids]], full[ids][fm[ids]])
+
+
+def test_mixed_multi_rank_track_cache(tmp_path):
+    """Multi-rank startup over all 8 tracks (cfg5's batch; verdict r05 item 5): `bench.py --gpus 2 --plumbing --mixed`
+    on gloo, both ranks prebuilding the 8 tracks into one on-disk track cache (rotated orders, a lock file per track):
+    every track is built exactly once across the ranks and loaded by the other; a second job on the same cache builds
+    nothing and each rank's tracks load in a fraction of the build time.  (Coarse 8 m beam cells keep the CPU test
+    small; the file format and the locking do not depend on it.)"""
+    import json
+    cache = str(tmp_path / "tracks")
+    args = ["--gpus", "2", "--plumbing", "--mixed", "--beam-cell", "8", "--steps", "2", "--warmup", "1", "--envs", "16",
+            "--cars", "2", "--settle", "2", "--no-secondary"]
+    runs = []
+    for _ in range(2):
+        r = _bench(args, env={"NASCAR_TRACK_CACHE": cache})
+        assert r.returncode == 0, r.stderr[-3000:]
+        runs.append(json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])["track_cache"])
+    first, second = runs
+    assert first["dir"] == cache
+    assert sum(first["built"]) == 8 and sum(first["loaded"]) == 8, first      # each track built once, loaded once
+    assert sum(second["built"]) == 0 and second["loaded"] == [8, 8], second
+    assert max(second["prebuild_s"]) < 3.0 and max(second["prebuild_s"]) < max(first["prebuild_s"]), (first, second)
+    assert len([f for f in os.listdir(cache) if f.endswith(".nbt")]) == 8

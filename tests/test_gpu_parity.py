@@ -122,10 +122,12 @@ def _random_actions(rng, E, C, k):
 def test_random_batch_vs_oracle(track, E, C, steps):
     """Seeded random driving (crashes, disables, stuck cars) on E x C cars: GPU == CPU oracle, every step, at one
     env per workgroup and at the most envs a workgroup holds (128 // C: e.g. daytona 64 x 4 at 32 envs per
-    workgroup), the same actions into both engines."""
+    workgroup), the same actions into both engines; at cfg4's car count also at 16 envs per workgroup, the layout
+    the engine picks for cfg4's rank (8192 x 4: 512 workgroups, profiles/r05_sweep.jsonl)."""
     from oracle_lib import OracleEnv
     rng = np.random.default_rng(hash(track) % 2**32)
-    envs = [_env(track, E, C, envs_per_block=epb) for epb in (1, 128 // C)]
+    layouts = sorted({1, 128 // C} | ({16} if (track, C) == ("daytona.track", 4) else set()))
+    envs = [_env(track, E, C, envs_per_block=epb) for epb in layouts]
     orc = OracleEnv(os.path.join(TRACKS, track), E, C)
     o = orc.reset()[0]
     for env in envs:

@@ -36,13 +36,16 @@ def _per_step(env, policy, seed, step0, K):
     # 12 envs per workgroup: 2 track groups of 250 envs = 2 x 21 workgroups (the last of each with 10 envs), 3 uneven
     # shards of 14 workgroups
     (["daytona.track", "nascar.track"], 500, 10, 3, 1200, 200, 12),
+    # cfg5's kind of batch: all 8 tracks, 72 envs each = 6 workgroups of 12 per track, interleaved over 4 shards
+    (["daytona.track", "martinsville.track", "michigan.track", "nascar.track", "nascar2.track", "nascar_banked.track",
+      "talladega.track", "trioval.track"], 576, 10, 3, 600, 150, 12),
 ])
 def test_rollout_equals_per_step(tracks, E, C, policy, warm, K, epb, streams):
     """the per-step path at the automatic layout (one env per workgroup for these batch sizes) against the
     rollout at `epb` envs per workgroup: the same results whatever the schedule and the layout"""
     rol = policy == 0
     a, b = _engine(tracks, E, C, rol), _engine(tracks, E, C, rol, envs_per_block=epb)
-    b.set_rollout_streams(streams if E < 500 or streams == 0 else 3)
+    b.set_rollout_streams(streams if E != 500 or streams == 0 else 3)
     a.reset()
     if warm:                                    # leave the reset state first (cars spread, contacts active)
         a.rollout(policy, warm, seed=5, step0=0, auto_reset=True)

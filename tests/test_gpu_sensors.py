@@ -11,6 +11,8 @@ poses, ~500 k rays), with the CPU oracle's brute-force b2PolygonShape::RayCast o
 import ctypes
 import math
 import os
+import subprocess
+import sys
 import zlib
 
 import numpy as np
@@ -218,3 +220,36 @@ def test_sensor_workgroup_sizes_identical():
     for k in ("64", "256", "512", "1024", "lpc4"):
         bad = np.argwhere(out[k].view(np.uint32) != out["128"].view(np.uint32))
         assert len(bad) == 0, f"{k} differs from 128-thread workgroups at {bad[:5].tolist()}"
+
+
+def test_coop_walk_round_cap_fallback(tmp_path):
+    """ray_walk_coop hands a ray still walking after RAY_COOP_ROUNDS rounds to its own lane (ray_walk_rest); no bundled
+    list gets there in the product build (1024 rounds).  The tools build with a cap of 1 round
+    (tools/build/libnascar_coop1.so, __graft_entry__.build) sends every walk longer than the heads plus one round down
+    that branch; on martinsville (the tightest track: the longest walks) and on the many-walls track its sensor values
+    equal the product build's and the wall-group kernel's on every pose, bit for bit (16 lanes per car)."""
+    from nascargymnasium_amd.batched import BatchedCarEnv
+    from nascargymnasium_amd.track import build_walls, load_track
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    variant = os.path.join(root, "tools", "build", "libnascar_coop1.so")
+    assert os.path.exists(variant), "build() builds the RAY_COOP_ROUNDS=1 test variant"
+    many = str(tmp_path / "many_walls.track")
+    with open(many, "w") as f:
+        f.write(MANY_WALLS_TRACK)
+    for path, E, C in ((os.path.join(TRACKS, "martinsville.track"), 512, 8), (many, 256, 4)):
+        rng = np.random.default_rng(99)
+        poses = _poses(rng, build_walls(load_track(path)), E * C)
+        env = BatchedCarEnv(E, C, path, device="cuda:0")
+        product = _device_sensors(env, poses, 1)
+        groups = _device_sensors(env, poses, 0)
+        env.close()
+        pf, of = str(tmp_path / "poses.npy"), str(tmp_path / "out.npy")
+        np.save(pf, poses)
+        child = os.path.join(root, "tests", "sensor_child.py")
+        r = subprocess.run([sys.executable, child, path, str(E), str(C), pf, of], capture_output=True, text=True,
+                           timeout=300, env=dict(os.environ, NASCAR_LIB=variant))
+        assert r.returncode == 0, r.stderr[-2000:]
+        capped = np.load(of)
+        bad = np.argwhere(capped.view(np.uint32) != product.view(np.uint32))
+        assert len(bad) == 0, f"{os.path.basename(path)}: capped walk differs at {bad[:5].tolist()}"
+        assert np.array_equal(capped[:, 22:].view(np.uint32), groups[:, 22:].view(np.uint32))
