@@ -1457,7 +1457,9 @@ __device__ __forceinline__ int beam_slot0(double ang) {   // list slot of ray 0'
 // All 4 lanes of a car are consecutive lanes of one quad and call this together.
 // LPC = 16 (small batches, see launch_sensors_impl): one ray per lane, the 16 lanes of a car store its 16 values
 // directly (64 contiguous bytes per car).
-template <int LPC = RAY_LPC, bool GW = false>
+// COOP: the wave-cooperative list continuations when every lane of the wave is here (16 lanes per car); false: every
+// ray walks its own list (callers whose lanes are not lockstep rays of whole cars, e.g. rt_switch_kernel)
+template <int LPC = RAY_LPC, bool GW = false, bool COOP = true>
 __device__ __forceinline__ void ray_lane(const Params& P, const TrackDev& T, const float4* __restrict__ sw, int n, int r,
                                          float* obs, float* terminal_obs, int passes) {
   static_assert(LPC == 4 || LPC == 16, "lanes per car");
@@ -1520,7 +1522,7 @@ __device__ __forceinline__ void ray_lane(const Params& P, const TrackDev& T, con
       const float dx = (p2.x - p1.x) * 0.004f, dy = (p2.y - p1.y) * 0.004f;   // cull only
       float bi = 2.0f;
       uint32_t kc = 0u;   // (wave-cooperative continuation: this ray's next ent[] index, 0 when its walk is done)
-      const bool coop = LPC == 16 && RAY_COOP_WALK && __ballot(1) == ~0ull;   // every lane active: wave-uniform
+      const bool coop = COOP && LPC == 16 && RAY_COOP_WALK && __ballot(1) == ~0ull;   // every lane active: wave-uniform
       if (base >= 0) {
         const int sl = slot_of(i);
 #if RAY_HEADS_AHEAD
@@ -2532,10 +2534,13 @@ __global__ void __launch_bounds__(RT_SWITCH_BLOCK) rt_switch_kernel(Params P, Rt
   }
   __threadfence();
   __syncthreads();                        // the pass-B poses stored before the walks read them
-  for (int t = tid; t < ns * C * 16; t += RT_SWITCH_BLOCK) {   // one ray per thread
-    const int cc = t >> 4, q = cc / C, car = cc - q * C;
-    const TrackDev T = P.tracks[s_tr[q]];
-    ray_lane<16, true>(P, T, T.swall, s_env[q] * C + car, t & 15, obs, nullptr, 2);
+  for (int t0 = 0; t0 < ns * C * 16; t0 += RT_SWITCH_BLOCK) {   // one ray per thread (block-uniform loop), each
+    const int t = t0 + tid;                                     // walking its whole list on its own lane
+    if (t < ns * C * 16) {
+      const int cc = t >> 4, q = cc / C, car = cc - q * C;
+      const TrackDev T = P.tracks[s_tr[q]];
+      ray_lane<16, true, false>(P, T, T.swall, s_env[q] * C + car, t & 15, obs, nullptr, 2);
+    }
   }
 }
 // The workgroup layout rebuilt on the device (random-track mode; prepare() builds it on the host otherwise): envs
@@ -3550,7 +3555,12 @@ static int prepare(NascarHandle* h, hipStream_t stream) {
       const int nbt = (int)((per[tr].size() + h->epb - 1) / h->epb);
       for (int i = 0; i < nbt; ++i) order.push_back({(i + 0.5) / nbt, tr, i});
     }
-    std::stable_sort(order.begin(), order.end(), [](const Blk& a, const Blk& b) { return a.key < b.key; });
+    bool interleave = true;
+#ifdef NASCAR_AB_KNOBS   // A/B tools builds only: NASCAR_MAP_CONTIGUOUS restores the round-5 track-major order
+    if (getenv("NASCAR_MAP_CONTIGUOUS")) interleave = false;
+#endif
+    if (interleave)
+      std::stable_sort(order.begin(), order.end(), [](const Blk& a, const Blk& b) { return a.key < b.key; });
     for (const Blk& b : order) {
       const std::vector<int>& envs = per[b.tr];
       blk_track.push_back(b.tr);
