@@ -1,7 +1,9 @@
 """Before/after of the drop-in VecCarEnv path (round 6): the same measurement as bench.drop_in_pass's random-track
 rows, run on the round-5 package (tools/r05_tree: `git archive 8194fc8`, its own libnascar.so), whose random-track mode
 synchronised with the host every step (done flags, Python redraws, host block-map rebuild, masked reset).
-    python tools/vec_before.py [E] [C] [K]    (GPU; prints one JSON line)"""
+    mkdir tools/r05_tree && git archive 8194fc8 nascargymnasium_amd include | tar -x -C tools/r05_tree
+    (cd tools/r05_tree && python -c "from nascargymnasium_amd import _lib; _lib.build()")
+    python tools/vec_before.py [E] [C] [K]    (GPU; prints one JSON line; profiles/r06_vec_env_before.jsonl)"""
 import json
 import os
 import sys
