@@ -251,6 +251,11 @@ int nascar_debug_sincosf(const float* x, float* s, float* c, int32_t n, void* st
  * DistanceSensor values obs[n*38 + 22 .. 37] (src/distance_sensor.py:71-117, src/car_env.py:946). */
 int nascar_debug_sensors(NascarHandle* h, const float* poses, float* obs, int32_t impl, void* stream);
 
+/* Test hook: the workgroup layout the next launch uses (block map; prepare()d first) copied into caller device buffers,
+ * blk_track [cap_blocks] and blk_env [cap_blocks * envs per workgroup] int32; returns the number of workgroups launched
+ * (random-track mode: those past the last track's are empty, track -1), or < 0 on error. */
+int nascar_debug_block_map(NascarHandle* h, int32_t* blk_track, int32_t* blk_env, int32_t cap_blocks, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

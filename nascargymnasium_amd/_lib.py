@@ -142,6 +142,8 @@ def lib():
     L.nascar_set_track_cache.restype = ctypes.c_int
     L.nascar_prebuild_track.argtypes = [d_p, i32, ctypes.c_double, d_p, i32, ctypes.c_float]
     L.nascar_prebuild_track.restype = ctypes.c_int
+    L.nascar_debug_block_map.argtypes = [vp, vp, vp, i32, vp]
+    L.nascar_debug_block_map.restype = ctypes.c_int
     _lib = L
     # track build cache: NASCAR_TRACK_CACHE names an on-disk cache directory (none by default; bench.py sets one for
     # multi-rank runs), NASCAR_TRACK_RETAIN the builds kept alive after their last handle (default 8)
@@ -154,7 +156,7 @@ EXPORTED = ["nascar_create", "nascar_destroy", "nascar_last_error", "nascar_add_
             "nascar_set_state", "nascar_policy_actions", "nascar_set_step_events", "nascar_set_actor", "nascar_set_actor_precision", "nascar_actor_forward",
             "nascar_debug_sincosf", "nascar_debug_sensors", "nascar_track_draw", "nascar_set_random_tracks",
             "nascar_get_env_tracks", "nascar_vec_post", "nascar_check_actions", "nascar_set_track_cache",
-            "nascar_prebuild_track"]
+            "nascar_prebuild_track", "nascar_debug_block_map"]
 
 
 def check(rc):

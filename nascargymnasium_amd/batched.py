@@ -211,6 +211,17 @@ class BatchedCarEnv:
         ids, _ = self.env_track_ids()
         return [self._track_files_by_id[i] for i in ids]
 
+    def block_map(self):
+        """(blk_track [nb], blk_env [nb, envs_per_block]) numpy int32: the workgroup layout of the next launch (test hook,
+        nascar_debug_block_map; one host synchronisation)"""
+        cap = self.E + 128
+        bt = torch.empty(cap, dtype=torch.int32, device=self.device)
+        be = torch.empty(cap * max(1, self.envs_per_block), dtype=torch.int32, device=self.device)
+        with torch.cuda.device(self.device):
+            nb = _lib.check(self.L.nascar_debug_block_map(self.h, _ptr(bt), _ptr(be), cap, _stream()))
+        epb = self.envs_per_block
+        return bt[:nb].cpu().numpy(), be[:nb * epb].cpu().numpy().reshape(nb, epb)
+
     # ------------------------------------------------------------------ core API
     def reset(self, env_mask: Optional[torch.Tensor] = None) -> torch.Tensor:
         """CarEnv.reset for all envs (or those with env_mask[e] != 0, uint8[E] on device)."""

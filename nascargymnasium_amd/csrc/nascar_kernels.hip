@@ -2112,68 +2112,144 @@ __device__ __forceinline__ void logic_run(const Params& P, const TrackDev& T, co
   LPROF(8);}
 
 // ------------------------------------------------------------------ car-car contact (build-only extension)
-// NOT in the reference: each reference car lives in its own b2World (src/car_physics.py:74-107), so cars of
-// one env never touch.  With nascar_set_car_contact(h, 1) the cars of an env collide: after the
-// Box2D step every overlapping pair of car boxes (separating-axis test on the 4 box axes) that is closing
-// along the axis of least penetration exchanges a frictionless central impulse with restitution 0.25 (the
-// wall's, src/constants/physics.py), Jacobi-style from the post-step velocities (all of an env's cars are
-// read before any is written: the env sits in one workgroup), and the impulse magnitude enters the car's
-// collision impulse as CarCollisionListener.PostSolve does for walls (max over contacts), so damage and
-// impact disables apply.  Positions are left to the next step's integration (Box2D proxies stay valid).
-// Sensors still see walls only.  Default off; every parity test runs with it off.
-__device__ __forceinline__ bool car_box_overlap(V2 pa, Rot qa, V2 pb, Rot qb, V2& n, float& depth) {
-  const V2 d = vsub(pb, pa);
-  const V2 ax[4] = {V(qa.c, qa.s), V(-qa.s, qa.c), V(qb.c, qb.s), V(-qb.s, qb.c)};
-  depth = FLT_BIG;
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const V2 u = ax[k];
-    const float ea = CAR_HX * fabsf(vdot(u, V(qa.c, qa.s))) + CAR_HY * fabsf(vdot(u, V(-qa.s, qa.c)));
-    const float eb = CAR_HX * fabsf(vdot(u, V(qb.c, qb.s))) + CAR_HY * fabsf(vdot(u, V(-qb.s, qb.c)));
-    const float sd = vdot(u, d), pen = ea + eb - fabsf(sd);
-    if (pen <= 0.0f) return false;
-    if (pen < depth) { depth = pen; n = sd >= 0.0f ? u : vneg(u); }   // n: from a toward b
-  }
-  return true;
-}
-__device__ __forceinline__ void car_contact_block(const Params& P, int tid, int el, int car, int env, int n) {
-  const int C = P.C;
-  V2 dv = zero2();
-  double jmax = 0.0;
-  if (env >= 0) {
-    const V2 pa = V(F32P(P, xpx)[n], F32P(P, xpy)[n]);
-    Rot qa; qa.s = F32P(P, qs)[n]; qa.c = F32P(P, qc)[n];
-    const V2 va = V(F32P(P, vx)[n], F32P(P, vy)[n]);
-    const int e0 = env * C;
-    for (int j = 0; j < C; ++j) {
-      if (j == car) continue;
-      const int m = e0 + j;
-      const V2 pb = V(F32P(P, xpx)[m], F32P(P, xpy)[m]);
-      if (fabsf(pb.x - pa.x) > 5.7f || fabsf(pb.y - pa.y) > 5.7f) continue;   // > 2 circumradii apart
-      Rot qb; qb.s = F32P(P, qs)[m]; qb.c = F32P(P, qc)[m];
-      V2 nn; float depth;
-      if (!car_box_overlap(pa, qa, pb, qb, nn, depth)) continue;
-      const V2 vb = V(F32P(P, vx)[m], F32P(P, vy)[m]);
-      const float vrel = vdot(vsub(vb, va), nn);
-      if (vrel >= 0.0f) continue;                                  // separating
-      const float J = -(1.0f + MIX_RESTITUTION) * vrel * (0.5f / CAR_INV_MASS);   // equal masses
-      dv = vsub(dv, vmul(J * CAR_INV_MASS, nn));
-      jmax = pymax(jmax, (double)J);
+// NOT in the reference: each reference car lives in its own b2World (src/car_physics.py:74-107) and its fixture's mask
+// filters other cars out (src/constants/physics.py:9 COLLISION_MASK_CARS), so cars of one env never touch.
+// With nascar_set_car_contact(h, 1) the cars of an env collide after their Box2D steps, with Box2D's contact algorithms
+// for two dynamic bodies: every pair of car boxes whose centres are within two circumradii gets b2CollidePolygons'
+// manifold (collide_polygons: 1-2 clip points, the same code as the wall contacts), and the env's touching pairs are
+// solved by b2ContactSolver's sequential impulses -- per iteration and contact, the tangent (friction) impulses clamped
+// by friction x normal impulse, then the normal impulses accumulated and clamped at >= 0, each applied to both cars'
+// linear AND angular velocity (mass 1500 kg, the box's inertia) -- for BOX2D_VELOCITY_ITERATIONS (6), with the fixture
+// mixing Box2D applies to a car pair: friction sqrt(0.7 * 0.7), restitution max(0.1, 0.1) (src/constants/car_specs.py:
+// 39-40) as a velocity bias below -1 m/s relative normal speed (b2_velocityThreshold).  The accumulated normal impulses
+// enter each car's collision impulse as CarCollisionListener.PostSolve does for walls (max over contact points), so
+// damage and impact disables apply; a car that receives an impulse is woken.  What a shared b2World would do and this
+// does not: the car-car constraints are solved after (not interleaved with) each car's wall island, with no warm start
+// across steps, the 2-point block solver replaced by point-by-point sequential impulses, and no position correction (the
+// per-car Box2D steps, their proxies and TOI sweeps are done; overlap is removed by the velocities over the next steps).
+// One lane per env (its car 0) solves the env; the bodies and constraints sit in the caller's LDS scratch
+// (CC_LDS_BYTES).  Sensors still see walls only.  Default off; every parity test runs with it off.
+#define CAR_FRICTION_MIX 0.7f      // sqrt(CAR_FRICTION * CAR_FRICTION)
+#define CAR_RESTITUTION_MIX 0.1f   // max(CAR_RESTITUTION, CAR_RESTITUTION)
+#define CC_VELOCITY_ITERATIONS 6   // BOX2D_VELOCITY_ITERATIONS (src/constants/physics.py:16)
+struct CCBody { V2 c; Rot q; V2 v; float w, jmax; };
+struct CCon {                       // one touching car pair: b2ContactVelocityConstraint for two dynamic bodies
+  int ia, ib, np; V2 n;
+  V2 rA[2], rB[2]; float nm[2], tm[2], vb[2], ni[2], ti[2];
+};
+#define CC_LDS_BYTES ((size_t)SBLOCK * (sizeof(CCBody) + sizeof(CCon)))
+#ifndef CC_FUSED
+#define CC_FUSED 1   // the car-car phase inside model_logic_kernel (a call; 0: the two-launch path when it is on)
+#endif
+__device__ __attribute__((noinline)) void car_contact_env(CCBody* B, CCon* K, int C, int kcap) {
+  Poly box; make_box(&box, CAR_HX, CAR_HY);
+  int nk = 0;
+  for (int i = 0; i < C; ++i)
+    for (int j = i + 1; j < C; ++j) {
+      const CCBody A = B[i], D = B[j];
+      if (fabsf(D.c.x - A.c.x) > 5.7f || fabsf(D.c.y - A.c.y) > 5.7f) continue;   // > 2 circumradii apart
+      Xf xa; xa.p = A.c; xa.q = A.q;
+      Xf xb; xb.p = D.c; xb.q = D.q;
+      DContact m;
+      collide_polygons(m, &box, xa, &box, xb);
+      if (m.pointCount == 0 || nk == kcap) continue;
+      V2 nrm, pts[2];
+      world_manifold(m, xa, xb, &nrm, pts);
+      CCon k;
+      k.ia = i; k.ib = j; k.np = m.pointCount; k.n = nrm;
+      const V2 t = vcross_vs(nrm, 1.0f);
+      for (int q = 0; q < 2; ++q) {
+        k.ni[q] = 0.0f; k.ti[q] = 0.0f; k.nm[q] = 0.0f; k.tm[q] = 0.0f; k.vb[q] = 0.0f;
+        k.rA[q] = zero2(); k.rB[q] = zero2();
+        if (q >= k.np) continue;
+        const V2 rA = vsub(pts[q], A.c), rB = vsub(pts[q], D.c);
+        k.rA[q] = rA; k.rB[q] = rB;
+        const float rnA = vcross(rA, nrm), rnB = vcross(rB, nrm);
+        const float kn = CAR_INV_MASS + CAR_INV_MASS + CAR_INV_I * rnA * rnA + CAR_INV_I * rnB * rnB;
+        k.nm[q] = kn > 0.0f ? fdiv_cr(1.0f, kn) : 0.0f;
+        const float rtA = vcross(rA, t), rtB = vcross(rB, t);
+        const float kt = CAR_INV_MASS + CAR_INV_MASS + CAR_INV_I * rtA * rtA + CAR_INV_I * rtB * rtB;
+        k.tm[q] = kt > 0.0f ? fdiv_cr(1.0f, kt) : 0.0f;
+        const V2 dv = vsub(vadd(D.v, vcross_sv(D.w, rB)), vadd(A.v, vcross_sv(A.w, rA)));
+        const float vrel = vdot(nrm, dv);
+        if (vrel < -VELOCITY_THRESHOLD) k.vb[q] = -CAR_RESTITUTION_MIX * vrel;
+      }
+      K[nk++] = k;
     }
+  if (nk == 0) return;
+  for (int it = 0; it < CC_VELOCITY_ITERATIONS; ++it)
+    for (int kk = 0; kk < nk; ++kk) {
+      CCon& k = K[kk];
+      CCBody& A = B[k.ia];
+      CCBody& D = B[k.ib];
+      V2 vA = A.v, vB = D.v; float wA = A.w, wB = D.w;
+      const V2 nrm = k.n, t = vcross_vs(nrm, 1.0f);
+      for (int q = 0; q < k.np; ++q) {   // friction first, as b2ContactSolver::SolveVelocityConstraints
+        const V2 dv = vsub(vadd(vB, vcross_sv(wB, k.rB[q])), vadd(vA, vcross_sv(wA, k.rA[q])));
+        const float vt = vdot(dv, t);
+        float lambda = k.tm[q] * (-vt);
+        const float maxF = CAR_FRICTION_MIX * k.ni[q];
+        const float ni = fclamp(k.ti[q] + lambda, -maxF, maxF);
+        lambda = ni - k.ti[q];
+        k.ti[q] = ni;
+        const V2 Pt = vmul(lambda, t);
+        vA = vsub(vA, vmul(CAR_INV_MASS, Pt)); wA -= CAR_INV_I * vcross(k.rA[q], Pt);
+        vB = vadd(vB, vmul(CAR_INV_MASS, Pt)); wB += CAR_INV_I * vcross(k.rB[q], Pt);
+      }
+      for (int q = 0; q < k.np; ++q) {   // normal: accumulated impulse clamped at >= 0
+        const V2 dv = vsub(vadd(vB, vcross_sv(wB, k.rB[q])), vadd(vA, vcross_sv(wA, k.rA[q])));
+        const float vn = vdot(dv, nrm);
+        float lambda = -k.nm[q] * (vn - k.vb[q]);
+        const float ni = fmaxb(k.ni[q] + lambda, 0.0f);
+        lambda = ni - k.ni[q];
+        k.ni[q] = ni;
+        const V2 Pn = vmul(lambda, nrm);
+        vA = vsub(vA, vmul(CAR_INV_MASS, Pn)); wA -= CAR_INV_I * vcross(k.rA[q], Pn);
+        vB = vadd(vB, vmul(CAR_INV_MASS, Pn)); wB += CAR_INV_I * vcross(k.rB[q], Pn);
+      }
+      A.v = vA; A.w = wA; D.v = vB; D.w = wB;
+    }
+  for (int kk = 0; kk < nk; ++kk) {   // CarCollisionListener.PostSolve: the largest normal impulse per car
+    const CCon& k = K[kk];
+    float j = 0.0f;
+    for (int q = 0; q < k.np; ++q) j = fmaxb(j, k.ni[q]);
+    B[k.ia].jmax = fmaxb(B[k.ia].jmax, j);
+    B[k.ib].jmax = fmaxb(B[k.ib].jmax, j);
   }
-  __syncthreads();   // every car of the env has read the post-step velocities
-  if (env >= 0 && (dv.x != 0.0f || dv.y != 0.0f)) {
-    F32P(P, vx)[n] = F32P(P, vx)[n] + dv.x;
-    F32P(P, vy)[n] = F32P(P, vy)[n] + dv.y;
-    if (!I32P(P, imp_present)[n]) { I32P(P, imp_present)[n] = 1; F64P(P, imp)[n] = 0.0; }
-    F64P(P, imp)[n] = pymax(F64P(P, imp)[n], jmax);
+}
+// every thread of the block calls it (block barriers); scratch: CC_LDS_BYTES of LDS
+__device__ __forceinline__ void car_contact_block(const Params& P, int tid, int el, int car, int env, int n,
+                                                  unsigned char* scratch) {
+  const int C = P.C;
+  CCBody* B = (CCBody*)scratch;
+  CCon* K = (CCon*)(scratch + (size_t)SBLOCK * sizeof(CCBody));
+  if (env >= 0) {
+    CCBody b;
+    b.c = V(F32P(P, xpx)[n], F32P(P, xpy)[n]);      // (the body origin is its centre of mass)
+    b.q.s = F32P(P, qs)[n]; b.q.c = F32P(P, qc)[n];
+    b.v = V(F32P(P, vx)[n], F32P(P, vy)[n]); b.w = F32P(P, w)[n];
+    b.jmax = 0.0f;
+    B[tid] = b;
+  }
+  __syncthreads();
+  if (env >= 0 && car == 0 && C > 1) car_contact_env(B + tid, K + tid, C, C);   // an env's C slots hold <= C contacts
+  __syncthreads();
+  if (env >= 0) {
+    const CCBody b = B[tid];
+    if (b.jmax > 0.0f) {
+      F32P(P, vx)[n] = b.v.x; F32P(P, vy)[n] = b.v.y; F32P(P, w)[n] = b.w;
+      if (!I32P(P, awake)[n]) { I32P(P, awake)[n] = 1; F32P(P, sleep)[n] = 0.0f; }
+      if (!I32P(P, imp_present)[n]) { I32P(P, imp_present)[n] = 1; F64P(P, imp)[n] = 0.0; }
+      F64P(P, imp)[n] = pymax(F64P(P, imp)[n], (double)b.jmax);
+    }
   }
 }
 __global__ void __launch_bounds__(SBLOCK) car_contact_kernel(Params P) {
   const int tid = threadIdx.x, C = P.C;
   const int el = tid / C, car = tid - el * C;
   const int env = blk_env_of(P, el, (blockIdx.x + P.blk0) * P.epb + el);
-  car_contact_block(P, tid, el, car, env, env >= 0 ? env * C + car : 0);
+  if (blk_track_of(P, blockIdx.x + P.blk0) < 0) return;   // empty workgroup (device-built block map)
+  car_contact_block(P, tid, el, car, env, env >= 0 ? env * C + car : 0, smem);
 }
 
 #ifndef LOGIC_WPE
@@ -2255,7 +2331,9 @@ model_logic_kernel(Params P, const void* actions, int discrete, int want_term, i
   model_block<true>(P, actions, discrete, want_term, policy, seed, step, pobs, tid, env, n, c, sr);
   __syncthreads();   // the block's Box2D steps done: body state stored, contact slots written back (LDS free)
   PROF(6);           // profile builds: the fused kernel's logic half (stamp slots 6-9)
-  if (P.car_contact) car_contact_block(P, tid, el, car, env, n);   // block-uniform; holds its own barrier
+#if CC_FUSED
+  if (P.car_contact) car_contact_block(P, tid, el, car, env, n, smem);   // block-uniform; holds its own barriers
+#endif
   fused_logic_phase(P, tid, el, car, env, n, obs, reward, car_flags, env_flags, auto_reset, terminal_obs, c, sim, pend_in,
                     reason_in, sr);
   PROF(8);
@@ -2322,7 +2400,8 @@ static __device__ __attribute__((noinline)) void ro_logic_phase(ParamsK Pk, floa
 static __device__ __attribute__((noinline)) void ro_contact_phase(ParamsK Pk) {
   const Params& P = *(const Params*)Pk;
   const RoSlot s = ro_slot(P);
-  car_contact_block(P, s.tid, s.el, s.car, s.env, s.n);
+  const TrackDev T = P.tracks[blk_track_of(P, blockIdx.x)];   // the scratch follows the staged sensor wall image
+  car_contact_block(P, s.tid, s.el, s.car, s.env, s.n, smem + ((2 * (size_t)T.nwall * sizeof(float4) + 15) & ~(size_t)15));
 }
 static __device__ __attribute__((noinline)) void ro_sensor_phase(ParamsK Pk, float* obs, int passes) {
   const Params& P = *(const Params*)Pk;
@@ -2549,11 +2628,83 @@ __global__ void __launch_bounds__(RT_SWITCH_BLOCK) rt_switch_kernel(Params P, Rt
 // no launch waits for the host.  One 1024-thread workgroup: per-track counts (LDS atomics), block offsets, then each
 // env's rank among its track's envs by ballots over 1024-env chunks.  Does nothing unless *dirty (or force).
 #define RT_MAX_TRACKS 64
+// word w of a thread's packed per-track counts: tracks 2w (low 16 bits) and 2w + 1 (high 16 bits)
+__device__ __forceinline__ uint32_t pk_get(const uint32_t c[4], int t) {
+  const uint32_t w = (t >> 1) == 0 ? c[0] : (t >> 1) == 1 ? c[1] : (t >> 1) == 2 ? c[2] : c[3];
+  return (t & 1) ? w >> 16 : w & 0xFFFFu;
+}
+__device__ __forceinline__ void pk_add(uint32_t c[4], int t, uint32_t v) {
+  const uint32_t inc = v << ((t & 1) * 16);
+#pragma unroll
+  for (int w = 0; w < 4; ++w) c[w] += (t >> 1) == w ? inc : 0u;
+}
 __global__ void __launch_bounds__(1024) block_map_kernel(int E, int epb, int ntr, const int* env_track, int* blk_track,
                                                          int* blk_env, int nb_cap, int* dirty, int force) {
   __shared__ int cnt[RT_MAX_TRACKS], boff[RT_MAX_TRACKS + 1], run[RT_MAX_TRACKS], woff[16][RT_MAX_TRACKS];
+  __shared__ uint32_t s_wt[16][4];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   if (!force && *dirty == 0) return;      // (every thread reads it before thread 0 clears it, after the barriers below)
+  auto track_of = [&](int b) {
+    int tr = -1;
+    for (int t = 0; t < ntr; ++t) tr = (b >= boff[t] && b < boff[t + 1]) ? t : tr;
+    return tr;
+  };
+  if (ntr <= 8 && E < 65536) {
+    // Fast path (up to 8 tracks: the bundled ones): thread t owns envs [t R, t R + R); its per-track counts packed as
+    // 16-bit fields in 4 words, one block-wide exclusive scan of the packed words (wave scan by shuffles, then the 16
+    // wave totals from LDS), so every env's slot comes out of one pass with a single barrier.
+    const int R = (E + 1023) / 1024, e0 = tid * R;
+    uint32_t c[4] = {0u, 0u, 0u, 0u};
+    for (int i = 0; i < R; ++i) {
+      const int e = e0 + i;
+      if (e < E) pk_add(c, env_track[e], 1u);
+    }
+    uint32_t incl[4] = {c[0], c[1], c[2], c[3]};
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const uint32_t x = (uint32_t)__shfl_up((int)incl[k], d);
+        if (lane >= d) incl[k] += x;
+      }
+    if (lane == 63) { s_wt[w][0] = incl[0]; s_wt[w][1] = incl[1]; s_wt[w][2] = incl[2]; s_wt[w][3] = incl[3]; }
+    __syncthreads();
+    uint32_t before[4] = {0u, 0u, 0u, 0u}, total[4] = {0u, 0u, 0u, 0u};
+    for (int ww = 0; ww < 16; ++ww)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const uint32_t x = s_wt[ww][k];
+        before[k] += ww < w ? x : 0u;
+        total[k] += x;
+      }
+    uint32_t ex[4];   // this thread's first rank within each track
+#pragma unroll
+    for (int k = 0; k < 4; ++k) ex[k] = before[k] + incl[k] - c[k];
+    int bo[9];        // block offsets of the tracks (every thread computes them)
+    bo[0] = 0;
+#pragma unroll
+    for (int t = 0; t < 8; ++t) bo[t + 1] = bo[t] + (t < ntr ? (int)((pk_get(total, t) + epb - 1) / epb) : 0);
+    if (tid <= 8) boff[tid] = bo[tid];
+    for (int i = 0; i < R; ++i) {
+      const int e = e0 + i;
+      if (e >= E) break;
+      const int t = env_track[e];
+      int b0 = 0;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) b0 = t == k ? bo[k] : b0;
+      blk_env[b0 * epb + (int)pk_get(ex, t)] = e;
+      pk_add(ex, t, 1u);
+    }
+    __syncthreads();   // boff published
+    for (int b = tid; b < nb_cap; b += 1024) blk_track[b] = track_of(b);
+    for (int s = tid; s < ntr * epb; s += 1024) {   // the unfilled tail of each track's last workgroup
+      const int t = s / epb, k = s - t * epb;
+      const int n = (int)pk_get(total, t), tail = (boff[t + 1] - boff[t]) * epb - n;
+      if (k < tail) blk_env[boff[t] * epb + n + k] = -1;
+    }
+    if (tid == 0) *dirty = 0;
+    return;
+  }
   for (int t = tid; t < ntr; t += 1024) { cnt[t] = 0; run[t] = 0; }
   __syncthreads();
   for (int e = tid; e < E; e += 1024) atomicAdd(&cnt[env_track[e]], 1);
@@ -2564,15 +2715,11 @@ __global__ void __launch_bounds__(1024) block_map_kernel(int E, int epb, int ntr
     boff[ntr] = b;
   }
   __syncthreads();
-  auto track_of = [&](int b) {
-    int tr = -1;
-    for (int t = 0; t < ntr; ++t) tr = (b >= boff[t] && b < boff[t + 1]) ? t : tr;
-    return tr;
-  };
   for (int b = tid; b < nb_cap; b += 1024) blk_track[b] = track_of(b);
-  for (int s = tid; s < nb_cap * epb; s += 1024) {   // the slots no env fills
-    const int b = s / epb, t = track_of(b);
-    if (t < 0 || s - boff[t] * epb >= cnt[t]) blk_env[s] = -1;
+  // the unfilled tail of each track's last workgroup (workgroups of track -1 are never read: every kernel returns first)
+  for (int s = tid; s < ntr * epb; s += 1024) {
+    const int t = s / epb, k = s - t * epb, tail = (boff[t + 1] - boff[t]) * epb - cnt[t];
+    if (k < tail) blk_env[boff[t] * epb + cnt[t] + k] = -1;
   }
   const unsigned long long below = lane ? (~0ull >> (64 - lane)) : 0ull;
   for (int c0 = 0; c0 < E; c0 += 1024) {
@@ -3199,10 +3346,12 @@ static int sensor_lds_reserve(size_t need) {
   for (const void* k : kern) {
     hipFuncAttributes a;
     if (hipFuncGetAttributes(&a, k) != hipSuccess) return fail("hipFuncGetAttributes failed");
-    if (a.sharedSizeBytes + need > LDS_PER_CU)
+    // the fused rollout kernel also holds the car-car extension's scratch after the wall image
+    const size_t n2 = k == (const void*)rollout_kernel ? ((need + 15) & ~(size_t)15) + CC_LDS_BYTES : need;
+    if (a.sharedSizeBytes + n2 > LDS_PER_CU)
       return fail("track needs %zu B of LDS for its sensor wall image; with %zu B of static LDS a workgroup has %zu",
                   need, (size_t)a.sharedSizeBytes, LDS_PER_CU - (size_t)a.sharedSizeBytes);
-    if (need > 64 * 1024) HIPCHK(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)need));
+    if (n2 > 64 * 1024) HIPCHK(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)n2));
   }
   return 0;
 }
@@ -3778,7 +3927,7 @@ static int launch_step_range(NascarHandle* h, const Params& P, int nb, const voi
                              uint8_t* car_flags, uint8_t* env_flags, int32_t auto_reset, float* terminal_obs,
                              hipStream_t s, int phases = PH_ALL, bool model_issued = false) {
   const bool timed = h->step_ev[0] && nb == h->nblocks;   // nascar_set_step_events: whole-grid steps only
-  if (h->fuse_ml) {   // model + logic in one launch (model_logic_kernel); the logic phase is part of PH_MODEL
+  if (h->fuse_ml && (CC_FUSED || !h->car_contact)) {   // model + logic in one launch (model_logic_kernel); logic is part of PH_MODEL
     // Under the fused kernel the logic phase IS part of PH_MODEL's launch, so a PH_LOGIC-only request enqueues nothing:
     // only a caller that has already requested PH_MODEL for the same step and range may make it (model_issued: the
     // sharded rollout's phase-major loop, 1 << ph for ph = 0, 1, 2); anyone else gets an error, not a silently
@@ -3801,7 +3950,7 @@ static int launch_step_range(NascarHandle* h, const Params& P, int nb, const voi
                        terminal_obs != nullptr, policy, seed, step, obs_in);
     HIPCHK(hipGetLastError());
     if (h->car_contact) {
-      hipLaunchKernelGGL(car_contact_kernel, dim3(nb), dim3(SBLOCK), 0, s, P);
+      hipLaunchKernelGGL(car_contact_kernel, dim3(nb), dim3(SBLOCK), CC_LDS_BYTES, s, P);
       HIPCHK(hipGetLastError());
     }
     if (timed) HIPCHK(hipEventRecord(h->step_ev[1], s));
@@ -3974,7 +4123,8 @@ extern "C" int nascar_rollout(NascarHandle* h, int32_t policy, uint64_t seed, in
     h->params_up = P; h->params_valid = true;
     HIPCHK(hipMemcpyAsync(h->d_params, &h->params_up, sizeof(Params), hipMemcpyHostToDevice, (hipStream_t)stream));
   }
-  const size_t lds = h->max_sensor_lds;   // >= 2 float4 per wall of the largest track
+  // >= 2 float4 per wall of the largest track; the car-car extension's scratch after it
+  const size_t lds = ((h->max_sensor_lds + 15) & ~(size_t)15) + (h->car_contact ? CC_LDS_BYTES : 0);
   hipLaunchKernelGGL(rollout_kernel, dim3(h->nblocks), dim3(SBLOCK), lds, (hipStream_t)stream, (const Params*)h->d_params,
                      steps, policy, seed, step0, obs, reward, car_flags, env_flags, auto_reset, traj);
   HIPCHK(hipGetLastError());
@@ -4285,6 +4435,20 @@ extern "C" int nascar_debug_sensors(NascarHandle* h, const float* poses, float* 
   launch_sensors_impl(h, P, h->nblocks, obs, nullptr, 1, stream, impl);
   HIPCHK(hipGetLastError());
   return 0;
+}
+
+// Test hook: the current workgroup layout (block map) into caller device buffers -- blk_track [cap_blocks] and
+// blk_env [cap_blocks * epb] int32 -- as the next launch would use it (prepare() first); returns the grid size
+// (workgroups launched; in random-track mode the workgroups past the last track's are empty, track -1), or < 0.
+extern "C" int nascar_debug_block_map(NascarHandle* h, int32_t* blk_track, int32_t* blk_env, int32_t cap_blocks,
+                                      void* stream) {
+  if (!h || !blk_track || !blk_env) return fail("null argument");
+  if (prepare(h, (hipStream_t)stream)) return -1;
+  if (cap_blocks < h->nblocks) return fail("block map needs %d workgroups, buffer holds %d", h->nblocks, cap_blocks);
+  HIPCHK(hipMemcpyAsync(blk_track, h->d_blk_track, sizeof(int) * h->nblocks, hipMemcpyDeviceToDevice, (hipStream_t)stream));
+  HIPCHK(hipMemcpyAsync(blk_env, h->d_blk_env, sizeof(int) * (size_t)h->nblocks * h->epb, hipMemcpyDeviceToDevice,
+                        (hipStream_t)stream));
+  return h->nblocks;
 }
 
 #ifdef NASCAR_PROFILE

@@ -190,6 +190,52 @@ def test_car_contact_rear_end():
     env.close()
 
 
+def test_car_contact_impulses_conserve_momentum():
+    """The car-car extension's solver (b2CollidePolygons manifolds, b2ContactSolver sequential impulses with friction
+    and angular terms, restitution 0.1 / friction 0.7 mixed as Box2D mixes two car fixtures): from the state just before
+    car 2 (steering slightly) first runs into car 0, one step with the extension on and one with it off differ only by
+    the car-car impulses, so the velocity changes must conserve linear momentum and angular momentum about the origin
+    (equal and opposite impulses at one contact point), spin the cars (an off-centre hit: angular response), and the
+    impulse is reported on both cars."""
+    from gpu_state import decode
+    from nascargymnasium_amd.batched import BatchedCarEnv
+    E, C = 1, 3
+    path = os.path.join(TRACKS, "daytona.track")
+    env = BatchedCarEnv(E, C, path, device="cuda:0")
+    env.set_car_contact(True)
+    env.reset()
+    a = torch.tensor([[[0.0, 0.0], [0.0, 0.0], [1.0, 0.08]]], device="cuda")
+    prev = None
+    for k in range(300):
+        prev = (env.get_state().clone(), env.obs.clone())
+        env.step(a)
+        if int(env.car_flags[0, 0]) & 4 and int(env.car_flags[0, 2]) & 4:
+            break
+    else:
+        raise AssertionError("car 2 never reached car 0")
+    outs = []
+    for on in (True, False):
+        t = BatchedCarEnv(E, C, path, device="cuda:0")
+        t.set_car_contact(on)
+        t.set_state(prev[0]); t.obs.copy_(prev[1])
+        t.step(a)
+        outs.append((decode(t.get_state().cpu().numpy(), E * C), t.car_flags.cpu().numpy()[0].copy()))
+        t.close()
+    (on, flags_on), (off, flags_off) = outs
+    m, I = 1500.0, 1500.0 * (5.042 ** 2 + 1.996 ** 2) * 0.5 / 12.0     # the car body's mass and inertia (CAR_I_F)
+    dvx, dvy, dw = (on[f].astype(np.float64) - off[f] for f in ("vx", "vy", "w"))
+    cx, cy = off["xpx"].astype(np.float64), off["xpy"].astype(np.float64)
+    p = m * np.hypot(dvx, dvy).max()
+    assert p > 100.0, "no car-car impulse"
+    assert abs(m * dvx.sum()) < 1e-3 * p and abs(m * dvy.sum()) < 1e-3 * p       # linear momentum
+    L = (I * dw + m * (cx * dvy - cy * dvx)).sum()                                 # angular momentum about (0, 0)
+    assert abs(L) < 1e-3 * p * (1.0 + np.hypot(cx, cy).max())
+    assert np.abs(dw).max() > 1e-4, "an off-centre hit must spin the cars (angular response)"
+    assert abs(dvx[1]) == 0.0 and abs(dvy[1]) == 0.0                               # car 1 untouched
+    assert flags_on[0] & 4 and flags_on[2] & 4 and not flags_off[0] & 4   # the impulse reported on both cars
+    env.close()
+
+
 def test_full_size_batch_independence_and_determinism():
     """BASELINE's full single-GPU shape (8192 envs x 10 cars, daytona) through size-independent properties:
     (1) every env of the full batch evolves exactly as the same env in a 16-env batch fed the same actions

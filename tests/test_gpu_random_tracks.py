@@ -114,3 +114,58 @@ def test_random_tracks_rollout_equals_per_step():
     assert np.array_equal(a.env_track_ids()[0], b.env_track_ids()[0])
     for g in engs:
         g.close()
+
+
+def _expected_map(ids, ntracks, epb):
+    """the layout block_map_kernel must build: tracks in id order, each track's envs in ascending order in whole
+    workgroups of epb envs (the last one padded with -1)"""
+    bt, be = [], []
+    for t in range(ntracks):
+        envs = np.nonzero(ids == t)[0].tolist()
+        for i in range(0, len(envs), epb):
+            bt.append(t)
+            chunk = envs[i:i + epb]
+            be.append(chunk + [-1] * (epb - len(chunk)))
+    return np.array(bt, np.int32), np.array(be, np.int32).reshape(-1, epb)
+
+
+@pytest.mark.parametrize("extra_tracks", [0, 2])     # 8 tracks: the packed-count fast path; 10: the generic path
+def test_device_block_map_matches_host_layout(tmp_path, extra_tracks):
+    """block_map_kernel (random-track mode's workgroup layout, rebuilt on the device) against the layout computed here
+    from the device's env -> track map, after the initial build, after masked resets (draws) and after steps whose
+    auto-resets switch tracks: the used workgroups exactly as expected, the rest empty (track -1)."""
+    from nascargymnasium_amd.batched import BatchedCarEnv
+    from nascargymnasium_amd.track import available_tracks
+    tracks = available_tracks()
+    for k in range(extra_tracks):     # copies of bundled tracks under other names: more tracks than the fast path takes
+        p = tmp_path / f"extra{k}.track"
+        p.write_text(open(tracks[k]).read())
+        tracks.append(str(p))
+    E, C, epb = 301, 1, 5
+    eng = BatchedCarEnv(E, C, [tracks[e % len(tracks)] for e in range(E)], device="cuda:0", envs_per_block=epb)
+    eng.set_random_tracks(tracks, np.arange(E, dtype=np.uint64) * 31 + 7)
+    rng = np.random.default_rng(3)
+    checks = 0
+
+    def check():
+        ids, _ = eng.env_track_ids()
+        bt, be = eng.block_map()
+        want_t, want_e = _expected_map(ids, len(tracks), epb)
+        assert len(bt) == (E + epb - 1) // epb + len(tracks)
+        n = len(want_t)
+        assert np.array_equal(bt[:n], want_t) and (bt[n:] == -1).all()
+        assert np.array_equal(be[:n], want_e)
+        return 1
+    checks += check()
+    eng.reset()
+    checks += check()
+    for k in range(6):
+        mask = torch.from_numpy((rng.random(E) < 0.3).astype(np.uint8)).cuda()
+        eng.reset(mask)
+        checks += check()
+    a = torch.zeros(E, C, 2, device="cuda")          # idle: every env stuck-disabled at ~600 steps, auto-resets, switches
+    for k in range(700):
+        eng.step(a, auto_reset=True)
+    checks += check()
+    assert checks == 9
+    eng.close()
