@@ -1392,6 +1392,10 @@ __device__ __forceinline__ float ray_walk(const BeamGrid& G, const float4* __res
 #ifndef RAY_COOP_ROUNDS
 #define RAY_COOP_ROUNDS 1024
 #endif
+// lanes per walking ray and round at most 64 >> RAY_COOP_LGMIN (0: up to the whole wave for a lone ray)
+#ifndef RAY_COOP_LGMIN
+#define RAY_COOP_LGMIN 0
+#endif
 template <bool GW>
 __device__ __forceinline__ float ray_walk_coop(const BeamGrid& G, const float4* __restrict__ sw, uint32_t k, float bi, V2 p1,
                                                V2 p2, float dx, float dy) {
@@ -1401,7 +1405,7 @@ __device__ __forceinline__ float ray_walk_coop(const BeamGrid& G, const float4* 
     const unsigned long long m = __ballot(k != 0u);
     if (!m) break;
     const int na = __popcll(m);
-    const int lg = na > 1 ? 32 - __clz(na - 1) : 0;      // ceil(log2 na)
+    const int lg = max(na > 1 ? 32 - __clz(na - 1) : 0, RAY_COOP_LGMIN);   // ceil(log2 na), at least the minimum
     const int E = 64 >> lg;                               // lanes per walking ray
     const int q = lane >> (6 - lg), o = lane & (E - 1);   // this lane's ray (q-th walking one) and entry offset
     const bool serve = q < na;
