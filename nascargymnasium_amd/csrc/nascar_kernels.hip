@@ -130,6 +130,12 @@ __device__ __forceinline__ int blk_env_of(const Params& P, int el, int s) {
   return P.blk_env[s];
 }
 __device__ __forceinline__ int blk_track_of(const Params& P, int b) { return P.one_track >= 0 ? P.one_track : P.blk_track[b]; }
+// a workgroup of no track: the device-built block map's workgroups past the last track's (random-track mode); every
+// kernel returns first for them (never taken with the host-built map, whose workgroups all hold envs)
+#ifndef EMPTY_GUARD
+#define EMPTY_GUARD 1
+#endif
+__device__ __forceinline__ bool blk_empty(const Params& P, int b) { return EMPTY_GUARD && P.one_track < 0 && P.blk_track[b] < 0; }
 // BeamGrid list base (built cell id * BEAM_NB) of the cell holding (x, y); -1 outside the built cells
 __device__ __forceinline__ int beam_cell_base(const BeamGrid& G, float x, float y) {
   const float fx = (x - G.ox) * G.inv_cell, fy = (y - G.oy) * G.inv_cell;
@@ -1032,7 +1038,7 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(SENS
   const int slot = sub * CPW + lc;          // car slot within the step kernel's workgroup b
   const int el = slot / C, car = slot - el * C;
   const int env = blk_env_of(P, el, b * P.epb + el);
-  if (blk_track_of(P, b) < 0) return;   // an empty workgroup of a device-built block map (random-track mode)
+  if (blk_empty(P, b)) return;   // an empty workgroup of a device-built block map (random-track mode)
   const TrackDev T = P.tracks[blk_track_of(P, b)];
   const int nw = T.nwall, ng = T.ngroup;
   // walls and groups read straight from the track's global image (L1/L2-resident, shared by every
@@ -1671,7 +1677,7 @@ ray_sensor_kernel(Params P, float* obs, float* terminal_obs, int passes, int SUB
   const int slot = sub * CPW + lc;
   const int el = slot / C, car = slot - el * C;
   const int env = blk_env_of(P, el, b * P.epb + el);
-  if (blk_track_of(P, b) < 0) return;   // an empty workgroup of a device-built block map (random-track mode)
+  if (blk_empty(P, b)) return;   // an empty workgroup of a device-built block map (random-track mode)
   const TrackDev& T = P.tracks[blk_track_of(P, b)];
   PROF_B0(P.blk0 * SUB);   // profile builds: stamp rows numbered over the whole grid (the sharded rollout's shards)
   PROFR_RT(14); PROFR(0); PROFR_XCC(8);   // profile builds: stamp slots 0-7 (16 lanes per car: ray_lane's 2-6), realtime 14 / 15
@@ -1869,7 +1875,7 @@ __global__ void __launch_bounds__(SBLOCK) __attribute__((amdgpu_waves_per_eu(MOD
   const int el = tid / C, car = tid - el * C;
   const int slot = (blockIdx.x + P.blk0) * P.epb + el;
   const int env = blk_env_of(P, el, slot);
-  if (blk_track_of(P, blockIdx.x + P.blk0) < 0) return;   // empty workgroup (device-built block map)
+  if (blk_empty(P, blockIdx.x + P.blk0)) return;   // empty workgroup (device-built block map)
   Car c;
   SegReg sr;
   model_block<false>(P, actions, discrete, want_term, policy, seed, step, pobs, tid, env, env >= 0 ? env * C + car : 0, c, sr);
@@ -2252,7 +2258,7 @@ __global__ void __launch_bounds__(SBLOCK) car_contact_kernel(Params P) {
   const int tid = threadIdx.x, C = P.C;
   const int el = tid / C, car = tid - el * C;
   const int env = blk_env_of(P, el, (blockIdx.x + P.blk0) * P.epb + el);
-  if (blk_track_of(P, blockIdx.x + P.blk0) < 0) return;   // empty workgroup (device-built block map)
+  if (blk_empty(P, blockIdx.x + P.blk0)) return;   // empty workgroup (device-built block map)
   car_contact_block(P, tid, el, car, env, env >= 0 ? env * C + car : 0, smem);
 }
 
@@ -2273,7 +2279,7 @@ __global__ void __launch_bounds__(SBLOCK) LOGIC_ATTR logic_kernel(Params P, floa
   const int slot = (blockIdx.x + P.blk0) * P.epb + el;
   const int env = blk_env_of(P, el, slot);
   const int n = env >= 0 ? env * C + car : 0;
-  if (blk_track_of(P, blockIdx.x + P.blk0) < 0) return;   // empty workgroup (device-built block map)
+  if (blk_empty(P, blockIdx.x + P.blk0)) return;   // empty workgroup (device-built block map)
   PROF_B0(P.blk0);
   LPROF(0);
   Car c;
@@ -2326,7 +2332,7 @@ model_logic_kernel(Params P, const void* actions, int discrete, int want_term, i
   const int slot = (blockIdx.x + P.blk0) * P.epb + el;
   const int env = blk_env_of(P, el, slot);
   const int n = env >= 0 ? env * C + car : 0;
-  if (blk_track_of(P, blockIdx.x + P.blk0) < 0) return;   // empty workgroup (device-built block map)
+  if (blk_empty(P, blockIdx.x + P.blk0)) return;   // empty workgroup (device-built block map)
   Car c;
   SegReg sr;
   double sim;
@@ -2417,7 +2423,7 @@ rollout_kernel(const Params* __restrict__ Pg, int K, int policy, uint64_t seed, 
                uint8_t* car_flags, uint8_t* env_flags, int auto_reset, int traj) {
   ParamsK Pk = (ParamsK)Pg;   // global -> constant address space (same addresses)
   const Params& P = *Pg;
-  if (blk_track_of(P, blockIdx.x) < 0) return;   // empty workgroup (device-built block map)
+  if (blk_empty(P, blockIdx.x)) return;   // empty workgroup (device-built block map)
   PROF_B0(0);
   {
     const TrackDev T = P.tracks[blk_track_of(P, blockIdx.x)];
@@ -2461,7 +2467,7 @@ __global__ void __launch_bounds__(SBLOCK) reset_kernel(Params P, const uint8_t* 
   const int el = tid / C, car = tid - el * C;
   const int slot = blockIdx.x * P.epb + el;
   int env = blk_env_of(P, el, slot);
-  if (blk_track_of(P, blockIdx.x) < 0) return;   // empty workgroup (device-built block map)
+  if (blk_empty(P, blockIdx.x)) return;   // empty workgroup (device-built block map)
   if (env >= 0 && mask && !mask[env]) { P.pose[env * C + car] = make_float4(0.f, 0.f, 0.f, __int_as_float(0)); env = -1; }
   const TrackDev T = P.tracks[blk_track_of(P, blockIdx.x)];
   const WallSet S{T.walls, T.nwall, T.bp, T.sn, T.wfat};
