@@ -56,9 +56,10 @@ struct DSeg {   // per segment, float64 (src/track_generator.py TrackSegment)
 // Ray-candidate lists ("beams"), built on the host (build_beams): for every cell (nascar_set_beam_cell) near the
 // walls and every one of BEAM_NB direction bins, the walls that a ray starting anywhere in the cell with a
 // direction in the bin can reach within 250 m, sorted by a lower bound of their distance from the cell.
-// Entry = (lower bound in cm, floored) << 16 | wall index.  A ray walks its list and stops at the first
-// entry whose lower bound exceeds its best hit so far: the minimum exact fraction over the walls visited
-// is the minimum over all walls, i.e. the reference's Box2D RayCast result.
+// Entry (16 bits) = bound code << 10 | wall index: code c stands for the bound c^2 / 16 m, rounded down from the
+// wall's exact bound (c <= 62; 63 = the sentinel, past every hit), so the codes are conservative and ascend along a
+// list.  A ray walks its list and stops at the first entry whose bound exceeds its best hit so far: the minimum exact
+// fraction over the walls visited is the minimum over all walls, i.e. the reference's Box2D RayCast result.
 #ifndef BEAM_NB
 #define BEAM_NB 256       // direction bins (measured 64: 44.2 us, 128: 41.7, 256: 38.7, 512: 39.1) (a multiple of 16: ray i is BEAM_NB / 16 bins from ray i + 1)
 #endif
@@ -67,28 +68,38 @@ struct DSeg {   // per segment, float64 (src/track_generator.py TrackSegment)
 // 16 adjacent lists
 __host__ __device__ __forceinline__ int beam_slot(int bin) { return (bin % BEAM_STRIDE) * 16 + bin / BEAM_STRIDE; }
 __host__ __device__ __forceinline__ int beam_bin(int slot) { return (slot % 16) * BEAM_STRIDE + slot / 16; }
+#define BEAM_WALL_BITS 10
+#define BEAM_MAX_WALLS (1 << BEAM_WALL_BITS)   // tracks with more walls get no lists (every ray takes the wall-group walk)
+#define BEAM_PAD 0xFFFFu                       // sentinel: code 63, stops every walk
+#define BEAM_CONT_MAX 0xFFFFu                  // continuation entries of one cell (16-bit offsets from the cell's base)
 struct BeamGrid {
   float ox, oy, inv_cell; int nx, ny;
-  const int* cell;          // [nx * ny]: first list of the cell (built cell id * BEAM_NB), -1: not built
-  const uint32_t* ent;      // list continuations, each closed by a BEAM_PAD sentinel
-  // [built cells * BEAM_NB][BEAM_HW] head records: the first BEAM_HEAD entries of each list (padded with
-  // BEAM_PAD) and a tail word -- the ent[] index of the rest of a longer list (0: none) -- so a walk starts with
-  // BEAM_HW independent 16-byte loads and reads the rest in chunks of RAY_CHUNK entries up to the sentinel
-  const uint4* head;
+  // [nx * ny]: (first list of the cell = built cell id * BEAM_NB, -1: no lists; the cell's first ent[] index)
+  const int2* cell;
+  const uint16_t* ent;      // list continuations, each closed by a BEAM_PAD sentinel
+  // [built cells * BEAM_NB] 8-byte head records: the first BEAM_HEAD entries of each list (padded with BEAM_PAD) and
+  // the offset + 1 of the list's continuation from its cell's first ent[] index (0: none), so a walk starts with one
+  // 8-byte load and reads the rest in chunks of RAY_CHUNK entries up to the sentinel.  (Round 5's 16-byte heads held
+  // three 32-bit entries and an absolute index: 256 B of heads per car and step against 128.)
+  const uint2* head;
 };
-#ifndef BEAM_HW
-#define BEAM_HW 1   // 16-byte heads (3 entries + tail): at 1 m cells the median ray walks 2 entries (2-word heads measured slower)
-#endif
-#define BEAM_HEAD (4 * BEAM_HW - 1)
+#define BEAM_HEAD 3
 #ifndef RAY_CHUNK
 #define RAY_CHUNK 4    // list entries past the head requested together
 #endif
-#define BEAM_PAD 0xFFFFFFFFu   // bound 655.35 m: past every best hit (<= 2 * 250 m), so a walk always stops on it
-struct BeamHead { uint4 w[BEAM_HW]; };
-__device__ __forceinline__ BeamHead beam_head(const BeamGrid& G, int li) {
+// an entry's distance bound in m (the sentinel's: beyond every hit) and its wall
+__device__ __forceinline__ float beam_bound(uint32_t v) {
+  const uint32_t c = v >> BEAM_WALL_BITS;
+  return c >= 63u ? 1e30f : (float)(c * c) * 0.0625f;
+}
+__device__ __forceinline__ int beam_wall(uint32_t v) { return (int)(v & (BEAM_MAX_WALLS - 1)); }
+// a walk goes on past an entry while its bound is within the best hit (fraction bi of the 250 m ray), with margin
+__device__ __forceinline__ bool beam_beyond(uint32_t v, float bi) { return beam_bound(v) > bi * 250.0f * 1.00001f + 0.01f; }
+struct BeamHead { uint2 w; uint32_t cb; };   // the head record and its cell's first ent[] index
+__device__ __forceinline__ BeamHead beam_head(const BeamGrid& G, int2 cell, int li) {
   BeamHead h;
-#pragma unroll
-  for (int k = 0; k < BEAM_HW; ++k) h.w[k] = ldg(G.head + (size_t)li * BEAM_HW + k);
+  h.w = ldg(G.head + li);
+  h.cb = (uint32_t)cell.y;
   return h;
 }
 #define LDS_PER_CU ((size_t)160 * 1024)   // gfx950: 160 KiB of LDS per CU, all of which one workgroup may declare
@@ -136,11 +147,27 @@ __device__ __forceinline__ int blk_track_of(const Params& P, int b) { return P.o
 #define EMPTY_GUARD 1
 #endif
 __device__ __forceinline__ bool blk_empty(const Params& P, int b) { return EMPTY_GUARD && P.one_track < 0 && P.blk_track[b] < 0; }
-// BeamGrid list base (built cell id * BEAM_NB) of the cell holding (x, y); -1 outside the built cells
-__device__ __forceinline__ int beam_cell_base(const BeamGrid& G, float x, float y) {
+// The step kernels' workgroup (block-map index) of this dispatch slot.  The dispatcher deals a launch's workgroups
+// round-robin over the 8 XCDs (slot b on XCD b % 8), each with its own L2; with XCD_REMAP, each XCD takes a contiguous
+// run of the launch's workgroups instead, so the state cache lines two neighbouring workgroups share (a workgroup's
+// SoA run of cars rarely ends on a 128-B line) are fetched into one L2, not two.
+#ifndef XCD_REMAP
+#define XCD_REMAP 1
+#endif
+__device__ __forceinline__ int wg_block(const Params& P) {
+#if XCD_REMAP
+  const int nb = gridDim.x, b = blockIdx.x, q = nb >> 3, r = nb & 7, x = b & 7;
+  return P.blk0 + x * q + min(x, r) + (b >> 3);
+#else
+  return blockIdx.x + P.blk0;
+#endif
+}
+// BeamGrid cell record of the cell holding (x, y): (list base = built cell id * BEAM_NB, the cell's first ent[] index);
+// list base -1 outside the built cells
+__device__ __forceinline__ int2 beam_cell(const BeamGrid& G, float x, float y) {
   const float fx = (x - G.ox) * G.inv_cell, fy = (y - G.oy) * G.inv_cell;
   if (fx >= 0.0f && fy >= 0.0f && fx < (float)G.nx && fy < (float)G.ny) return ldg(G.cell + (int)fy * G.nx + (int)fx);
-  return -1;
+  return make_int2(-1, 0);
 }
 
 #define F32P(P, f) ((P).f32 + (size_t)F32_##f * (P).N)
@@ -1347,8 +1374,8 @@ __device__ __forceinline__ float ray_walk_rest(const BeamGrid& G, const float4* 
 #pragma unroll
     for (int q = 0; q < RAY_CHUNK; ++q) {
       const uint32_t v = v4[q];
-      if ((float)(v >> 16) * 0.01f > bi * 250.0f * 1.00001f + 0.01f) { stop = true; break; }
-      const int j = (int)(v & 0xFFFFu);
+      if (beam_beyond(v, bi)) { stop = true; break; }
+      const int j = beam_wall(v);
       PCOUNT(10, 1);
       bi = GW ? wall_cast(ldg(sw + 2 * j), ldg(sw + 2 * j + 1), p1, p2.x, p2.y, dx, dy, bi)
              : wall_cast(sw[2 * j], sw[2 * j + 1], p1, p2.x, p2.y, dx, dy, bi);
@@ -1363,20 +1390,19 @@ template <bool GW, bool COOP = false>
 __device__ __forceinline__ float ray_walk(const BeamGrid& G, const float4* __restrict__ sw, int li, const BeamHead& h, V2 p1,
                                           V2 p2, float dx, float dy, uint32_t* kc = nullptr) {
   float bi = 2.0f;
-  uint32_t hv[4 * BEAM_HW];
-#pragma unroll
-  for (int k = 0; k < BEAM_HW; ++k) { hv[4 * k] = h.w[k].x; hv[4 * k + 1] = h.w[k].y; hv[4 * k + 2] = h.w[k].z; hv[4 * k + 3] = h.w[k].w; }
+  const uint32_t hv[BEAM_HEAD] = {h.w.x & 0xFFFFu, h.w.x >> 16, h.w.y & 0xFFFFu};
   bool more = true;
 #pragma unroll
   for (int k = 0; k < BEAM_HEAD; ++k) {
     const uint32_t v = hv[k];
-    if ((float)(v >> 16) * 0.01f > bi * 250.0f * 1.00001f + 0.01f) { more = false; break; }
-    const int j = (int)(v & 0xFFFFu);
+    if (beam_beyond(v, bi)) { more = false; break; }
+    const int j = beam_wall(v);
     PCOUNT(10, 1);
     bi = GW ? wall_cast(ldg(sw + 2 * j), ldg(sw + 2 * j + 1), p1, p2.x, p2.y, dx, dy, bi)
                : wall_cast(sw[2 * j], sw[2 * j + 1], p1, p2.x, p2.y, dx, dy, bi);
   }
-  const uint32_t tail = hv[BEAM_HEAD];
+  const uint32_t off = h.w.y >> 16;
+  const uint32_t tail = off ? h.cb + off - 1u : 0u;   // (ent[0] is a sentinel: a continuation never starts at 0)
   if (COOP) { *kc = more ? tail : 0u; return bi; }
   if (more && tail != 0u) bi = ray_walk_rest<GW>(G, sw, tail, bi, p1, p2, dx, dy);
   return bi;
@@ -1429,13 +1455,13 @@ __device__ __forceinline__ float ray_walk_coop(const BeamGrid& G, const float4* 
     const float bo = __shfl(bi, owner);
     const V2 po = V(__shfl(p1.x, owner), __shfl(p1.y, owner)), qo = V(__shfl(p2.x, owner), __shfl(p2.y, owner));
     const float dxo = __shfl(dx, owner), dyo = __shfl(dy, owner);
-    const uint32_t v = serve ? ldg(G.ent + ko + o) : BEAM_PAD;
+    const uint32_t v = serve ? (uint32_t)ldg(G.ent + ko + o) : BEAM_PAD;
     const unsigned long long pm = __ballot(v == BEAM_PAD);
     const unsigned long long gm = (lg == 0 ? ~0ull : ((1ull << E) - 1ull)) << (q * E & 63);
     const bool valid = serve && v != BEAM_PAD && !(pm & gm & below);
     float c = bo;
     if (valid) {
-      const int j = (int)(v & 0xFFFFu);
+      const int j = beam_wall(v);
       PCOUNT(10, 1);
       c = GW ? wall_cast(ldg(sw + 2 * j), ldg(sw + 2 * j + 1), po, qo.x, qo.y, dxo, dyo, bo)
              : wall_cast(sw[2 * j], sw[2 * j + 1], po, qo.x, qo.y, dxo, dyo, bo);
@@ -1449,7 +1475,7 @@ __device__ __forceinline__ float ray_walk_coop(const BeamGrid& G, const float4* 
     const unsigned long long gmo = (lg == 0 ? ~0ull : ((1ull << E) - 1ull)) << g0;
     if (k != 0u) {
       bi = gb;
-      const bool stop = (pm & gmo) != 0ull || (float)(vl >> 16) * 0.01f > bi * 250.0f * 1.00001f + 0.01f;
+      const bool stop = (pm & gmo) != 0ull || beam_beyond(vl, bi);
       k = stop ? 0u : k + (uint32_t)E;
     }
   }
@@ -1494,7 +1520,8 @@ __device__ __forceinline__ void ray_lane(const Params& P, const TrackDev& T, con
     const double px = ps.x, py = ps.y, ang = ps.z;
     const double2 cs = P.pose_cs[pass == 0 ? (size_t)n : (size_t)P.N + n];
     if (LPC == 16 && pass == 0) PROFR(2);   // profile builds (16 lanes per car): pose loaded
-    const int base = beam_cell_base(G, p1.x, p1.y);
+    const int2 cell = beam_cell(G, p1.x, p1.y);
+    const int base = cell.x;
     if (LPC == 16 && pass == 0) { asm volatile("" :: "v"(base)); PROFR(3); }   // beam cell looked up
     // direction bin of sa = -radians(22.5 i) + ang (f64; the lists carry a 2e-3 rad guard) -> list slot
     // ray i is exactly BEAM_STRIDE bins clockwise of ray 0 in real arithmetic, and the f64 rounding of
@@ -1511,12 +1538,12 @@ __device__ __forceinline__ void ray_lane(const Params& P, const TrackDev& T, con
 #pragma unroll
     for (int q = 0; q < RPL; ++q) v[q] = 0.0f;
 #if RAY_HEADS_AHEAD
-    // the four rays' list heads requested together (independent 16-byte loads) before the first walk
+    // the four rays' list heads requested together (independent 8-byte loads) before the first walk
     BeamHead hd[RPL];
 #pragma unroll
     for (int q = 0; q < RPL; ++q) {
-      if (base >= 0) hd[q] = beam_head(G, base + slot_of(r + LPC * q));
-      else for (int k = 0; k < BEAM_HW; ++k) hd[q].w[k] = make_uint4(0, 0, 0, 0);
+      if (base >= 0) hd[q] = beam_head(G, cell, base + slot_of(r + LPC * q));
+      else hd[q] = BeamHead{make_uint2(0u, 0u), 0u};
     }
 #pragma unroll
 #else
@@ -1538,17 +1565,17 @@ __device__ __forceinline__ void ray_lane(const Params& P, const TrackDev& T, con
 #if RAY_HEADS_AHEAD
         bi = ray_walk<GW>(G, sw, base + sl, hd[q], p1, p2, dx, dy);
 #elif RAY_NO_WALK   // timing probe only (wrong results): the head load without the walk
-        const BeamHead h = beam_head(G, base + sl);
-        bi = __uint_as_float((h.w[0].x & 1u) | 0x3f800000u);
+        const BeamHead h = beam_head(G, cell, base + sl);
+        bi = __uint_as_float((h.w.x & 1u) | 0x3f800000u);
 #else
 #ifdef NASCAR_PROFILE
-        const BeamHead hh = beam_head(G, base + sl);
-        if (LPC == 16 && pass == 0) { PROFR(4); asm volatile("" :: "v"(hh.w[0].x)); PROFR(5); }   // end points; head loaded
+        const BeamHead hh = beam_head(G, cell, base + sl);
+        if (LPC == 16 && pass == 0) { PROFR(4); asm volatile("" :: "v"(hh.w.x)); PROFR(5); }   // end points; head loaded
         if (LPC == 16 && coop) bi = ray_walk<GW, true>(G, sw, base + sl, hh, p1, p2, dx, dy, &kc);
         else bi = ray_walk<GW>(G, sw, base + sl, hh, p1, p2, dx, dy);
 #else
-        if (LPC == 16 && coop) bi = ray_walk<GW, true>(G, sw, base + sl, beam_head(G, base + sl), p1, p2, dx, dy, &kc);
-        else bi = ray_walk<GW>(G, sw, base + sl, beam_head(G, base + sl), p1, p2, dx, dy);
+        if (LPC == 16 && coop) bi = ray_walk<GW, true>(G, sw, base + sl, beam_head(G, cell, base + sl), p1, p2, dx, dy, &kc);
+        else bi = ray_walk<GW>(G, sw, base + sl, beam_head(G, cell, base + sl), p1, p2, dx, dy);
 #endif
 #endif
       } else {
@@ -1592,7 +1619,8 @@ __device__ __forceinline__ void ray_block_batched(const Params& P, const TrackDe
   constexpr int NJ = 4, RPL = 4;
   const int t = threadIdx.x, r = t & 3, C = P.C;
   const BeamGrid G = T.beam;
-  int n[NJ], base[NJ], slot0[NJ];
+  int n[NJ], slot0[NJ];
+  int2 base[NJ];   // beam cell records (list base, first ent[] index)
   bool ok[NJ];
   float4 pa[NJ];
   double2 cs[NJ];
@@ -1611,7 +1639,7 @@ __device__ __forceinline__ void ray_block_batched(const Params& P, const TrackDe
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
     ok[j] = ok[j] && (__float_as_int(pa[j].w) & PM_A_OBS) != 0;
-    base[j] = ok[j] ? beam_cell_base(G, pa[j].x, pa[j].y) : -1;
+    base[j] = ok[j] ? beam_cell(G, pa[j].x, pa[j].y) : make_int2(-1, 0);
     slot0[j] = beam_slot0((double)pa[j].z);
   }
   V2 p2[NJ][RPL];
@@ -1623,8 +1651,8 @@ __device__ __forceinline__ void ray_block_batched(const Params& P, const TrackDe
       double dxd, dyd;
       p2[j][q] = ray_end(P, pa[j].x, pa[j].y, pa[j].z, cs[j].x, cs[j].y, r + RAY_LPC * q, dxd, dyd);
       const int sl = (slot0[j] & ~15) | ((slot0[j] - (r + RAY_LPC * q)) & 15);
-      if (base[j] >= 0) hd[j][q] = beam_head(G, base[j] + sl);
-      else for (int k = 0; k < BEAM_HW; ++k) hd[j][q].w[k] = make_uint4(0, 0, 0, 0);
+      if (base[j].x >= 0) hd[j][q] = beam_head(G, base[j], base[j].x + sl);
+      else hd[j][q] = BeamHead{make_uint2(0u, 0u), 0u};
     }
   }
 #pragma unroll
@@ -1642,9 +1670,9 @@ __device__ __forceinline__ void ray_block_batched(const Params& P, const TrackDe
       const V2 e = e0;
       const float dx = (e.x - p1.x) * 0.004f, dy = (e.y - p1.y) * 0.004f;   // cull only
       float bi;
-      if (base[j] >= 0) {
+      if (base[j].x >= 0) {
         const int sl = (slot0[j] & ~15) | ((slot0[j] - i) & 15);
-        bi = ray_walk<false>(G, sw, base[j] + sl, h0, p1, e, dx, dy);
+        bi = ray_walk<false>(G, sw, base[j].x + sl, h0, p1, e, dx, dy);
       } else {
         bi = ray_fallback(T, p1, e.x, e.y, dx, dy, pa[j].z, i);
       }
@@ -1852,7 +1880,7 @@ __device__ __forceinline__ void model_block(const Params& P, const void* actions
       tb = ((const float*)actions)[2 * n]; st = ((const float*)actions)[2 * n + 1];
     }
   }
-  TrackDev T = P.tracks[blk_track_of(P, (blockIdx.x + P.blk0))];
+  TrackDev T = P.tracks[blk_track_of(P, wg_block(P))];
   if (tid < T.nseg) {
     const DSeg sg = ldg(T.segs + tid);
     g_step_segs[tid] = sg;
@@ -1873,9 +1901,9 @@ __global__ void __launch_bounds__(SBLOCK) __attribute__((amdgpu_waves_per_eu(MOD
                                                                                                     int policy, uint64_t seed, int64_t step, const float* pobs) {
   const int tid = threadIdx.x, C = P.C;
   const int el = tid / C, car = tid - el * C;
-  const int slot = (blockIdx.x + P.blk0) * P.epb + el;
+  const int slot = wg_block(P) * P.epb + el;
   const int env = blk_env_of(P, el, slot);
-  if (blk_empty(P, blockIdx.x + P.blk0)) return;   // empty workgroup (device-built block map)
+  if (blk_empty(P, wg_block(P))) return;   // empty workgroup (device-built block map)
   Car c;
   SegReg sr;
   model_block<false>(P, actions, discrete, want_term, policy, seed, step, pobs, tid, env, env >= 0 ? env * C + car : 0, c, sr);
@@ -2257,8 +2285,8 @@ __device__ __forceinline__ void car_contact_block(const Params& P, int tid, int 
 __global__ void __launch_bounds__(SBLOCK) car_contact_kernel(Params P) {
   const int tid = threadIdx.x, C = P.C;
   const int el = tid / C, car = tid - el * C;
-  const int env = blk_env_of(P, el, (blockIdx.x + P.blk0) * P.epb + el);
-  if (blk_empty(P, blockIdx.x + P.blk0)) return;   // empty workgroup (device-built block map)
+  const int env = blk_env_of(P, el, wg_block(P) * P.epb + el);
+  if (blk_empty(P, wg_block(P))) return;   // empty workgroup (device-built block map)
   car_contact_block(P, tid, el, car, env, env >= 0 ? env * C + car : 0, smem);
 }
 
@@ -2276,17 +2304,17 @@ __global__ void __launch_bounds__(SBLOCK) LOGIC_ATTR logic_kernel(Params P, floa
   __shared__ TrackLDS TL;
   const int tid = threadIdx.x, C = P.C;
   const int el = tid / C, car = tid - el * C;
-  const int slot = (blockIdx.x + P.blk0) * P.epb + el;
+  const int slot = wg_block(P) * P.epb + el;
   const int env = blk_env_of(P, el, slot);
   const int n = env >= 0 ? env * C + car : 0;
-  if (blk_empty(P, blockIdx.x + P.blk0)) return;   // empty workgroup (device-built block map)
+  if (blk_empty(P, wg_block(P))) return;   // empty workgroup (device-built block map)
   PROF_B0(P.blk0);
   LPROF(0);
   Car c;
   double sim;
   int pend_in, reason_in;
   logic_load(P, env, car, n, c, sim, pend_in, reason_in);   // state loads issued before the staging barrier
-  TrackDev T = P.tracks[blk_track_of(P, (blockIdx.x + P.blk0))];
+  TrackDev T = P.tracks[blk_track_of(P, wg_block(P))];
   stage_track_lds(T, TL, tid);
   __syncthreads();
   T.segs = TL.segs; T.prefix = TL.prefix;
@@ -2314,7 +2342,7 @@ static __device__ void fused_logic_phase(const Params& P, int tid, int el, int c
                                          Car& c, double sim, int pend_in, int reason_in, const SegReg& sr) {
   FusedLogicLDS& F = *(FusedLogicLDS*)smem;
   if (env >= 0) logic_from_model(P, n, c);
-  TrackDev T = P.tracks[blk_track_of(P, (blockIdx.x + P.blk0))];
+  TrackDev T = P.tracks[blk_track_of(P, wg_block(P))];
   if (tid < T.nseg) { F.TL.prefix[tid] = sr.prefix; F.TL.sg[tid] = sr.sg; F.TL.rll[tid] = sr.rll; }   // (model half's loads)
   __syncthreads();
   PROF(7);
@@ -2329,10 +2357,10 @@ model_logic_kernel(Params P, const void* actions, int discrete, int want_term, i
                    float* terminal_obs) {
   const int tid = threadIdx.x, C = P.C;
   const int el = tid / C, car = tid - el * C;
-  const int slot = (blockIdx.x + P.blk0) * P.epb + el;
+  const int slot = wg_block(P) * P.epb + el;
   const int env = blk_env_of(P, el, slot);
   const int n = env >= 0 ? env * C + car : 0;
-  if (blk_empty(P, blockIdx.x + P.blk0)) return;   // empty workgroup (device-built block map)
+  if (blk_empty(P, wg_block(P))) return;   // empty workgroup (device-built block map)
   Car c;
   SegReg sr;
   double sim;
@@ -2825,9 +2853,9 @@ struct HostTrack {
   HostGrid bp, sn;
   struct {
     BeamGrid g{};
-    std::vector<int> cell; std::vector<uint32_t> ent; std::vector<uint4> head;
-    int* d_cell = nullptr; uint32_t* d_ent = nullptr; uint4* d_head = nullptr;
-    size_t entries = 0, nlist = 0;
+    std::vector<int2> cell; std::vector<uint16_t> ent; std::vector<uint2> head;
+    int2* d_cell = nullptr; uint16_t* d_ent = nullptr; uint2* d_head = nullptr;
+    size_t entries = 0, nlist = 0, dropped = 0;   // dropped: cells whose continuations overflow the 16-bit offsets
     double build_s = 0.0;
   } beam;
   std::vector<float4> groups; float4* d_groups = nullptr;
@@ -2936,7 +2964,7 @@ static void build_grids(HostTrack& t) {
 // Both are conservative, so the walk in ray_sensor_kernel visits every wall that can be the first hit.
 // Cell size: the cell's disk widens every wall's angular arc and lowers its distance bound, so smaller cells give
 // shorter walks (steady-state sensor tails; bench step 191 -> 178 / 174 / 168 / 167 us at 2 / 1.5 / 1 / 0.75 m,
-// tools/ab2.sh) at ~0.8 GB of lists per track at 1 m (16-byte heads + sentinel-terminated continuations).
+// tools/ab2.sh) at 0.2-0.5 GB of lists per track at 1 m (8-byte heads + sentinel-terminated continuations).
 #ifndef BEAM_CELL_M
 #define BEAM_CELL_M 1.0f
 #endif
@@ -2986,10 +3014,11 @@ static void build_beams(HostTrack& t, const float cell) {
         if (segdist(j, x, y) <= D) mark[(size_t)cy * nx + cx] = 1;
       }
   }
-  B.cell.assign((size_t)nx * ny, -1);
+  B.cell.assign((size_t)nx * ny, make_int2(-1, 0));
   std::vector<int> cells;
-  for (size_t k = 0; k < mark.size(); ++k)
-    if (mark[k]) { B.cell[k] = (int)cells.size() * BEAM_NB; cells.push_back((int)k); }
+  if (nw <= BEAM_MAX_WALLS)   // (more walls than the 10-bit entries address: no lists, every ray takes the wall-group walk)
+    for (size_t k = 0; k < mark.size(); ++k)
+      if (mark[k]) { B.cell[k] = make_int2((int)cells.size() * BEAM_NB, 0); cells.push_back((int)k); }
   const int ncell = (int)cells.size();
   const double rc = cell * 0.70710678 + 0.05, two_pi = 2.0 * M_PI, dbin = two_pi / BEAM_NB;
   std::vector<std::vector<uint32_t>> lists((size_t)ncell * BEAM_NB);
@@ -3021,43 +3050,67 @@ static void build_beams(HostTrack& t, const float cell) {
   std::vector<std::thread> th;
   for (int k = 0; k < nth; ++k) th.emplace_back(work, (int)((long)ncell * k / nth), (int)((long)ncell * (k + 1) / nth));
   for (auto& x : th) x.join();
-  // per list (cell-major, slot order, beam_slot): the head record holds its first BEAM_HEAD entries (BEAM_PAD
-  // filled) and, when the list is longer, in its last word the ent[] index of the continuation -- the remaining
-  // entries followed by one BEAM_PAD sentinel (bound 655.35 m stops every walk), so a walk needs no list end.
-  // ent[0] is a sentinel (tail word 0 = no continuation); BEAM_COOP_PAD sentinels close the array (the chunked and the
-  // wave-cooperative walks read past a list's sentinel).
+  // 16-bit entries: the bound code c = floor(4 sqrt(bound)), so c^2 / 16 m <= the wall's bound (rounded down again where
+  // the double sqrt rounded up onto an integer), at most 62; each list sorted by entry, so the codes ascend
+  auto code_of = [](uint32_t e) {
+    const double lb = (double)(e >> 16) * 0.01;   // the cm bound, itself rounded down
+    int c = std::min(62, (int)std::floor(4.0 * std::sqrt(lb)));
+    while (c > 0 && (double)(c * c) * 0.0625 > lb) --c;
+    return (uint16_t)((c << BEAM_WALL_BITS) | (e & 0xFFFFu));
+  };
+  // per list (cell-major, slot order, beam_slot): the head record holds its first BEAM_HEAD entries (BEAM_PAD filled)
+  // and, when the list is longer, 1 + the offset of its continuation -- the remaining entries followed by one BEAM_PAD
+  // sentinel, so a walk needs no list end -- from the cell's first ent[] index (cell record .y).  ent[0] is a sentinel;
+  // BEAM_COOP_PAD sentinels close the array (the chunked and the wave-cooperative walks read past a list's sentinel).
+  // A cell whose continuations would exceed the 16-bit offsets keeps no lists (its rays take the wall-group walk).
   const size_t nlist = (size_t)ncell * BEAM_NB;
-  B.head.assign(nlist * BEAM_HW, make_uint4(BEAM_PAD, BEAM_PAD, BEAM_PAD, BEAM_PAD));
-  B.ent.assign(1, BEAM_PAD);
+  B.head.assign(nlist, make_uint2(BEAM_PAD | (BEAM_PAD << 16), BEAM_PAD));
+  B.ent.assign(1, (uint16_t)BEAM_PAD);
   B.entries = 0;
-  for (int ci = 0; ci < ncell; ++ci)
+  B.dropped = 0;
+  std::vector<uint16_t> L16;
+  for (int ci = 0; ci < ncell; ++ci) {
+    size_t cont = 0;
+    for (int slot = 0; slot < BEAM_NB; ++slot) {
+      const size_t len = lists[(size_t)ci * BEAM_NB + slot].size();
+      if (len > (size_t)BEAM_HEAD) cont += len - BEAM_HEAD + 1;
+    }
+    int2& rec = B.cell[cells[ci]];
+    if (cont >= BEAM_CONT_MAX) { rec = make_int2(-1, 0); ++B.dropped; continue; }
+    rec.y = (int)B.ent.size();
     for (int slot = 0; slot < BEAM_NB; ++slot) {
       const auto& L = lists[(size_t)ci * BEAM_NB + beam_bin(slot)];
-      const size_t s = (size_t)ci * BEAM_NB + slot;
       B.entries += L.size();
-      uint32_t h[4 * BEAM_HW];
-      for (int k = 0; k < BEAM_HEAD; ++k) h[k] = (size_t)k < L.size() ? L[k] : BEAM_PAD;
-      h[BEAM_HEAD] = 0u;
-      if (L.size() > (size_t)BEAM_HEAD) {
-        h[BEAM_HEAD] = (uint32_t)B.ent.size();
-        B.ent.insert(B.ent.end(), L.begin() + BEAM_HEAD, L.end());
-        B.ent.push_back(BEAM_PAD);
+      L16.resize(L.size());
+      for (size_t k = 0; k < L.size(); ++k) L16[k] = code_of(L[k]);
+      std::sort(L16.begin(), L16.end());
+      uint32_t h[4];
+      for (int k = 0; k < BEAM_HEAD; ++k) h[k] = (size_t)k < L16.size() ? L16[k] : BEAM_PAD;
+      h[3] = 0u;
+      if (L16.size() > (size_t)BEAM_HEAD) {
+        h[3] = (uint32_t)(B.ent.size() - (size_t)rec.y) + 1u;
+        B.ent.insert(B.ent.end(), L16.begin() + BEAM_HEAD, L16.end());
+        B.ent.push_back((uint16_t)BEAM_PAD);
       }
-      for (int k = 0; k < BEAM_HW; ++k) B.head[s * BEAM_HW + k] = make_uint4(h[4 * k], h[4 * k + 1], h[4 * k + 2], h[4 * k + 3]);
+      B.head[(size_t)ci * BEAM_NB + slot] = make_uint2(h[0] | (h[1] << 16), h[2] | (h[3] << 16));
     }
-  for (int k = 0; k < (RAY_CHUNK > BEAM_COOP_PAD ? RAY_CHUNK : BEAM_COOP_PAD); ++k) B.ent.push_back(BEAM_PAD);
+  }
+  for (int k = 0; k < (RAY_CHUNK > BEAM_COOP_PAD ? RAY_CHUNK : BEAM_COOP_PAD); ++k) B.ent.push_back((uint16_t)BEAM_PAD);
+  if (getenv("NASCAR_VERBOSE"))
+    fprintf(stderr, "build_beams: %d cells with lists, %zu dropped (continuation offsets), %zu entries, heads %.1f MB + "
+            "continuations %.1f MB\n", ncell, B.dropped, B.entries, 8.0 * B.head.size() / 1e6, 2.0 * B.ent.size() / 1e6);
   B.nlist = nlist;
   B.build_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
 }
 static int upload_beams(HostTrack& t) {
   auto& B = t.beam;
-  if (B.ent.size() >= 0xFFFFFFF0u) return fail("beam list continuations hold %zu entries (32-bit offsets)", B.ent.size());
-  HIPCHK(hipMalloc(&B.d_cell, sizeof(int) * B.cell.size()));
-  HIPCHK(hipMemcpy(B.d_cell, B.cell.data(), sizeof(int) * B.cell.size(), hipMemcpyHostToDevice));
-  HIPCHK(hipMalloc(&B.d_ent, sizeof(uint32_t) * std::max<size_t>(B.ent.size(), 1)));
-  if (!B.ent.empty()) HIPCHK(hipMemcpy(B.d_ent, B.ent.data(), sizeof(uint32_t) * B.ent.size(), hipMemcpyHostToDevice));
-  HIPCHK(hipMalloc(&B.d_head, sizeof(uint4) * std::max<size_t>(B.head.size(), 1)));
-  if (!B.head.empty()) HIPCHK(hipMemcpy(B.d_head, B.head.data(), sizeof(uint4) * B.head.size(), hipMemcpyHostToDevice));
+  if (B.ent.size() >= 0x7FFFFFF0u) return fail("beam list continuations hold %zu entries (31-bit cell offsets)", B.ent.size());
+  HIPCHK(hipMalloc(&B.d_cell, sizeof(int2) * B.cell.size()));
+  HIPCHK(hipMemcpy(B.d_cell, B.cell.data(), sizeof(int2) * B.cell.size(), hipMemcpyHostToDevice));
+  HIPCHK(hipMalloc(&B.d_ent, sizeof(uint16_t) * std::max<size_t>(B.ent.size(), 1)));
+  if (!B.ent.empty()) HIPCHK(hipMemcpy(B.d_ent, B.ent.data(), sizeof(uint16_t) * B.ent.size(), hipMemcpyHostToDevice));
+  HIPCHK(hipMalloc(&B.d_head, sizeof(uint2) * std::max<size_t>(B.head.size(), 1)));
+  if (!B.head.empty()) HIPCHK(hipMemcpy(B.d_head, B.head.data(), sizeof(uint2) * B.head.size(), hipMemcpyHostToDevice));
   B.g.cell = B.d_cell; B.g.ent = B.d_ent; B.g.head = B.d_head;
   return 0;
 }
@@ -3079,7 +3132,7 @@ static int upload_grid(HostGrid& G) {
 // A built track: the device tables of one .track (walls, segments, grids, beam lists, sensor image), read-only
 // once built.  Handles share them through a process-wide cache keyed by the track's input arrays and the device:
 // every env of a batch, every VecEnv sub-engine and every later handle on the same track uses one copy (the beam
-// lists are ~0.8 GB per track at 1 m cells and take ~2 s of host time to build).  The last handle to drop a
+// lists are 0.2-0.5 GB per track at 1 m cells and take ~2 s of host time to build).  The last handle to drop a
 // build frees its device memory.
 struct TrackBuild {
   int device = 0;
@@ -3450,11 +3503,11 @@ static int upload_track(HostTrack& t, size_t& lds_out) {
             "(%zu entries, mean %.1f per cell)\n", t.walls.size(), t.groups.size(), t.bp.g.nx, t.bp.g.ny, t.bp.idx.size(),
             t.sn.g.nx, t.sn.g.ny, t.sn.idx.size(), (double)t.sn.idx.size() / ((double)t.sn.g.nx * t.sn.g.ny));
   if (getenv("NASCAR_VERBOSE"))
-    fprintf(stderr, "nascar_add_track: beam grid %dx%d (%.2f m cells), %zu cells with lists, %zu entries (mean %.2f per "
-            "list), heads %.1f MB + continuations %.1f MB + cell map %.1f MB, built in %.2f s\n", t.beam.g.nx, t.beam.g.ny,
-            1.0 / (double)t.beam.g.inv_cell, t.beam.nlist / BEAM_NB, t.beam.entries,
-            (double)t.beam.entries / std::max<size_t>(1, t.beam.nlist), 16.0 * t.beam.head.size() / 1e6,
-            4.0 * t.beam.ent.size() / 1e6, 4.0 * t.beam.cell.size() / 1e6, t.beam.build_s);
+    fprintf(stderr, "nascar_add_track: beam grid %dx%d (%.2f m cells), %zu cells with lists (%zu dropped: continuation "
+            "offsets), %zu entries (mean %.2f per list), heads %.1f MB + continuations %.1f MB + cell map %.1f MB, built in "
+            "%.2f s\n", t.beam.g.nx, t.beam.g.ny, 1.0 / (double)t.beam.g.inv_cell, t.beam.nlist / BEAM_NB - t.beam.dropped,
+            t.beam.dropped, t.beam.entries, (double)t.beam.entries / std::max<size_t>(1, t.beam.nlist),
+            8.0 * t.beam.head.size() / 1e6, 2.0 * t.beam.ent.size() / 1e6, 8.0 * t.beam.cell.size() / 1e6, t.beam.build_s);
   t.beam.cell.clear(); t.beam.ent.clear(); t.beam.head.clear();
   t.beam.cell.shrink_to_fit(); t.beam.ent.shrink_to_fit(); t.beam.head.shrink_to_fit();
   lds_out = sizeof(LWall) * t.walls.size();
@@ -3462,12 +3515,12 @@ static int upload_track(HostTrack& t, size_t& lds_out) {
 }
 
 // ------------------------------------------------------------------ track cache on disk (nascar_set_track_cache)
-// A host build (walls, grids and ~0.8 GB of beam lists per track at 1 m cells: ~2 s of 16 threads) written once and read
+// A host build (walls, grids and 0.2-0.5 GB of beam lists per track at 1 m cells: ~2 s of 16 threads) written once and read
 // by every later process: ranks of one node (bench.py --gpus N, learn/ppo.py-style SubprocVecEnv runs) share one build
 // per track.  File = magic, format version, the full key (segments, walls, total length, cell size: compared byte for
 // byte on load, so a hash collision can only miss), then the host tables.  Written to a temporary name and renamed; the
 // builders of one key serialise on an flock'ed lock file, so concurrent ranks build each track once and the others load.
-static const uint32_t TRACK_FILE_VERSION = 1;
+static const uint32_t TRACK_FILE_VERSION = 2;   // 2: 8-byte heads, 16-bit entries (round 6)
 static std::string g_cache_dir;                       // "" = no disk cache (default)
 static int g_retain = 8;                              // builds kept alive after their last handle (most recent first)
 static std::deque<std::shared_ptr<TrackBuild>>* g_retained = new std::deque<std::shared_ptr<TrackBuild>>();
@@ -3507,7 +3560,7 @@ template <class IO, class HT> static void track_io(IO& io, HT& t) {   // the hos
   io.pod(t.bp.g); io.vec(t.bp.start); io.vec(t.bp.idx); io.vec(t.bp.box);
   io.pod(t.sn.g); io.vec(t.sn.start); io.vec(t.sn.idx); io.vec(t.sn.box);
   io.pod(t.beam.g); io.vec(t.beam.cell); io.vec(t.beam.ent); io.vec(t.beam.head);
-  io.pod(t.beam.entries); io.pod(t.beam.nlist); io.pod(t.beam.build_s);
+  io.pod(t.beam.entries); io.pod(t.beam.nlist); io.pod(t.beam.dropped); io.pod(t.beam.build_s);
   io.vec(t.groups);
 }
 static bool load_track_file(const std::string& path, const std::string& key, HostTrack& t) {

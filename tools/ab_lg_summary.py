@@ -36,5 +36,5 @@ for kt in sorted(glob.glob(os.path.join(d, "kt*"))):
             acc[k][1] += cars
         for k, (b, n) in acc.items():
             per[k] += b / max(n, 1)
-    print(f"lg{v}: sensor {dur.get('ray_sensor_kernel', 0):.2f} us/dispatch, {per['ray_sensor_kernel']:.0f} B/car; "
+    print(f"{v}: sensor {dur.get('ray_sensor_kernel', 0):.2f} us/dispatch, {per['ray_sensor_kernel']:.0f} B/car; "
           f"model_logic {dur.get('model_logic_kernel', 0):.2f} us, {per['model_logic_kernel']:.0f} B/car")

@@ -55,6 +55,7 @@ def main():
     ap.add_argument("--every", type=int, default=25)
     ap.add_argument("--envs", type=int, default=16)
     ap.add_argument("--sub", type=int, default=8)
+    ap.add_argument("--heads", action="store_true", help="head-format study (continuation reads, quantised bounds)")
     a = ap.parse_args()
     from nascargymnasium_amd.track import build_walls, load_track, track_path
     path = track_path(a.track)
@@ -78,6 +79,7 @@ def main():
     sens = np.zeros((len(pf), 16), np.float32)
     orc.L.or_sensors(orc.h, pf.ctypes.data_as(fp), len(pf), sens.ctypes.data_as(fp))
     walked, listlen, free_sub, hit = [], [], [], []
+    headst = {}
     cache = {}
     for n, (x, y, ang) in enumerate(poses):
         cx, cy = int((np.float32(x) - np.float32(ox)) / CELL), int((np.float32(y) - np.float32(oy)) / CELL)
@@ -110,6 +112,13 @@ def main():
             L = np.sort(lb[member])
             walked.append(int(np.searchsorted(L, best, side="right")) + (1 if (L > best).any() else 0))
             listlen.append(len(L))
+            if a.heads:    # head-format study: continuation reads and casts with exact / quantised bounds
+                for qn, Lq in (("cm", np.floor(L * 100) / 100), ("q6", (np.floor(np.minimum(4 * np.sqrt(L), 62)) / 4) ** 2),
+                               ("q8", (np.floor(np.minimum(16 * np.sqrt(L), 254)) / 16) ** 2)):
+                    k = int(np.searchsorted(Lq, best, side="right"))
+                    casts = k + (1 if k < len(Lq) else 0)
+                    for H in (2, 3):
+                        headst.setdefault((qn, H), []).append((k >= H and len(Lq) > H, casts, max(0, len(Lq) - H)))
             hit.append(sens[n, i] < 1.0)
             # sub-bin certificate: no member's arc intersects the ray's sub-bin (with guard)
             sub = int((u * NB - b) * a.sub)
@@ -119,6 +128,10 @@ def main():
             any_sub = (member & (inside | (rel2 <= span) | ((lo - slo) % (2 * np.pi) < w))).any()
             free_sub.append(not any_sub)
     walked, listlen, free_sub, hit = map(np.array, (walked, listlen, free_sub, hit))
+    for (qn, H), v in sorted(headst.items()):
+        v = np.array(v)
+        print(f"heads {qn} H={H}: rays reading a continuation {v[:, 0].mean():.4f}, casts per ray {v[:, 1].mean():.3f}, "
+              f"p99 {np.percentile(v[:, 1], 99):.0f}")
     print(f"rays {len(walked)}: hit {hit.mean():.3f}; list length mean {listlen.mean():.1f} p99 {np.percentile(listlen, 99):.0f}")
     print(f"walked entries: mean {walked.mean():.2f}, p50 {np.percentile(walked, 50):.0f}, p90 {np.percentile(walked, 90):.0f}, "
           f"p99 {np.percentile(walked, 99):.0f}, max {walked.max()}")
