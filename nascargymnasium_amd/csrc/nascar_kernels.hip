@@ -56,9 +56,9 @@ struct DSeg {   // per segment, float64 (src/track_generator.py TrackSegment)
 // Ray-candidate lists ("beams"), built on the host (build_beams): for every cell (nascar_set_beam_cell) near the
 // walls and every one of BEAM_NB direction bins, the walls that a ray starting anywhere in the cell with a
 // direction in the bin can reach within 250 m, sorted by a lower bound of their distance from the cell.
-// Entry (16 bits) = bound code << 10 | wall index: code c stands for the bound c^2 / 16 m, rounded down from the
-// wall's exact bound (c <= 62; 63 = the sentinel, past every hit), so the codes are conservative and ascend along a
-// list.  A ray walks its list and stops at the first entry whose bound exceeds its best hit so far: the minimum exact
+// Entry (16 bits) = bound code << wbits | wall index (wbits = 10 up to 1024 walls, up to 13 for 8192): code c stands
+// for the bound c^2 * kq m, rounded down from the wall's exact bound (c < cmax = 2^(16 - wbits) - 1, the sentinel's
+// code, past every hit), so the codes are conservative and ascend along a list.  A ray walks its list and stops at the first entry whose bound exceeds its best hit so far: the minimum exact
 // fraction over the walls visited is the minimum over all walls, i.e. the reference's Box2D RayCast result.
 #ifndef BEAM_NB
 #define BEAM_NB 256       // direction bins (measured 64: 44.2 us, 128: 41.7, 256: 38.7, 512: 39.1) (a multiple of 16: ray i is BEAM_NB / 16 bins from ray i + 1)
@@ -68,12 +68,12 @@ struct DSeg {   // per segment, float64 (src/track_generator.py TrackSegment)
 // 16 adjacent lists
 __host__ __device__ __forceinline__ int beam_slot(int bin) { return (bin % BEAM_STRIDE) * 16 + bin / BEAM_STRIDE; }
 __host__ __device__ __forceinline__ int beam_bin(int slot) { return (slot % 16) * BEAM_STRIDE + slot / 16; }
-#define BEAM_WALL_BITS 10
-#define BEAM_MAX_WALLS (1 << BEAM_WALL_BITS)   // tracks with more walls get no lists (every ray takes the wall-group walk)
-#define BEAM_PAD 0xFFFFu                       // sentinel: code 63, stops every walk
+#define BEAM_MAX_WALL_BITS 13                  // tracks with more than 8192 walls get no lists (the wall-group walk)
+#define BEAM_PAD 0xFFFFu                       // sentinel: the largest code, stops every walk
 #define BEAM_CONT_MAX 0xFFFFu                  // continuation entries of one cell (16-bit offsets from the cell's base)
 struct BeamGrid {
   float ox, oy, inv_cell; int nx, ny;
+  uint32_t wbits, wmask, cmax; float kq;   // entry layout: wall index bits, their mask, sentinel code, bound scale (m)
   // [nx * ny]: (first list of the cell = built cell id * BEAM_NB, -1: no lists; the cell's first ent[] index)
   const int2* cell;
   const uint16_t* ent;      // list continuations, each closed by a BEAM_PAD sentinel
@@ -88,13 +88,15 @@ struct BeamGrid {
 #define RAY_CHUNK 4    // list entries past the head requested together
 #endif
 // an entry's distance bound in m (the sentinel's: beyond every hit) and its wall
-__device__ __forceinline__ float beam_bound(uint32_t v) {
-  const uint32_t c = v >> BEAM_WALL_BITS;
-  return c >= 63u ? 1e30f : (float)(c * c) * 0.0625f;
+__device__ __forceinline__ float beam_bound(const BeamGrid& G, uint32_t v) {
+  const uint32_t c = v >> G.wbits;
+  return c >= G.cmax ? 1e30f : (float)(c * c) * G.kq;
 }
-__device__ __forceinline__ int beam_wall(uint32_t v) { return (int)(v & (BEAM_MAX_WALLS - 1)); }
+__device__ __forceinline__ int beam_wall(const BeamGrid& G, uint32_t v) { return (int)(v & G.wmask); }
 // a walk goes on past an entry while its bound is within the best hit (fraction bi of the 250 m ray), with margin
-__device__ __forceinline__ bool beam_beyond(uint32_t v, float bi) { return beam_bound(v) > bi * 250.0f * 1.00001f + 0.01f; }
+__device__ __forceinline__ bool beam_beyond(const BeamGrid& G, uint32_t v, float bi) {
+  return beam_bound(G, v) > bi * 250.0f * 1.00001f + 0.01f;
+}
 struct BeamHead { uint2 w; uint32_t cb; };   // the head record and its cell's first ent[] index
 __device__ __forceinline__ BeamHead beam_head(const BeamGrid& G, int2 cell, int li) {
   BeamHead h;
@@ -1374,8 +1376,8 @@ __device__ __forceinline__ float ray_walk_rest(const BeamGrid& G, const float4* 
 #pragma unroll
     for (int q = 0; q < RAY_CHUNK; ++q) {
       const uint32_t v = v4[q];
-      if (beam_beyond(v, bi)) { stop = true; break; }
-      const int j = beam_wall(v);
+      if (beam_beyond(G, v, bi)) { stop = true; break; }
+      const int j = beam_wall(G, v);
       PCOUNT(10, 1);
       bi = GW ? wall_cast(ldg(sw + 2 * j), ldg(sw + 2 * j + 1), p1, p2.x, p2.y, dx, dy, bi)
              : wall_cast(sw[2 * j], sw[2 * j + 1], p1, p2.x, p2.y, dx, dy, bi);
@@ -1395,8 +1397,8 @@ __device__ __forceinline__ float ray_walk(const BeamGrid& G, const float4* __res
 #pragma unroll
   for (int k = 0; k < BEAM_HEAD; ++k) {
     const uint32_t v = hv[k];
-    if (beam_beyond(v, bi)) { more = false; break; }
-    const int j = beam_wall(v);
+    if (beam_beyond(G, v, bi)) { more = false; break; }
+    const int j = beam_wall(G, v);
     PCOUNT(10, 1);
     bi = GW ? wall_cast(ldg(sw + 2 * j), ldg(sw + 2 * j + 1), p1, p2.x, p2.y, dx, dy, bi)
                : wall_cast(sw[2 * j], sw[2 * j + 1], p1, p2.x, p2.y, dx, dy, bi);
@@ -1461,7 +1463,7 @@ __device__ __forceinline__ float ray_walk_coop(const BeamGrid& G, const float4* 
     const bool valid = serve && v != BEAM_PAD && !(pm & gm & below);
     float c = bo;
     if (valid) {
-      const int j = beam_wall(v);
+      const int j = beam_wall(G, v);
       PCOUNT(10, 1);
       c = GW ? wall_cast(ldg(sw + 2 * j), ldg(sw + 2 * j + 1), po, qo.x, qo.y, dxo, dyo, bo)
              : wall_cast(sw[2 * j], sw[2 * j + 1], po, qo.x, qo.y, dxo, dyo, bo);
@@ -1475,7 +1477,7 @@ __device__ __forceinline__ float ray_walk_coop(const BeamGrid& G, const float4* 
     const unsigned long long gmo = (lg == 0 ? ~0ull : ((1ull << E) - 1ull)) << g0;
     if (k != 0u) {
       bi = gb;
-      const bool stop = (pm & gmo) != 0ull || beam_beyond(vl, bi);
+      const bool stop = (pm & gmo) != 0ull || beam_beyond(G, vl, bi);
       k = stop ? 0u : k + (uint32_t)E;
     }
   }
@@ -3014,9 +3016,15 @@ static void build_beams(HostTrack& t, const float cell) {
         if (segdist(j, x, y) <= D) mark[(size_t)cy * nx + cx] = 1;
       }
   }
+  // entry layout: 10 wall bits up to 1024 walls (6-bit codes of c^2 / 16 m), then one more per doubling; the code scale
+  // keeps the largest non-sentinel code near 240 m (a 250 m ray)
+  uint32_t wb = 10;
+  while (wb < BEAM_MAX_WALL_BITS && nw > (1 << wb)) ++wb;
+  B.g.wbits = wb; B.g.wmask = (1u << wb) - 1u; B.g.cmax = (1u << (16 - wb)) - 1u;
+  B.g.kq = (float)(0.0625 * std::pow(62.0 / (double)(B.g.cmax - 1), 2.0));
   B.cell.assign((size_t)nx * ny, make_int2(-1, 0));
   std::vector<int> cells;
-  if (nw <= BEAM_MAX_WALLS)   // (more walls than the 10-bit entries address: no lists, every ray takes the wall-group walk)
+  if (nw <= (1 << BEAM_MAX_WALL_BITS))   // (more walls than the entries address: no lists, the wall-group walk)
     for (size_t k = 0; k < mark.size(); ++k)
       if (mark[k]) { B.cell[k] = make_int2((int)cells.size() * BEAM_NB, 0); cells.push_back((int)k); }
   const int ncell = (int)cells.size();
@@ -3050,13 +3058,15 @@ static void build_beams(HostTrack& t, const float cell) {
   std::vector<std::thread> th;
   for (int k = 0; k < nth; ++k) th.emplace_back(work, (int)((long)ncell * k / nth), (int)((long)ncell * (k + 1) / nth));
   for (auto& x : th) x.join();
-  // 16-bit entries: the bound code c = floor(4 sqrt(bound)), so c^2 / 16 m <= the wall's bound (rounded down again where
-  // the double sqrt rounded up onto an integer), at most 62; each list sorted by entry, so the codes ascend
-  auto code_of = [](uint32_t e) {
+  // 16-bit entries: the bound code c = floor(sqrt(bound / kq)), so c^2 kq <= the wall's bound (rounded down again where
+  // the double sqrt rounded up onto an integer), at most cmax - 1; each list sorted by entry, so the codes ascend
+  const uint32_t cmax = B.g.cmax;
+  const double kq = (double)B.g.kq;
+  auto code_of = [&](uint32_t e) {
     const double lb = (double)(e >> 16) * 0.01;   // the cm bound, itself rounded down
-    int c = std::min(62, (int)std::floor(4.0 * std::sqrt(lb)));
-    while (c > 0 && (double)(c * c) * 0.0625 > lb) --c;
-    return (uint16_t)((c << BEAM_WALL_BITS) | (e & 0xFFFFu));
+    int c = (int)std::min<double>((double)cmax - 1.0, std::floor(std::sqrt(lb / kq)));
+    while (c > 0 && (double)(c * c) * kq > lb) --c;
+    return (uint16_t)(((uint32_t)c << wb) | (e & 0xFFFFu));
   };
   // per list (cell-major, slot order, beam_slot): the head record holds its first BEAM_HEAD entries (BEAM_PAD filled)
   // and, when the list is longer, 1 + the offset of its continuation -- the remaining entries followed by one BEAM_PAD
@@ -3097,8 +3107,9 @@ static void build_beams(HostTrack& t, const float cell) {
   }
   for (int k = 0; k < (RAY_CHUNK > BEAM_COOP_PAD ? RAY_CHUNK : BEAM_COOP_PAD); ++k) B.ent.push_back((uint16_t)BEAM_PAD);
   if (getenv("NASCAR_VERBOSE"))
-    fprintf(stderr, "build_beams: %d cells with lists, %zu dropped (continuation offsets), %zu entries, heads %.1f MB + "
-            "continuations %.1f MB\n", ncell, B.dropped, B.entries, 8.0 * B.head.size() / 1e6, 2.0 * B.ent.size() / 1e6);
+    fprintf(stderr, "build_beams: %d walls (%u-bit wall indices, bound codes of %.4f m x c^2), %d cells with lists, %zu "
+            "dropped (continuation offsets), %zu entries, heads %.1f MB + continuations %.1f MB\n", nw, B.g.wbits,
+            (double)B.g.kq, ncell, B.dropped, B.entries, 8.0 * B.head.size() / 1e6, 2.0 * B.ent.size() / 1e6);
   B.nlist = nlist;
   B.build_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
 }
@@ -3520,7 +3531,7 @@ static int upload_track(HostTrack& t, size_t& lds_out) {
 // per track.  File = magic, format version, the full key (segments, walls, total length, cell size: compared byte for
 // byte on load, so a hash collision can only miss), then the host tables.  Written to a temporary name and renamed; the
 // builders of one key serialise on an flock'ed lock file, so concurrent ranks build each track once and the others load.
-static const uint32_t TRACK_FILE_VERSION = 2;   // 2: 8-byte heads, 16-bit entries (round 6)
+static const uint32_t TRACK_FILE_VERSION = 3;   // 3: 8-byte heads, 16-bit entries, per-track wall bits (round 6)
 static std::string g_cache_dir;                       // "" = no disk cache (default)
 static int g_retain = 8;                              // builds kept alive after their last handle (most recent first)
 static std::deque<std::shared_ptr<TrackBuild>>* g_retained = new std::deque<std::shared_ptr<TrackBuild>>();
