@@ -74,11 +74,14 @@ __host__ __device__ __forceinline__ int beam_bin(int slot) { return (slot % 16) 
 struct BeamGrid {
   float ox, oy, inv_cell; int nx, ny;
   uint32_t wbits, wmask, cmax; float kq;   // entry layout: wall index bits, their mask, sentinel code, bound scale (m)
-  // [nx * ny]: (first list of the cell = built cell id * BEAM_NB, -1: no lists; the cell's first ent[] index)
-  const int2* cell;
+  // the cell map in chunks of BEAM_CHUNK cells along x, [ny][nxc]: (first list of the chunk's first built cell = its
+  // id * BEAM_NB, the chunk's first ent[] index, the mask of its built cells, 0) -- the built cells of a chunk have
+  // consecutive ids, so a cell's list base is the chunk's plus BEAM_NB per built cell below it.  ~0.5 MB per track
+  // (a dense int2 per cell was ~9 MB, a random 128-byte line per car that no L2 held; this table stays cached)
+  const int4* chunk; int nxc;
   const uint16_t* ent;      // list continuations, each closed by a BEAM_PAD sentinel
   // [built cells * BEAM_NB] 8-byte head records: the first BEAM_HEAD entries of each list (padded with BEAM_PAD) and
-  // the offset + 1 of the list's continuation from its cell's first ent[] index (0: none), so a walk starts with one
+  // the offset + 1 of the list's continuation from its chunk's first ent[] index (0: none), so a walk starts with one
   // 8-byte load and reads the rest in chunks of RAY_CHUNK entries up to the sentinel.  (Round 5's 16-byte heads held
   // three 32-bit entries and an absolute index: 256 B of heads per car and step against 128.)
   const uint2* head;
@@ -97,7 +100,8 @@ __device__ __forceinline__ int beam_wall(const BeamGrid& G, uint32_t v) { return
 __device__ __forceinline__ bool beam_beyond(const BeamGrid& G, uint32_t v, float bi) {
   return beam_bound(G, v) > bi * 250.0f * 1.00001f + 0.01f;
 }
-struct BeamHead { uint2 w; uint32_t cb; };   // the head record and its cell's first ent[] index
+#define BEAM_CHUNK 32
+struct BeamHead { uint2 w; uint32_t cb; };   // the head record and its chunk's first ent[] index
 __device__ __forceinline__ BeamHead beam_head(const BeamGrid& G, int2 cell, int li) {
   BeamHead h;
   h.w = ldg(G.head + li);
@@ -164,12 +168,16 @@ __device__ __forceinline__ int wg_block(const Params& P) {
   return blockIdx.x + P.blk0;
 #endif
 }
-// BeamGrid cell record of the cell holding (x, y): (list base = built cell id * BEAM_NB, the cell's first ent[] index);
+// BeamGrid record of the cell holding (x, y): (list base = built cell id * BEAM_NB, its chunk's first ent[] index);
 // list base -1 outside the built cells
 __device__ __forceinline__ int2 beam_cell(const BeamGrid& G, float x, float y) {
   const float fx = (x - G.ox) * G.inv_cell, fy = (y - G.oy) * G.inv_cell;
-  if (fx >= 0.0f && fy >= 0.0f && fx < (float)G.nx && fy < (float)G.ny) return ldg(G.cell + (int)fy * G.nx + (int)fx);
-  return make_int2(-1, 0);
+  if (!(fx >= 0.0f && fy >= 0.0f && fx < (float)G.nx && fy < (float)G.ny)) return make_int2(-1, 0);
+  const int cx = (int)fx;
+  const int4 ch = ldg(G.chunk + (int)fy * G.nxc + cx / BEAM_CHUNK);
+  const uint32_t bit = 1u << (cx % BEAM_CHUNK), m = (uint32_t)ch.z;
+  if (!(m & bit)) return make_int2(-1, 0);
+  return make_int2(ch.x + __popc(m & (bit - 1u)) * BEAM_NB, ch.y);
 }
 
 #define F32P(P, f) ((P).f32 + (size_t)F32_##f * (P).N)
@@ -2855,8 +2863,9 @@ struct HostTrack {
   HostGrid bp, sn;
   struct {
     BeamGrid g{};
-    std::vector<int2> cell; std::vector<uint16_t> ent; std::vector<uint2> head;
-    int2* d_cell = nullptr; uint16_t* d_ent = nullptr; uint2* d_head = nullptr;
+    std::vector<int4> chunk; std::vector<uint16_t> ent; std::vector<uint2> head;
+    int4* d_chunk = nullptr; uint16_t* d_ent = nullptr; uint2* d_head = nullptr;
+    int nxc = 0;
     size_t entries = 0, nlist = 0, dropped = 0;   // dropped: cells whose continuations overflow the 16-bit offsets
     double build_s = 0.0;
   } beam;
@@ -3022,11 +3031,10 @@ static void build_beams(HostTrack& t, const float cell) {
   while (wb < BEAM_MAX_WALL_BITS && nw > (1 << wb)) ++wb;
   B.g.wbits = wb; B.g.wmask = (1u << wb) - 1u; B.g.cmax = (1u << (16 - wb)) - 1u;
   B.g.kq = (float)(0.0625 * std::pow(62.0 / (double)(B.g.cmax - 1), 2.0));
-  B.cell.assign((size_t)nx * ny, make_int2(-1, 0));
-  std::vector<int> cells;
+  std::vector<int> cells;   // the marked cells, row-major
   if (nw <= (1 << BEAM_MAX_WALL_BITS))   // (more walls than the entries address: no lists, the wall-group walk)
     for (size_t k = 0; k < mark.size(); ++k)
-      if (mark[k]) { B.cell[k] = make_int2((int)cells.size() * BEAM_NB, 0); cells.push_back((int)k); }
+      if (mark[k]) cells.push_back((int)k);
   const int ncell = (int)cells.size();
   const double rc = cell * 0.70710678 + 0.05, two_pi = 2.0 * M_PI, dbin = two_pi / BEAM_NB;
   std::vector<std::vector<uint32_t>> lists((size_t)ncell * BEAM_NB);
@@ -3070,24 +3078,39 @@ static void build_beams(HostTrack& t, const float cell) {
   };
   // per list (cell-major, slot order, beam_slot): the head record holds its first BEAM_HEAD entries (BEAM_PAD filled)
   // and, when the list is longer, 1 + the offset of its continuation -- the remaining entries followed by one BEAM_PAD
-  // sentinel, so a walk needs no list end -- from the cell's first ent[] index (cell record .y).  ent[0] is a sentinel;
-  // BEAM_COOP_PAD sentinels close the array (the chunked and the wave-cooperative walks read past a list's sentinel).
-  // A cell whose continuations would exceed the 16-bit offsets keeps no lists (its rays take the wall-group walk).
-  const size_t nlist = (size_t)ncell * BEAM_NB;
+  // sentinel, so a walk needs no list end -- from its chunk's first ent[] index.  ent[0] is a sentinel; BEAM_COOP_PAD
+  // sentinels close the array (the chunked and the wave-cooperative walks read past a list's sentinel).  A cell whose
+  // continuations would overflow its chunk's 16-bit offsets keeps no lists (its rays take the wall-group walk).
+  B.nxc = (nx + BEAM_CHUNK - 1) / BEAM_CHUNK;
+  B.chunk.assign((size_t)B.nxc * ny, make_int4(-1, 0, 0, 0));
+  std::vector<uint8_t> keep(ncell, 1);
+  B.dropped = 0;
+  for (int c0 = 0, c1; c0 < ncell; c0 = c1) {   // cells of one chunk: consecutive in row-major order
+    const int key = cells[c0] / nx * B.nxc + cells[c0] % nx / BEAM_CHUNK;
+    for (c1 = c0; c1 < ncell && cells[c1] / nx * B.nxc + cells[c1] % nx / BEAM_CHUNK == key; ++c1) {}
+    size_t used = 0;
+    for (int ci = c0; ci < c1; ++ci) {
+      size_t cont = 0;
+      for (int slot = 0; slot < BEAM_NB; ++slot) {
+        const size_t len = lists[(size_t)ci * BEAM_NB + slot].size();
+        if (len > (size_t)BEAM_HEAD) cont += len - BEAM_HEAD + 1;
+      }
+      if (used + cont >= BEAM_CONT_MAX) { keep[ci] = 0; ++B.dropped; } else used += cont;
+    }
+  }
+  const size_t nkept = (size_t)ncell - B.dropped, nlist = nkept * BEAM_NB;
   B.head.assign(nlist, make_uint2(BEAM_PAD | (BEAM_PAD << 16), BEAM_PAD));
   B.ent.assign(1, (uint16_t)BEAM_PAD);
   B.entries = 0;
-  B.dropped = 0;
   std::vector<uint16_t> L16;
+  int id = 0, cur = -1;
+  size_t cb = 0;
   for (int ci = 0; ci < ncell; ++ci) {
-    size_t cont = 0;
-    for (int slot = 0; slot < BEAM_NB; ++slot) {
-      const size_t len = lists[(size_t)ci * BEAM_NB + slot].size();
-      if (len > (size_t)BEAM_HEAD) cont += len - BEAM_HEAD + 1;
-    }
-    int2& rec = B.cell[cells[ci]];
-    if (cont >= BEAM_CONT_MAX) { rec = make_int2(-1, 0); ++B.dropped; continue; }
-    rec.y = (int)B.ent.size();
+    if (!keep[ci]) continue;
+    const int cx = cells[ci] % nx, cy = cells[ci] / nx, key = cy * B.nxc + cx / BEAM_CHUNK;
+    int4& ch = B.chunk[key];
+    if (key != cur) { cur = key; cb = B.ent.size(); ch = make_int4(id * BEAM_NB, (int)cb, 0, 0); }
+    ch.z = (int)((uint32_t)ch.z | (1u << (cx % BEAM_CHUNK)));
     for (int slot = 0; slot < BEAM_NB; ++slot) {
       const auto& L = lists[(size_t)ci * BEAM_NB + beam_bin(slot)];
       B.entries += L.size();
@@ -3098,31 +3121,32 @@ static void build_beams(HostTrack& t, const float cell) {
       for (int k = 0; k < BEAM_HEAD; ++k) h[k] = (size_t)k < L16.size() ? L16[k] : BEAM_PAD;
       h[3] = 0u;
       if (L16.size() > (size_t)BEAM_HEAD) {
-        h[3] = (uint32_t)(B.ent.size() - (size_t)rec.y) + 1u;
+        h[3] = (uint32_t)(B.ent.size() - cb) + 1u;
         B.ent.insert(B.ent.end(), L16.begin() + BEAM_HEAD, L16.end());
         B.ent.push_back((uint16_t)BEAM_PAD);
       }
-      B.head[(size_t)ci * BEAM_NB + slot] = make_uint2(h[0] | (h[1] << 16), h[2] | (h[3] << 16));
+      B.head[(size_t)id * BEAM_NB + slot] = make_uint2(h[0] | (h[1] << 16), h[2] | (h[3] << 16));
     }
+    ++id;
   }
   for (int k = 0; k < (RAY_CHUNK > BEAM_COOP_PAD ? RAY_CHUNK : BEAM_COOP_PAD); ++k) B.ent.push_back((uint16_t)BEAM_PAD);
   if (getenv("NASCAR_VERBOSE"))
     fprintf(stderr, "build_beams: %d walls (%u-bit wall indices, bound codes of %.4f m x c^2), %d cells with lists, %zu "
             "dropped (continuation offsets), %zu entries, heads %.1f MB + continuations %.1f MB\n", nw, B.g.wbits,
-            (double)B.g.kq, ncell, B.dropped, B.entries, 8.0 * B.head.size() / 1e6, 2.0 * B.ent.size() / 1e6);
+            (double)B.g.kq, ncell - (int)B.dropped, B.dropped, B.entries, 8.0 * B.head.size() / 1e6, 2.0 * B.ent.size() / 1e6);
   B.nlist = nlist;
   B.build_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
 }
 static int upload_beams(HostTrack& t) {
   auto& B = t.beam;
   if (B.ent.size() >= 0x7FFFFFF0u) return fail("beam list continuations hold %zu entries (31-bit cell offsets)", B.ent.size());
-  HIPCHK(hipMalloc(&B.d_cell, sizeof(int2) * B.cell.size()));
-  HIPCHK(hipMemcpy(B.d_cell, B.cell.data(), sizeof(int2) * B.cell.size(), hipMemcpyHostToDevice));
+  HIPCHK(hipMalloc(&B.d_chunk, sizeof(int4) * std::max<size_t>(B.chunk.size(), 1)));
+  if (!B.chunk.empty()) HIPCHK(hipMemcpy(B.d_chunk, B.chunk.data(), sizeof(int4) * B.chunk.size(), hipMemcpyHostToDevice));
   HIPCHK(hipMalloc(&B.d_ent, sizeof(uint16_t) * std::max<size_t>(B.ent.size(), 1)));
   if (!B.ent.empty()) HIPCHK(hipMemcpy(B.d_ent, B.ent.data(), sizeof(uint16_t) * B.ent.size(), hipMemcpyHostToDevice));
   HIPCHK(hipMalloc(&B.d_head, sizeof(uint2) * std::max<size_t>(B.head.size(), 1)));
   if (!B.head.empty()) HIPCHK(hipMemcpy(B.d_head, B.head.data(), sizeof(uint2) * B.head.size(), hipMemcpyHostToDevice));
-  B.g.cell = B.d_cell; B.g.ent = B.d_ent; B.g.head = B.d_head;
+  B.g.chunk = B.d_chunk; B.g.nxc = B.nxc; B.g.ent = B.d_ent; B.g.head = B.d_head;
   return 0;
 }
 
@@ -3156,7 +3180,7 @@ struct TrackBuild {
     hipFree(t.d_walls); hipFree(t.d_wfat); hipFree(t.d_segs); hipFree(t.d_prefix);
     hipFree(t.bp.d_start); hipFree(t.bp.d_idx); hipFree(t.bp.d_box); hipFree(t.sn.d_start); hipFree(t.sn.d_idx);
     hipFree(t.d_groups); hipFree(t.d_swall);
-    hipFree(t.beam.d_cell); hipFree(t.beam.d_ent); hipFree(t.beam.d_head);
+    hipFree(t.beam.d_chunk); hipFree(t.beam.d_ent); hipFree(t.beam.d_head);
     if (cur != device) hipSetDevice(cur);
   }
 };
@@ -3515,12 +3539,12 @@ static int upload_track(HostTrack& t, size_t& lds_out) {
             t.sn.g.nx, t.sn.g.ny, t.sn.idx.size(), (double)t.sn.idx.size() / ((double)t.sn.g.nx * t.sn.g.ny));
   if (getenv("NASCAR_VERBOSE"))
     fprintf(stderr, "nascar_add_track: beam grid %dx%d (%.2f m cells), %zu cells with lists (%zu dropped: continuation "
-            "offsets), %zu entries (mean %.2f per list), heads %.1f MB + continuations %.1f MB + cell map %.1f MB, built in "
-            "%.2f s\n", t.beam.g.nx, t.beam.g.ny, 1.0 / (double)t.beam.g.inv_cell, t.beam.nlist / BEAM_NB - t.beam.dropped,
+            "offsets), %zu entries (mean %.2f per list), heads %.1f MB + continuations %.1f MB + cell chunks %.1f MB, built in "
+            "%.2f s\n", t.beam.g.nx, t.beam.g.ny, 1.0 / (double)t.beam.g.inv_cell, t.beam.nlist / BEAM_NB,
             t.beam.dropped, t.beam.entries, (double)t.beam.entries / std::max<size_t>(1, t.beam.nlist),
-            8.0 * t.beam.head.size() / 1e6, 2.0 * t.beam.ent.size() / 1e6, 8.0 * t.beam.cell.size() / 1e6, t.beam.build_s);
-  t.beam.cell.clear(); t.beam.ent.clear(); t.beam.head.clear();
-  t.beam.cell.shrink_to_fit(); t.beam.ent.shrink_to_fit(); t.beam.head.shrink_to_fit();
+            8.0 * t.beam.head.size() / 1e6, 2.0 * t.beam.ent.size() / 1e6, 16.0 * t.beam.chunk.size() / 1e6, t.beam.build_s);
+  t.beam.chunk.clear(); t.beam.ent.clear(); t.beam.head.clear();
+  t.beam.chunk.shrink_to_fit(); t.beam.ent.shrink_to_fit(); t.beam.head.shrink_to_fit();
   lds_out = sizeof(LWall) * t.walls.size();
   return 0;
 }
@@ -3531,7 +3555,7 @@ static int upload_track(HostTrack& t, size_t& lds_out) {
 // per track.  File = magic, format version, the full key (segments, walls, total length, cell size: compared byte for
 // byte on load, so a hash collision can only miss), then the host tables.  Written to a temporary name and renamed; the
 // builders of one key serialise on an flock'ed lock file, so concurrent ranks build each track once and the others load.
-static const uint32_t TRACK_FILE_VERSION = 3;   // 3: 8-byte heads, 16-bit entries, per-track wall bits (round 6)
+static const uint32_t TRACK_FILE_VERSION = 4;   // 4: 8-byte heads, 16-bit entries, per-track wall bits, chunked cell map
 static std::string g_cache_dir;                       // "" = no disk cache (default)
 static int g_retain = 8;                              // builds kept alive after their last handle (most recent first)
 static std::deque<std::shared_ptr<TrackBuild>>* g_retained = new std::deque<std::shared_ptr<TrackBuild>>();
@@ -3570,7 +3594,7 @@ template <class IO, class HT> static void track_io(IO& io, HT& t) {   // the hos
   io.pod(t.total_length); io.pod(t.startline); io.pod(t.has_banking);
   io.pod(t.bp.g); io.vec(t.bp.start); io.vec(t.bp.idx); io.vec(t.bp.box);
   io.pod(t.sn.g); io.vec(t.sn.start); io.vec(t.sn.idx); io.vec(t.sn.box);
-  io.pod(t.beam.g); io.vec(t.beam.cell); io.vec(t.beam.ent); io.vec(t.beam.head);
+  io.pod(t.beam.g); io.vec(t.beam.chunk); io.pod(t.beam.nxc); io.vec(t.beam.ent); io.vec(t.beam.head);
   io.pod(t.beam.entries); io.pod(t.beam.nlist); io.pod(t.beam.dropped); io.pod(t.beam.build_s);
   io.vec(t.groups);
 }
