@@ -131,6 +131,9 @@ struct Params {
   const int* blk_track; const int* blk_env;
   const TrackDev* tracks;
   float4* pose;        // [2][N] sensor hand-off: (x, y, angle, mode) -- see sensor_kernel
+  // [E] this step's auto-reset envs (the logic writes every env's byte): the step's sensor passes read an env's pass-B
+  // pose only when its byte is set, so the pass-B records of the other cars are neither cleared nor read every step
+  uint8_t* reset_env;
   double2* pose_cs;    // [2][N] cos, sin of (double)angle for the ray end points (computed once per car)
   const double2* ray_cs;   // [16] cos, sin of the ray offsets radians(22.5 i) (nascar_rays.h)
   double* ctl;         // [N][4] rule-driver state of the device action sources (policy_car)
@@ -1091,7 +1094,7 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(SENS
   int mode = 0;   // A bits from pose[n], the B bit from pose[N + n]
   if (env >= 0) {
     if (passes & 1) { pa = P.pose[n]; mode = __float_as_int(pa.w) & (PM_A_OBS | PM_A_TERM); }
-    if (passes & 2) { pb = P.pose[P.N + n]; mode |= __float_as_int(pb.w) & PM_B_OBS; }
+    if ((passes & 2) && P.reset_env[env]) { pb = P.pose[P.N + n]; mode |= __float_as_int(pb.w) & PM_B_OBS; }
   }
   PROFS(1);
   unsigned* best = s_best + lc * 16;
@@ -1434,9 +1437,10 @@ __device__ __forceinline__ float ray_walk(const BeamGrid& G, const float4* __res
 #ifndef RAY_COOP_ROUNDS
 #define RAY_COOP_ROUNDS 1024
 #endif
-// lanes per walking ray and round at most 64 >> RAY_COOP_LGMIN (0: up to the whole wave for a lone ray)
+// lanes per walking ray and round at most 64 >> RAY_COOP_LGMIN (0: up to the whole wave for a lone ray; 2: 16 lanes, 32
+// bytes of 16-bit entries per round -- fewer line fills past a short list's sentinel; DESIGN round-6 table)
 #ifndef RAY_COOP_LGMIN
-#define RAY_COOP_LGMIN 0
+#define RAY_COOP_LGMIN 2
 #endif
 template <bool GW>
 __device__ __forceinline__ float ray_walk_coop(const BeamGrid& G, const float4* __restrict__ sw, uint32_t k, float bi, V2 p1,
@@ -1517,7 +1521,9 @@ __device__ __forceinline__ void ray_lane(const Params& P, const TrackDev& T, con
   // one ray per lane: its offset's cos / sin requested first, beside the pose loads (not behind the cell lookup)
   const double2 rk = LPC == 16 ? ldg((const double2*)P.ray_cs + r) : make_double2(0.0, 0.0);
   int mode = 0;
-  if (passes & 2) mode = __float_as_int(P.pose[P.N + n].w) & PM_B_OBS;
+  // a step's passes (A and B) read pass B's record only for this step's auto-reset envs (Params::reset_env); a pass-B-only
+  // call (rt_switch_kernel, the rollout's pass-B loop) names cars whose record it has just written
+  if ((passes & 2) && (!(passes & 1) || P.reset_env[(unsigned)n / (unsigned)P.C])) mode = __float_as_int(P.pose[P.N + n].w) & PM_B_OBS;
   const BeamGrid G = T.beam;
 #pragma unroll 1
   for (int pass = 0; pass < 2; ++pass) {
@@ -1699,7 +1705,7 @@ __device__ __forceinline__ void ray_block_batched(const Params& P, const TrackDe
     for (int j = 0; j < NJ; ++j) {
       const int lc = (t >> 2) + CPR * j, el = lc / C, car = lc - el * C;
       const int env = blk_env_of(P, el, blockIdx.x * P.epb + el);
-      if (env >= 0) ray_lane(P, T, sw, env * C + car, r, obs, nullptr, 2);
+      if (env >= 0 && P.reset_env[env]) ray_lane(P, T, sw, env * C + car, r, obs, nullptr, 2);
     }
   }
 }
@@ -2134,15 +2140,14 @@ __device__ __forceinline__ void logic_run(const Params& P, const TrackDev& T, co
     const bool reset_now = auto_reset && (L.envdone[el] & 1);
     LPROF(6);
     if (terminal_obs) { float* t = terminal_obs + (size_t)n * 38; for (int i = 0; i < 22; ++i) t[i] = o[i]; }
-    // sensor pass B: the reset pose of every auto-reset car (its pass-B values overwrite the pass-A
-    // ones in obs); cleared for every other car
+    // sensor pass B: the reset pose of every auto-reset car (its pass-B values overwrite the pass-A ones in obs); the
+    // env's reset byte tells the step's sensor passes which pass-B records are this step's
+    if (car == 0) P.reset_env[env] = reset_now ? 1 : 0;
     if (reset_now) {
       // an env never reset before (E_CREATED == 0) gets fresh worlds, as in reset_kernel
       car_reset(P, c, n, (L.envdone[el] & 2) != 0, S, T);
       car_obs(c, o);
       set_pose(P, (size_t)P.N + n, c, PM_B_OBS);
-    } else {
-      P.pose[P.N + n] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
     // the lane's 88 bytes of obs[n, 0:22], stored directly (8-byte aligned rows: 11 float2 stores; staging the block's
     // rows in LDS for coalesced stores cost a barrier: per-shard model_logic_kernel 103.8 -> 102.5 us without it)
@@ -3343,9 +3348,10 @@ extern "C" int nascar_create(const NascarConfig* cfg, NascarHandle** out) {
   if (e != hipSuccess) { delete h; return fail("hipMalloc(%zu) failed: %s", o, hipGetErrorString(e)); }
   hipMemset(h->arena, 0, o);
   h->d_ctl = (double*)((char*)h->arena + h->off_ctl);
-  // pose hand-off [2][N] float4
-  if (hipMalloc(&h->d_pose, sizeof(float4) * 2 * N) != hipSuccess) { hipFree(h->arena); delete h; return fail("hipMalloc(pose) failed"); }
-  hipMemset(h->d_pose, 0, sizeof(float4) * 2 * N);
+  // pose hand-off [2][N] float4, then the per-env reset bytes (Params::reset_env)
+  const size_t pose_bytes = sizeof(float4) * 2 * N + ((size_t)E + 15) / 16 * 16;
+  if (hipMalloc(&h->d_pose, pose_bytes) != hipSuccess) { hipFree(h->arena); delete h; return fail("hipMalloc(pose) failed"); }
+  hipMemset(h->d_pose, 0, pose_bytes);
   if (hipMalloc(&h->d_pose_cs, sizeof(double2) * 2 * N) != hipSuccess) { hipFree(h->arena); hipFree(h->d_pose); delete h; return fail("hipMalloc(pose_cs) failed"); }
   hipMemset(h->d_pose_cs, 0, sizeof(double2) * 2 * N);
   HIPCHK(hipMalloc(&h->d_ray_cs, sizeof(h_ray_cs)));
@@ -3881,7 +3887,7 @@ static Params make_params(NascarHandle* h) {
   P.act_n = (float*)(a + h->off_n); P.env_time = (double*)(a + h->off_time); P.env_i32 = (int*)(a + h->off_ei32);
   P.blk_track = h->d_blk_track; P.blk_env = h->d_blk_env; P.tracks = h->d_tracks;
   P.map_identity = h->map_identity; P.one_track = h->one_track;
-  P.pose = h->d_pose; P.pose_cs = h->d_pose_cs; P.ray_cs = h->d_ray_cs; P.ctl = h->d_ctl;
+  P.pose = h->d_pose; P.reset_env = (uint8_t*)(h->d_pose + 2 * (size_t)h->N); P.pose_cs = h->d_pose_cs; P.ray_cs = h->d_ray_cs; P.ctl = h->d_ctl;
   P.vhist = h->d_vhist;
   P.car_contact = h->car_contact;
   return P;
