@@ -393,6 +393,9 @@ class PlumbingEngine:
     def set_rollout_streams(self, streams=4):
         self.rollout_streams = int(streams)
 
+    def set_rollout_pipe(self, sensor_workgroups=0):
+        self.rollout_pipe = int(sensor_workgroups)
+
     def set_car_contact(self, enable=True):
         pass
 
@@ -523,6 +526,8 @@ def timed(step, first, K, world):
     if diag:
         print(f"[diag] K={K} wall {el * 1e3:.3f} ms, gpu span {e0.elapsed_time(e1):.3f} ms, host enqueue "
               f"{t_enq * 1e3:.3f} ms", file=sys.stderr, flush=True)
+    if getattr(step.env, "rollout_pipe", 0) and hasattr(step.env, "rollout_pipe_status") and step.env.rollout_pipe_status():
+        raise RuntimeError("a pipelined rollout gave up on a bounded device wait: the timed steps are not valid")
     return el
 
 
@@ -711,6 +716,8 @@ def main():
                     help="steps per nascar_rollout call for the device action sources (default 50: the sharded rollout, "
                          "bit-identical to the per-step path, which is timed beside it); 0: per-step path only "
                          "(nascar_step_driven per step)")
+    ap.add_argument("--rollout-pipe", type=int, default=0,
+                    help="pipelined rollout with this many sensor workgroups (0: off; BatchedCarEnv.set_rollout_pipe)")
     ap.add_argument("--rollout-streams", type=int, default=None,
                     help="shards (internal streams) of the --rollout path; 0: the fused rollout kernel (default: engine's 4)")
     ap.add_argument("--mixed", action="store_true", help="env e on track e mod 8 of the sorted bundled tracks "
@@ -776,6 +783,8 @@ def main():
     env = make_env()
     if args.rollout_streams is not None:
         env.set_rollout_streams(args.rollout_streams)
+    if args.rollout_pipe:
+        env.set_rollout_pipe(args.rollout_pipe)
     if args.car_contact:
         env.set_car_contact(True)
     gather = None

@@ -156,6 +156,17 @@ int nascar_rollout(NascarHandle* h, int32_t policy, uint64_t seed, int64_t step0
 int nascar_set_rollout_streams(NascarHandle* h, int32_t streams);
 int nascar_get_rollout_streams(NascarHandle* h);
 
+/* Pipelined rollout (no reference counterpart: a scheduling choice with identical results).  sensor_workgroups > 0:
+ * nascar_rollout runs its steps as two persistent kernels -- one workgroup per env group doing the vehicle model, the
+ * Box2D step and the env logic K times, and `sensor_workgroups` sensor workgroups taking each group's sensor work from
+ * a device queue as the group publishes it -- so every group goes on to its next step as soon as its own sensors are
+ * done instead of waiting for the batch's slowest car.  Applies to policies 0, 1, 3 without random tracks, car
+ * contact or obs trajectories (the streams setting applies otherwise); 0 turns it off (default).  Every device wait
+ * is clock-bounded: nascar_rollout_pipe_status waits for `stream` and returns 1 if a pipelined rollout since the
+ * last status call gave up (its results are not valid), 0 if not, -1 on error. */
+int nascar_set_rollout_pipe(NascarHandle* h, int32_t sensor_workgroups);
+int nascar_rollout_pipe_status(NascarHandle* h, void* stream);
+
 /* Workgroup layout (no reference counterpart: the reference loops over envs and cars one at a time,
  * learn/ppo.py:77 SubprocVecEnv and src/car_env.py:567-570; a scheduling choice with identical results).
  * The one-lane-per-car step kernels run 128-lane workgroups of `epb` whole envs each, epb in [1, 128 / C];

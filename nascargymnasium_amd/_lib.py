@@ -88,6 +88,10 @@ def lib():
     L.nascar_set_rollout_streams.restype = ctypes.c_int
     L.nascar_get_rollout_streams.argtypes = [vp]
     L.nascar_get_rollout_streams.restype = ctypes.c_int
+    L.nascar_set_rollout_pipe.argtypes = [vp, i32]
+    L.nascar_set_rollout_pipe.restype = ctypes.c_int
+    L.nascar_rollout_pipe_status.argtypes = [vp, vp]
+    L.nascar_rollout_pipe_status.restype = ctypes.c_int
     L.nascar_set_envs_per_block.argtypes = [vp, i32]
     L.nascar_set_envs_per_block.restype = ctypes.c_int
     L.nascar_get_envs_per_block.argtypes = [vp]
@@ -152,7 +156,7 @@ def lib():
 
 
 EXPORTED = ["nascar_create", "nascar_destroy", "nascar_last_error", "nascar_add_track", "nascar_set_env_tracks",
-            "nascar_reset", "nascar_step", "nascar_step_driven", "nascar_rollout", "nascar_get_info", "nascar_set_perf_history", "nascar_set_car_contact", "nascar_set_rollout_streams", "nascar_get_rollout_streams", "nascar_set_envs_per_block", "nascar_get_envs_per_block", "nascar_set_sensor_lanes", "nascar_set_sensor_block", "nascar_set_beam_cell", "nascar_set_fused_logic", "nascar_get_fused_logic", "nascar_state_bytes", "nascar_get_state",
+            "nascar_reset", "nascar_step", "nascar_step_driven", "nascar_rollout", "nascar_get_info", "nascar_set_perf_history", "nascar_set_car_contact", "nascar_set_rollout_streams", "nascar_get_rollout_streams", "nascar_set_rollout_pipe", "nascar_rollout_pipe_status", "nascar_set_envs_per_block", "nascar_get_envs_per_block", "nascar_set_sensor_lanes", "nascar_set_sensor_block", "nascar_set_beam_cell", "nascar_set_fused_logic", "nascar_get_fused_logic", "nascar_state_bytes", "nascar_get_state",
             "nascar_set_state", "nascar_policy_actions", "nascar_set_step_events", "nascar_set_actor", "nascar_set_actor_precision", "nascar_actor_forward",
             "nascar_debug_sincosf", "nascar_debug_sensors", "nascar_track_draw", "nascar_set_random_tracks",
             "nascar_get_env_tracks", "nascar_vec_post", "nascar_check_actions", "nascar_set_track_cache",

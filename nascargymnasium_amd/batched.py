@@ -95,6 +95,24 @@ class BatchedCarEnv:
     def rollout_streams(self) -> int:
         return int(self.L.nascar_get_rollout_streams(self.h))
 
+    def set_rollout_pipe(self, sensor_workgroups: int = 0):
+        """Pipelined `rollout` (identical results): each workgroup of envs goes on to its next step as soon as its own
+        sensors are done, with the sensors in a second persistent kernel of `sensor_workgroups` workgroups fed from a
+        device queue, so a slow car delays only its own envs (not the batch's step).  0 turns it off.  Used by
+        `rollout` for policies 0 / 1 / 3 without random tracks, car contact or obs trajectories (else the setting of
+        set_rollout_streams applies)."""
+        _lib.check(self.L.nascar_set_rollout_pipe(self.h, int(sensor_workgroups)))
+        self.rollout_pipe = int(sensor_workgroups)
+
+    def rollout_pipe_status(self) -> int:
+        """Waits for the current stream and reports whether a pipelined rollout since the last call gave up on a
+        clock-bounded wait (1; its results are not valid) or not (0)."""
+        import torch
+        r = int(self.L.nascar_rollout_pipe_status(self.h, ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)))
+        if r < 0:
+            _lib.check(r)
+        return r
+
     def set_envs_per_block(self, epb: int = 0):
         """Workgroup layout of the one-lane-per-car step kernels: `epb` whole envs per 128-lane workgroup, in
         [1, 128 // C]; 0 restores the automatic choice.  Results do not depend on it (tests pin every layout the

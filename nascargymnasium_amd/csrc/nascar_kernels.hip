@@ -2366,10 +2366,10 @@ static __device__ void fused_logic_phase(const Params& P, int tid, int el, int c
             terminal_obs);
 }
 #define MODEL_LOGIC_LDS_BYTES (MODEL_CT_LDS_BYTES > sizeof(FusedLogicLDS) ? MODEL_CT_LDS_BYTES : sizeof(FusedLogicLDS))
-__global__ void __launch_bounds__(SBLOCK) __attribute__((amdgpu_waves_per_eu(MODEL_WPE)))
-model_logic_kernel(Params P, const void* actions, int discrete, int want_term, int policy, uint64_t seed, int64_t step,
-                   const float* pobs, float* obs, float* reward, uint8_t* car_flags, uint8_t* env_flags, int auto_reset,
-                   float* terminal_obs) {
+// one step of this workgroup's envs (model_logic_kernel; pipe_step_kernel runs it once per step of its loop)
+__device__ __forceinline__ void model_logic_body(const Params& P, const void* actions, int discrete, int want_term, int policy,
+                                                 uint64_t seed, int64_t step, const float* pobs, float* obs, float* reward,
+                                                 uint8_t* car_flags, uint8_t* env_flags, int auto_reset, float* terminal_obs) {
   const int tid = threadIdx.x, C = P.C;
   const int el = tid / C, car = tid - el * C;
   const int slot = wg_block(P) * P.epb + el;
@@ -2391,6 +2391,13 @@ model_logic_kernel(Params P, const void* actions, int discrete, int want_term, i
                     reason_in, sr);
   PROF(8);
   PROF_RT(9);
+}
+__global__ void __launch_bounds__(SBLOCK) __attribute__((amdgpu_waves_per_eu(MODEL_WPE)))
+model_logic_kernel(Params P, const void* actions, int discrete, int want_term, int policy, uint64_t seed, int64_t step,
+                   const float* pobs, float* obs, float* reward, uint8_t* car_flags, uint8_t* env_flags, int auto_reset,
+                   float* terminal_obs) {
+  model_logic_body(P, actions, discrete, want_term, policy, seed, step, pobs, obs, reward, car_flags, env_flags, auto_reset,
+                   terminal_obs);
 }
 
 // Fused multi-step rollout (nascar_rollout): K env steps of each block's envs in one launch, the actions
@@ -2502,6 +2509,191 @@ rollout_kernel(const Params* __restrict__ Pg, int K, int policy, uint64_t seed, 
     const unsigned long long t3 = __builtin_amdgcn_s_memtime();
     RPROF_ADD(0, t1 - t0); RPROF_ADD(1, t2 - t1); RPROF_ADD(2, t3 - t2); RPROF_ADD(3, 1);
 #endif
+  }
+}
+
+// ------------------------------------------------------------------ pipelined rollout (nascar_set_rollout_pipe)
+// K closed-loop steps with no per-step launch boundary: every step workgroup (pipe_step_kernel, one per env group, the
+// rollout_kernel's model + logic phases) goes on to its next step as soon as its own sensors are done, and the sensors
+// run in a second, high-occupancy persistent kernel (pipe_sensor_kernel, 52 VGPRs) that takes 8-car items from a device
+// ring as the step workgroups publish them.  A slow car (a TOI chain) delays only its own group, not the step of the
+// whole batch.  Hand-offs follow the agent-scope release / acquire form (MI355X_MICROARCH.md, inter-workgroup
+// visibility): every storing wave drains its stores (vmcnt(0)), the workgroup barrier, one lane's release fence, then
+// the flag; the consumer's one lane polls, acquires, and the workgroup barrier precedes every load.  The protocol does
+// not depend on placement or residency: a sensor workgroup serves whatever item it claimed once it is published, and a
+// step workgroup waits only on its own group's items; every wait is clock-bounded and flags the call failed
+// (nascar_rollout_pipe_status) instead of hanging.  Same per-env code in the same order per env: results equal the
+// per-step path bit for bit (tests/test_gpu_rollout.py).
+struct PipeDev {
+  // per XCD x: ring[x * cap .. ] of (seq << 32) | (workgroup << 5 | item) -- the sensor items published by the step
+  // workgroups running on XCD x, served only by the sensor workgroups on XCD x, so every hand-off stays inside one
+  // XCD's L2 (the per-XCD L2s are not coherent with each other)
+  unsigned long long* ring;
+  // ctr[x * 32 + 0] items claimed, [x * 32 + 1] slots reserved, [x * 32 + 2] items expected on XCD x (per call);
+  // ctr[256] step workgroups registered (per call), ctr[288] sticky error flag
+  unsigned* ctr;
+  unsigned* sdone;            // [nblocks] sensor items completed per step workgroup (per call)
+  unsigned seq, cap;          // this call's ring tag; slots per XCD (all of the call's items)
+  int sub, nb;                // PIPE_CARS-car sensor items per step workgroup; step workgroups
+  int dbg;                    // NASCAR_PIPE_DEBUG: printf milestones of the first workgroups
+  unsigned long long timeout; // s_memrealtime ticks (100 MHz) a wait may last without progress (NASCAR_PIPE_TIMEOUT_MS)
+};
+#define PIPE_ERR 288
+#define PIPE_REG 256
+__device__ __forceinline__ unsigned pipe_ld(const unsigned* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+__device__ __forceinline__ void pipe_fail(const PipeDev& Q) { __hip_atomic_store(Q.ctr + PIPE_ERR, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+// agent-scope fences; NASCAR_PIPE_DEBUG bit 2 (value 4) makes them system-scope (diagnostic)
+__device__ __forceinline__ void pipe_acquire(const PipeDev& Q) {
+  if (Q.dbg & 4) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+  else __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the invalidate completes asynchronously: wait for it
+}
+// producer side: the producer and the consumer share the XCD's L2 (per-XCD rings), and every storing wave has drained
+// its stores into it (vmcnt(0)) before this, so the agent-scope release's L2 write-back (buffer_wbl2, which writes back
+// the whole XCD L2's dirty lines, ~2-7 us) is not needed; NASCAR_PIPE_DEBUG bit 2 (4) keeps a system-scope release
+__device__ __forceinline__ void pipe_release(const PipeDev& Q) {
+  if (Q.dbg & 4) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+__device__ __forceinline__ unsigned pipe_xcc() { return __builtin_amdgcn_s_getreg((3 << 11) | 20) & 7u; }   // HW_REG_XCC_ID
+
+// the step body as a call: allocated like model_logic_kernel on its own, not merged with the loop's live values
+// (Params from the launch's device copy through a constant-address-space pointer, as rollout_kernel's phases: a
+// by-value kernel argument whose address is taken would be copied to private memory)
+static __device__ __attribute__((noinline)) void pipe_step_body(ParamsK Pk, int policy, uint64_t seed, int64_t step,
+                                                                float* obs, float* reward, uint8_t* car_flags,
+                                                                uint8_t* env_flags, int auto_reset) {
+  const Params& P = *(const Params*)Pk;
+  model_logic_body(P, nullptr, 0, 0, policy, seed, step, obs, obs, reward, car_flags, env_flags, auto_reset, nullptr);
+}
+__global__ void __launch_bounds__(SBLOCK) __attribute__((amdgpu_waves_per_eu(MODEL_WPE)))
+pipe_step_kernel(const Params* __restrict__ Pg, PipeDev Q, int K, int policy, uint64_t seed, int64_t step0, float* obs,
+                 float* reward, uint8_t* car_flags, uint8_t* env_flags, int auto_reset, int traj) {
+  ParamsK Pk = (ParamsK)Pg;
+  const Params& P = *Pg;
+  const int b = wg_block(P), tid = threadIdx.x;
+  const unsigned x = pipe_xcc();
+  __shared__ int s_go;
+  if (tid == 0) {   // this workgroup's items of the call go to its XCD's ring
+    __hip_atomic_fetch_add(Q.ctr + x * 32 + 2, (unsigned)(Q.sub * K), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_fetch_add(Q.ctr + PIPE_REG, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (Q.dbg && b < 8) printf("pipe A b %d blockIdx %d xcc %u\n", b, (int)blockIdx.x, x);
+  }
+#pragma unroll 1
+  for (int k = 0; k < K; ++k) {
+    if (k > 0) {   // this group's sensors of step k - 1 done (the obs its driver reads, the state it steps)
+      if (tid == 0) {
+        const unsigned want = (unsigned)Q.sub * (unsigned)k;
+        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+        int ok = 1;
+        while (pipe_ld(Q.sdone + b) < want) {
+          if (pipe_ld(Q.ctr + PIPE_ERR) || __builtin_amdgcn_s_memrealtime() - t0 > Q.timeout) { pipe_fail(Q); ok = 0; break; }
+          __builtin_amdgcn_s_sleep(2);
+        }
+        pipe_acquire(Q);
+        s_go = ok;
+      }
+      __syncthreads();
+      if (Q.dbg && tid == 0 && b < 2) printf("pipe A b %d k %d go %d sdone %u\n", b, k, s_go, pipe_ld(Q.sdone + b));
+      if (!__builtin_amdgcn_readfirstlane(s_go)) return;   // (wave-uniform, see pipe_sensor_kernel)
+    }
+    if (Q.dbg && tid == 0 && b < 2) printf("pipe A b %d k %d step\n", b, k);
+    const size_t ko = traj ? (size_t)k : 0;
+    pipe_step_body(Pk, policy, seed, step0 + k, obs, reward + ko * P.N, car_flags ? car_flags + ko * P.N : nullptr,
+                   env_flags ? env_flags + ko * P.E : nullptr, auto_reset);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's stores done before the barrier and the release
+    __syncthreads();
+    if ((Q.dbg & 8) && tid == 0 && b < 2) {
+      const int n0 = blk_env_of(P, 0, b * P.epb) * P.C;
+      printf("pipe A b %d k %d car %d pose %f %f %f w %x\n", b, k, n0, P.pose[n0].x, P.pose[n0].y, P.pose[n0].z, __float_as_int(P.pose[n0].w));
+      printf("pipe A b %d k %d car %d pose %f %f %f w %x\n", b, k, n0 + 33, P.pose[n0 + 33].x, P.pose[n0 + 33].y, P.pose[n0 + 33].z, __float_as_int(P.pose[n0 + 33].w));
+    }
+    if (tid == 0) {   // publish the group's sensor items of step k
+      pipe_release(Q);
+      const unsigned s0 = __hip_atomic_fetch_add(Q.ctr + x * 32 + 1, (unsigned)Q.sub, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      unsigned long long* R = Q.ring + (size_t)x * Q.cap;
+      for (int j = 0; j < Q.sub; ++j)
+        __hip_atomic_store(R + s0 + j, ((unsigned long long)Q.seq << 32) | (unsigned)(b << 5 | j), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+      if (Q.dbg && b < 2) printf("pipe A b %d k %d published at %u\n", b, k, s0);
+    }
+  }
+}
+
+// 16 lanes per car, 4 cars per one-wave workgroup (so no workgroup barrier: the wave's own drained stores, then lane
+// 0's release), walls read from the track's global image (ray_sensor_kernel's default path); loops over claimed items
+// until the call's last.  The claimed item is read as a wave-uniform value (readfirstlane), so the loop's exit is a
+// scalar branch.
+#define PIPE_CARS 4
+// one item's 4 cars, as a call: the loop around it keeps only a few values, and the walk's divergent control flow
+// reconverges at the return (inlined into the item loop, lanes 1-15 of each car stayed off after the first item)
+static __device__ __attribute__((noinline)) void pipe_sensor_item(ParamsK Pk, unsigned item, float* obs, int passes,
+                                                                  int dbg) {
+  const Params& P = *(const Params*)Pk;
+  const int lane = threadIdx.x & 63, lc = lane / 16, r = lane % 16, C = P.C;
+  const int b = (int)(item >> 5), slot = (int)(item & 31u) * PIPE_CARS + lc;
+  if (slot < P.epb * C) {
+    const int el = slot / C, car = slot - el * C;
+    const int env = blk_env_of(P, el, b * P.epb + el);
+    const TrackDev& T = P.tracks[blk_track_of(P, b)];
+    if (env >= 0) {
+      if (dbg & 2) ray_lane<16, true, false>(P, T, T.swall, env * C + car, r, obs, nullptr, passes);
+      else ray_lane<16, true>(P, T, T.swall, env * C + car, r, obs, nullptr, passes);
+    }
+  }
+}
+// claiming an item and completing one as calls too: every lane enters and leaves each call with the whole wave
+// active, and the item comes back wave-uniform.  (With the lane-0 regions inlined into the loop, the first item of a
+// workgroup was walked right and later ones with only one lane of each car writing: the structurised loop did not
+// restore the full exec mask before the next item's walk.)
+static __device__ __attribute__((noinline)) unsigned pipe_claim(const PipeDev& Q, unsigned x) {
+  unsigned item = 0xFFFFFFFFu;   // none left (or the call failed)
+  if ((threadIdx.x & 63) == 0) {
+    unsigned s = 0xFFFFFFFFu;
+    unsigned* H = Q.ctr + x * 32;
+    unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    // take the next slot of this XCD's ring (a queue in publication order); past the XCD's expected items (once every
+    // step workgroup has registered them) there is nothing more to take
+    const unsigned h = __hip_atomic_fetch_add(H, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (;;) {
+      if (h < pipe_ld(H + 1)) { s = h; break; }   // reserved: its item is (being) published
+      if (pipe_ld(Q.ctr + PIPE_REG) == (unsigned)Q.nb && h >= pipe_ld(H + 2)) break;
+      if (pipe_ld(Q.ctr + PIPE_ERR) || __builtin_amdgcn_s_memrealtime() - t0 > Q.timeout) { pipe_fail(Q); break; }
+      __builtin_amdgcn_s_sleep(4);
+    }
+    if (s != 0xFFFFFFFFu) {
+      const unsigned long long* R = Q.ring + (size_t)x * Q.cap;
+      t0 = __builtin_amdgcn_s_memrealtime();
+      for (;;) {
+        const unsigned long long v = __hip_atomic_load(R + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if ((unsigned)(v >> 32) == Q.seq) { item = (unsigned)v; break; }
+        if (pipe_ld(Q.ctr + PIPE_ERR) || __builtin_amdgcn_s_memrealtime() - t0 > Q.timeout) { pipe_fail(Q); break; }
+        __builtin_amdgcn_s_sleep(2);
+      }
+      pipe_acquire(Q);
+    }
+  }
+  return __builtin_amdgcn_readfirstlane(item);
+}
+static __device__ __attribute__((noinline)) void pipe_done(const PipeDev& Q, int b) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the wave's obs stores done before the release
+  if ((threadIdx.x & 63) == 0) {
+    pipe_release(Q);
+    __hip_atomic_fetch_add(Q.sdone + b, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RSENSOR_WPE)))
+pipe_sensor_kernel(const Params* __restrict__ Pg, PipeDev Q, float* obs, int passes) {
+  ParamsK Pk = (ParamsK)Pg;
+  const unsigned x = pipe_xcc();
+#pragma unroll 1
+  for (;;) {
+    const unsigned item = pipe_claim(Q, x);
+    if (item == 0xFFFFFFFFu) return;
+    pipe_sensor_item(Pk, item, obs, passes, Q.dbg);
+    if (Q.dbg & 16) pipe_sensor_item(Pk, item, obs, passes, Q.dbg);
+    pipe_done(Q, (int)(item >> 5));
+    if (Q.dbg & 32) return;
   }
 }
 
@@ -3236,6 +3428,12 @@ struct NascarHandle {
   hipEvent_t ev_fork = nullptr;
   std::vector<hipEvent_t> ev_join;
   float* d_ro_act = nullptr;        // [N][2] actions of a policy-2 (SAC actor) sharded rollout
+  // pipelined rollout (nascar_set_rollout_pipe): sensor workgroups of pipe_sensor_kernel (0: off), the item ring,
+  // counters (claimed, published, sticky error, pad) and per-workgroup completion counts
+  int ro_pipe = 0;
+  unsigned long long* d_pipe_ring = nullptr; size_t pipe_cap = 0;
+  unsigned* d_pipe_ctr = nullptr; unsigned* d_pipe_sdone = nullptr; size_t pipe_nb = 0;
+  unsigned pipe_seq = 0;
   hipEvent_t step_ev[4] = {nullptr, nullptr, nullptr, nullptr};   // nascar_set_step_events (profiling)
   // prepare(): capacities of the track table / block map buffers, pinned staging of their stream-ordered uploads
   size_t cap_tracks = 0, cap_blocks = 0, cap_blk_env = 0;
@@ -3372,6 +3570,7 @@ extern "C" void nascar_destroy(NascarHandle* h) {
   if (!h) return;
   hipFree(h->d_vhist);
   hipFree(h->arena); hipFree(h->d_pose); hipFree(h->d_pose_cs); hipFree(h->d_ray_cs); hipFree(h->d_actor); hipFree(h->d_actor32); hipFree(h->d_params);
+  hipFree(h->d_pipe_ring); hipFree(h->d_pipe_ctr); hipFree(h->d_pipe_sdone);
   {   // the shared track builds are released (and freed by the last holder) under the cache lock
     std::lock_guard<std::mutex> lk(g_track_mu);
     h->tracks.clear();
@@ -4192,6 +4391,102 @@ static int rollout_sharded(NascarHandle* h, int S, int32_t policy, uint64_t seed
   return rc ? rc : jrc;
 }
 
+// Pipelined rollout (see pipe_step_kernel): the step kernel on the caller's stream, the sensor kernel on the first
+// shard stream, both launched after the per-call counter reset and joined into the caller's stream at the end.  Calls
+// are cut into chunks of at most PIPE_CHUNK steps (the ring holds one chunk's items).
+#define PIPE_CHUNK 64
+static int rollout_pipe(NascarHandle* h, int policy, uint64_t seed, int64_t step0, int steps, float* obs, float* reward,
+                        uint8_t* car_flags, uint8_t* env_flags, int auto_reset, int traj, hipStream_t stream) {
+  const int nb = h->nblocks, sub = (h->epb * h->C + PIPE_CARS - 1) / PIPE_CARS;
+  if (sub > 32) return fail("pipelined rollout: at most %d cars per step workgroup", 32 * PIPE_CARS);
+  const size_t per_step = (size_t)nb * sub, chunk = std::min<size_t>(PIPE_CHUNK, std::max<size_t>(1, 0x7FFFFFFFu / per_step));
+  const size_t cap = per_step * std::min<size_t>(chunk, (size_t)steps);   // slots per XCD: a chunk's items
+  if (h->pipe_cap < cap) {
+    hipFree(h->d_pipe_ring); h->d_pipe_ring = nullptr; h->pipe_cap = 0;
+    HIPCHK(hipMalloc(&h->d_pipe_ring, sizeof(unsigned long long) * 8 * cap));
+    HIPCHK(hipMemsetAsync(h->d_pipe_ring, 0, sizeof(unsigned long long) * 8 * cap, stream));   // tag 0 is never a call's
+    h->pipe_cap = cap;
+  }
+  if (!h->d_pipe_ctr) {
+    HIPCHK(hipMalloc(&h->d_pipe_ctr, 320 * sizeof(unsigned)));
+    HIPCHK(hipMemsetAsync(h->d_pipe_ctr, 0, 320 * sizeof(unsigned), stream));
+  }
+  if (h->pipe_nb < (size_t)nb) {
+    hipFree(h->d_pipe_sdone); h->d_pipe_sdone = nullptr; h->pipe_nb = 0;
+    HIPCHK(hipMalloc(&h->d_pipe_sdone, sizeof(unsigned) * nb));
+    h->pipe_nb = nb;
+  }
+  if (h->sub_stream.empty() || !h->ev_fork) {   // one extra stream (the first shard stream) and its join event
+    int cur = 0;
+    HIPCHK(hipGetDevice(&cur));
+    if (cur != h->cfg.device) HIPCHK(hipSetDevice(h->cfg.device));
+    bool ok = true;
+    if (h->sub_stream.empty()) {
+      hipStream_t st; hipEvent_t ev;
+      ok = hipStreamCreateWithFlags(&st, hipStreamNonBlocking) == hipSuccess;
+      if (ok && hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) { hipStreamDestroy(st); ok = false; }
+      if (ok) { h->sub_stream.push_back(st); h->ev_join.push_back(ev); }
+    }
+    if (ok && !h->ev_fork) ok = hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming) == hipSuccess;
+    if (cur != h->cfg.device) hipSetDevice(cur);
+    if (!ok) return fail("creating the pipelined rollout's sensor stream failed");
+  }
+  const Params P = make_params(h);
+  if (!h->d_params) {
+    HIPCHK(hipMalloc(&h->d_params, sizeof(Params)));
+    memset(&h->params_up, 0, sizeof(Params));
+  }
+  if (!h->params_valid || memcmp(&h->params_up, &P, sizeof(Params)) != 0) {   // stream-ordered upload when changed
+    h->params_up = P; h->params_valid = true;
+    HIPCHK(hipMemcpyAsync(h->d_params, &h->params_up, sizeof(Params), hipMemcpyHostToDevice, stream));
+  }
+  hipStream_t ss = h->sub_stream[0];
+  const size_t NC = (size_t)h->N, E = (size_t)h->E;
+  for (int k0 = 0; k0 < steps; k0 += (int)chunk) {
+    const int kc = (int)std::min<size_t>(chunk, (size_t)(steps - k0));
+    HIPCHK(hipMemsetAsync(h->d_pipe_ctr, 0, (PIPE_REG + 1) * sizeof(unsigned), stream));   // the per-call counters (not the error)
+    HIPCHK(hipMemsetAsync(h->d_pipe_sdone, 0, sizeof(unsigned) * nb, stream));
+    if (++h->pipe_seq == 0) h->pipe_seq = 1;
+#ifdef NASCAR_AB_KNOBS   // diagnostic builds (tools/mklib.sh): printf milestones, variants, a shorter bound
+    static const int dbg = getenv("NASCAR_PIPE_DEBUG") ? atoi(getenv("NASCAR_PIPE_DEBUG")) : 0;
+    static const unsigned long long tmo = 100000ull * (unsigned long long)(getenv("NASCAR_PIPE_TIMEOUT_MS") ? atoi(getenv("NASCAR_PIPE_TIMEOUT_MS")) : 2000);
+#else
+    const int dbg = 0;
+    const unsigned long long tmo = 100000ull * 2000;   // 2 s without progress fails the call
+#endif
+    PipeDev Q{h->d_pipe_ring, h->d_pipe_ctr, h->d_pipe_sdone, h->pipe_seq, (unsigned)h->pipe_cap, sub, nb, dbg, tmo};
+    // the sensor stream starts after the resets, not after the step kernel (which waits on it)
+    HIPCHK(hipEventRecord(h->ev_fork, stream));
+    HIPCHK(hipStreamWaitEvent(ss, h->ev_fork, 0));
+    const size_t ko = traj ? (size_t)k0 : 0;
+    hipLaunchKernelGGL(pipe_step_kernel, dim3(nb), dim3(SBLOCK), MODEL_LOGIC_LDS_BYTES, stream, (const Params*)h->d_params, Q,
+                       kc, policy, seed,
+                       step0 + k0, obs, reward + ko * NC, car_flags ? car_flags + ko * NC : nullptr,
+                       env_flags ? env_flags + ko * E : nullptr, auto_reset, traj);
+    HIPCHK(hipGetLastError());
+    hipLaunchKernelGGL(pipe_sensor_kernel, dim3(h->ro_pipe), dim3(64), 0, ss, (const Params*)h->d_params, Q, obs,
+                       auto_reset ? 3 : 1);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(h->ev_join[0], ss));
+    HIPCHK(hipStreamWaitEvent(stream, h->ev_join[0], 0));
+  }
+  return 0;
+}
+extern "C" int nascar_set_rollout_pipe(NascarHandle* h, int32_t sensor_workgroups) {
+  if (!h) return fail("null argument");
+  if (sensor_workgroups < 0 || sensor_workgroups > 65536) return fail("sensor workgroups must be in [0, 65536] (got %d)", sensor_workgroups);
+  h->ro_pipe = sensor_workgroups;
+  return 0;
+}
+extern "C" int nascar_rollout_pipe_status(NascarHandle* h, void* stream) {
+  if (!h) return fail("null argument");
+  if (!h->d_pipe_ctr) return 0;
+  unsigned err = 0;
+  HIPCHK(hipStreamSynchronize((hipStream_t)stream));
+  HIPCHK(hipMemcpy(&err, h->d_pipe_ctr + PIPE_ERR, sizeof(unsigned), hipMemcpyDeviceToHost));
+  if (err) HIPCHK(hipMemset(h->d_pipe_ctr + PIPE_ERR, 0, sizeof(unsigned)));
+  return err ? 1 : 0;
+}
 extern "C" int nascar_get_rollout_streams(NascarHandle* h) { return h ? h->ro_streams : -1; }
 extern "C" int nascar_set_rollout_streams(NascarHandle* h, int32_t streams) {
   if (!h) return fail("null argument");
@@ -4215,6 +4510,9 @@ extern "C" int nascar_rollout(NascarHandle* h, int32_t policy, uint64_t seed, in
   if (steps == 0) return 0;
   h->pristine = false;
   if (prepare(h, (hipStream_t)stream)) return -1;
+  if (h->ro_pipe > 0 && policy != 2 && !h->rt_on && !h->car_contact && !(traj & NASCAR_TRAJ_OBS))
+    return rollout_pipe(h, policy, seed, step0, steps, obs, reward, car_flags, env_flags, auto_reset, traj,
+                        (hipStream_t)stream);
   if (h->ro_streams > 0)
     return rollout_sharded(h, h->ro_streams, policy, seed, step0, steps, obs, reward, car_flags, env_flags, auto_reset,
                            traj, (hipStream_t)stream);

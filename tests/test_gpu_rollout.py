@@ -1,4 +1,5 @@
-"""nascar_rollout (sharded over internal streams, the default, and the fused multi-step kernel) against the per-step path: K x (nascar_policy_actions +
+"""nascar_rollout (sharded over internal streams, the default, the fused multi-step kernel and the pipelined pair of
+persistent kernels) against the per-step path: K x (nascar_policy_actions +
 nascar_step with auto-reset) from the same state must give the same per-step rewards / car flags / env flags,
 the same final observation and the same final engine state, bit for bit."""
 import os
@@ -27,7 +28,7 @@ def _per_step(env, policy, seed, step0, K):
     return torch.stack(R), torch.stack(CF), torch.stack(EF)
 
 
-@pytest.mark.parametrize("streams", [4, 0])        # sharded rollout (default) / fused rollout kernel
+@pytest.mark.parametrize("streams", [4, 0, -1])    # sharded rollout (default) / fused rollout kernel / pipelined rollout
 @pytest.mark.parametrize("tracks,E,C,policy,warm,K,epb", [
     (["daytona.track"], 48, 10, 3, 600, 900, 12),      # the bench workload and layout: noisy driver, contacts
     (["daytona.track"], 16, 2, 1, 0, 400, None),       # rule driver from reset
@@ -45,7 +46,10 @@ def test_rollout_equals_per_step(tracks, E, C, policy, warm, K, epb, streams):
     rollout at `epb` envs per workgroup: the same results whatever the schedule and the layout"""
     rol = policy == 0
     a, b = _engine(tracks, E, C, rol), _engine(tracks, E, C, rol, envs_per_block=epb)
-    b.set_rollout_streams(streams if E != 500 or streams == 0 else 3)
+    if streams == -1:
+        b.set_rollout_pipe(512)
+    else:
+        b.set_rollout_streams(streams if E != 500 or streams == 0 else 3)
     a.reset()
     if warm:                                    # leave the reset state first (cars spread, contacts active)
         a.rollout(policy, warm, seed=5, step0=0, auto_reset=True)
@@ -54,6 +58,8 @@ def test_rollout_equals_per_step(tracks, E, C, policy, warm, K, epb, streams):
     R, CF, EF = _per_step(a, policy, 5, warm, K)
     obs_b, Rb, CFb, EFb = b.rollout(policy, K, seed=5, step0=warm, auto_reset=True, trajectory=True)
     torch.cuda.synchronize()
+    if streams == -1:
+        assert b.rollout_pipe_status() == 0
     for k in range(K):
         assert torch.equal(R[k], Rb[k]), f"reward differs at step {k}"
         assert torch.equal(CF[k], CFb[k]), f"car flags differ at step {k}"
